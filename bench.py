@@ -1,0 +1,203 @@
+"""Headline benchmark: training steps/s at batch 2^18 on data/config_hash.json (HashGrid L16 F2
+log2T15 s1.5 + FullyFusedMLP 64x2, RelativeL2, Adam) -- BASELINE.json `metric`.
+
+One step = Trainer::training_step over one 2^18-point batch resident in HBM: fused grid-encode +
+MLP fwd + loss + MLP bwd + weight gradients, grid backward, reductions, Adam (and, with N>1 ranks,
+the RCCL all-reduce of the fp32 gradient sums). Synthetic data: uniform positions, analytic RGB
+targets (no image I/O). Multi-GPU is data parallel, weak scaling: every rank trains on its own
+2^18 batch per step; `value` counts 2^18-sample training steps completed by all ranks per second.
+
+  python bench.py [--gpus N --steps K --warmup W]
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+      --master-port P bench.py --gpus N --steps K --warmup W
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "neuralbtf-tiny-cuda-nn_amd")
+for _p in (REPO, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+# MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md): dense fp16 MFMA, HBM3E
+PEAK_FP16_TFLOPS = 2500.0
+PEAK_HBM_GBS = 8000.0
+# Algorithmic work per training sample (config_hash: W64 H2 in32 out_p16 D2 L16 F2)
+MLP_TRAIN_FLOP_PER_SAMPLE = 43008
+GRID_BWD_BYTES_PER_SAMPLE = 584
+PHASES = ["fused_grid_mlp_fwd_loss_bwd", "wgrad_reduce", "grid_bwd", "grid_reduce", "loss_sum", "adam"]
+
+
+def rgb_field_torch(pos):
+    import torch
+    x, y = pos[:, 0].double(), pos[:, 1].double()
+    r = 0.5 + 0.5 * torch.sin(9.0 * x) * torch.cos(7.0 * y)
+    g = 0.5 + 0.4 * torch.sin(23.0 * x * y + 1.0)
+    b = 0.5 + 0.3 * torch.cos(31.0 * x) * torch.sin(17.0 * y) + 0.1 * (torch.floor(x * 40) % 2)
+    return torch.stack([r, g, b], dim=1).float().contiguous()
+
+
+def cpu_baseline(cfg, budget_s=12.0):
+    """CPU restatement (oracle/, fp32 OpenMP) timed on the host: `port` baseline."""
+    import numpy as np
+    from oracle import oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads = min(threads, 16)
+    B = 1 << 16
+    om = O.OracleModel(cfg, 2, 3, seed=1337)
+    r = O.pcg32(1337)
+    pos = O.generate_uniform(r, 2 * B).reshape(B, 2)
+    tgt = np.stack([0.5 + 0.5 * np.sin(9 * pos[:, 0]), pos[:, 1], pos[:, 0] * pos[:, 1]], axis=1).astype(np.float32)
+    om.train_step(pos, tgt, n_threads=threads)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        om.train_step(pos, tgt, n_threads=threads)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or n >= 200:
+            break
+    steps_per_s_2p16 = n / el
+    return {
+        "value": steps_per_s_2p16 * (B / float(1 << 18)),
+        "unit": "training steps/s (2^18-sample batch equivalent)",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{n} oracle training steps of config_hash.json at B=2^16 on {threads} host threads "
+                  f"({el:.1f} s, {steps_per_s_2p16:.3f} steps/s at 2^16, scaled x1/4 to 2^18 samples/step)",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch-log2", type=int, default=18)
+    ap.add_argument("--config", default=os.path.join(REPO, "tests", "golden", "config_hash.json"))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from tinycudann import Trainer
+    import ctypes
+    from tinycudann import _lib as L
+
+    cfg = json.load(open(args.config))
+    B = 1 << args.batch_log2
+    trainer = Trainer(2, 3, cfg, seed=1337)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(1337 + 7919 * rank)
+    NB = 4
+    batches = []
+    for _ in range(NB):
+        pos = torch.rand(B, 2, device="cuda", generator=g).contiguous()
+        batches.append((pos, rgb_field_torch(pos)))
+
+    grads = None
+    if world > 1:
+        grads = trainer.gradients_fp32()
+        trainer.set_gradient_scale(1.0 / world)
+
+    def step(i):
+        pos, tgt = batches[i % NB]
+        if world == 1:
+            trainer.training_step(pos, tgt, run_optimizer=True)
+        else:
+            trainer.training_step(pos, tgt, run_optimizer=False)
+            dist.all_reduce(grads)
+            trainer.optimizer_step()
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    if not args.no_profile:
+        L.check(L.lib().tcnn_trainer_profile_begin(trainer.h))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+
+    phase_ms = None
+    if not args.no_profile:
+        ms = (ctypes.c_double * 6)()
+        nst = ctypes.c_uint32(0)
+        L.check(L.lib().tcnn_trainer_profile_end(trainer.h, ms, 6, ctypes.byref(nst)))
+        phase_ms = {PHASES[k]: ms[k] for k in range(6)}
+
+    loss = trainer.loss()
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    units = world * args.steps
+    value = units / elapsed
+    res = {
+        "metric": "training steps/sec at batch=2^18, config_hash.json (HashGrid+64-wide MLP)",
+        "value": value,
+        "unit": "training steps/s (2^18-sample batches, summed over ranks)",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1000.0 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp16 storage / fp32 MFMA accumulate",
+        "data": "synthetic (uniform positions, analytic RGB targets), random-init weights (Trainer seed 1337)",
+        "config": {
+            "workload": "mlp_learning_an_image training step, data/config_hash.json as-is "
+                        "(HashGrid L16 F2 log2T15 s1.5 base16 + FullyFusedMLP W64 H2 ReLU, RelativeL2, Adam)",
+            "global_batch": B * world, "per_gpu_batch": B, "parallelism": f"dp{world}",
+        },
+        "samples_per_s": value * B,
+        "final_loss": loss,
+    }
+    if phase_ms:
+        res["phase_ms"] = phase_ms
+        t_fused = phase_ms[PHASES[0]]
+        t_gbwd = phase_ms[PHASES[2]]
+        if t_fused >= t_gbwd:
+            achieved = MLP_TRAIN_FLOP_PER_SAMPLE * B / (t_fused * 1e-3) / 1e12
+            res["roofline"] = {"kernel": "k_fused_train_grid", "bound": "mfma", "achieved": achieved,
+                               "peak": PEAK_FP16_TFLOPS, "unit": "TFLOP/s", "frac": achieved / PEAK_FP16_TFLOPS,
+                               "traffic": None}
+        else:
+            achieved = GRID_BWD_BYTES_PER_SAMPLE * B / (t_gbwd * 1e-3) / 1e9
+            res["roofline"] = {"kernel": "k_grid_bwd_sliced", "bound": "hbm", "achieved": achieved,
+                               "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": None}
+    if world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(cfg)
+    print(json.dumps(res))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,130 @@
+/*
+ * tcnn_mi355x.h -- C-ABI drop-in boundary of the MI355X (gfx950) hash-grid + fully-fused-MLP engine.
+ *
+ * Plain pointers and sizes only (no torch / C++ types). All data pointers are DEVICE pointers owned
+ * by the caller unless stated otherwise; `stream` is a hipStream_t (NULL = default stream).
+ * Every entry point catches C++ exceptions at the boundary and reports failure through its return
+ * value (0 = success, nonzero / NULL = failure); the message is available from tcnn_last_error()
+ * (thread-local). This mirrors the reference's exception behaviour (pybind maps them to
+ * RuntimeError, reference bindings/torch/tinycudann/bindings.cpp).
+ *
+ * Two layers are exposed, each replacing one reference interface:
+ *   (1) tcnn_module_*  -- the runtime FFI tcnn::cpp::Module (reference include/tiny-cuda-nn/cpp_api.h:50-117,
+ *                         src/cpp_api.cu:30-167) that the PyTorch extension / NeuralBTF caller binds.
+ *   (2) tcnn_trainer_* -- create_from_config() + Trainer::training_step / loss / inference
+ *                         (reference include/tiny-cuda-nn/config.h:46-63, trainer.h:47-361,
+ *                         object.h:147-179) used by mlp_learning_an_image.
+ *
+ * Matrix conventions (reference common.h:157-167): input fp32 [n x n_input_dims] row-major
+ * (= CM [n_input_dims x n]); outputs / params are fp16 when precision is Fp16; n must be a multiple
+ * of tcnn_batch_size_granularity() (256).
+ */
+#ifndef TCNN_MI355X_H
+#define TCNN_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TCNN_PRECISION_FP32 0 /* tcnn::cpp::Precision::Fp32 (cpp_api.h:75-78) */
+#define TCNN_PRECISION_FP16 1 /* tcnn::cpp::Precision::Fp16 */
+
+typedef struct tcnn_module tcnn_module;   /* tcnn::cpp::Module* (cpp_api.h:86-112) */
+typedef struct tcnn_context tcnn_context; /* tcnn::cpp::Context (cpp_api.h:82-84) */
+typedef struct tcnn_trainer tcnn_trainer; /* TrainableModel {loss, optimizer, network, trainer} (config.h:46-51) */
+
+/* ---- library / device (cpp_api.h:61-80; src/cpp_api.cu:41-62) ---- */
+const char* tcnn_last_error(void);
+const char* tcnn_version(void);
+uint32_t tcnn_batch_size_granularity(void);       /* cpp::batch_size_granularity() */
+int tcnn_cuda_device(void);                       /* cpp::cuda_device() */
+int tcnn_set_cuda_device(int device);             /* cpp::set_cuda_device() */
+void tcnn_free_temporary_memory(void);            /* cpp::free_temporary_memory() */
+int tcnn_has_networks(void);                      /* cpp::has_networks() */
+float tcnn_default_loss_scale(int precision);     /* cpp::default_loss_scale() */
+int tcnn_preferred_precision(void);               /* cpp::preferred_precision() */
+
+/* ---- runtime module FFI (cpp_api.h:86-117) ---- */
+/* cpp::create_network_with_input_encoding(n_input_dims, n_output_dims, encoding, network) */
+tcnn_module* tcnn_create_network_with_input_encoding(uint32_t n_input_dims, uint32_t n_output_dims,
+                                                     const char* encoding_json, const char* network_json);
+/* cpp::create_network(n_input_dims, n_output_dims, network) (= Identity encoding + network) */
+tcnn_module* tcnn_create_network(uint32_t n_input_dims, uint32_t n_output_dims, const char* network_json);
+/* cpp::create_encoding(n_input_dims, encoding, requested_precision) */
+tcnn_module* tcnn_create_encoding(uint32_t n_input_dims, const char* encoding_json, int precision);
+void tcnn_module_destroy(tcnn_module* m);
+
+/* Module::inference(stream, n, input, output, params) (cpp_api.h:91) */
+int tcnn_module_inference(tcnn_module* m, void* stream, uint32_t n, const float* input, void* output, const void* params);
+/* Module::forward(stream, n, input, output, params, prepare_input_gradients) -> Context (cpp_api.h:92) */
+tcnn_context* tcnn_module_forward(tcnn_module* m, void* stream, uint32_t n, const float* input, void* output,
+                                  const void* params, int prepare_input_gradients);
+/* Module::backward(stream, ctx, n, dL_dinput?, dL_doutput, dL_dparams?, input, output, params) (cpp_api.h:93);
+ * dL_dparams == NULL -> GradientMode::Ignore, else Overwrite. dL_dinput may be NULL. */
+int tcnn_module_backward(tcnn_module* m, void* stream, const tcnn_context* ctx, uint32_t n, float* dL_dinput,
+                         const void* dL_doutput, void* dL_dparams, const float* input, const void* output,
+                         const void* params);
+void tcnn_context_destroy(tcnn_context* ctx);
+
+uint32_t tcnn_module_n_input_dims(const tcnn_module* m);
+uint32_t tcnn_module_n_output_dims(const tcnn_module* m); /* padded width (cpp_api.cu:130) */
+uint64_t tcnn_module_n_params(const tcnn_module* m);
+int tcnn_module_param_precision(const tcnn_module* m);
+int tcnn_module_output_precision(const tcnn_module* m);
+/* Module::initialize_params(seed, params_full_precision, scale): pcg32{seed} (cpp_api.cu:133-136);
+ * params_fp32 is a DEVICE pointer to n_params floats. */
+int tcnn_module_initialize_params(tcnn_module* m, uint64_t seed, float* params_fp32, float scale);
+/* hyperparams() / name() as JSON / plain strings; valid until the next call on this module. */
+const char* tcnn_module_hyperparams(tcnn_module* m);
+const char* tcnn_module_name(tcnn_module* m);
+
+/* ---- trainer: create_from_config + Trainer<float, __half, __half> (config.h:53-63, trainer.h) ---- */
+/* config_json holds {"loss", "optimizer", "encoding", "network"}; seed as Trainer(seed=1337). */
+tcnn_trainer* tcnn_trainer_create(uint32_t n_input_dims, uint32_t n_output_dims, const char* config_json, uint32_t seed);
+void tcnn_trainer_destroy(tcnn_trainer* t);
+/* Trainer::training_step(stream, input [n x n_in] fp32, target [n x n_out] fp32, run_optimizer) (trainer.h:163-190). */
+int tcnn_trainer_training_step(tcnn_trainer* t, void* stream, uint32_t n, const float* input, const float* target,
+                               int run_optimizer);
+/* Trainer::optimizer_step(stream, loss_scale) (trainer.h:155-157) */
+int tcnn_trainer_optimizer_step(tcnn_trainer* t, void* stream);
+/* Trainer::loss(stream, ctx) of the last training step (trainer.h:205-207); synchronises `stream`. */
+float tcnn_trainer_loss(tcnn_trainer* t, void* stream);
+/* Device pointer to the last step's loss sum (fp32 scalar), for graph-friendly readback. */
+const float* tcnn_trainer_loss_device(tcnn_trainer* t);
+/* network->inference(stream, input, output fp32 [n x n_out]) (object.h:147-176) */
+int tcnn_trainer_inference(tcnn_trainer* t, void* stream, uint32_t n, const float* input, float* output);
+uint64_t tcnn_trainer_n_params(const tcnn_trainer* t);
+uint64_t tcnn_trainer_n_network_params(const tcnn_trainer* t); /* MLP part; grid params follow */
+/* Parameter buffers (trainer.h:325-336): fp32 master, fp16 params, fp16 gradients; plus the fp32
+ * gradient sum the kernels produce (what a data-parallel all-reduce exchanges). */
+float* tcnn_trainer_params_fp32(tcnn_trainer* t);
+void* tcnn_trainer_params(tcnn_trainer* t);
+void* tcnn_trainer_param_gradients(tcnn_trainer* t);
+float* tcnn_trainer_gradients_fp32(tcnn_trainer* t);
+/* Data-parallel support: Adam reads grad_fp32 * grad_scale (set 1/N after a sum all-reduce). */
+int tcnn_trainer_set_gradient_scale(tcnn_trainer* t, float scale);
+/* Re-upload params from a host fp32 array (Trainer::set_params_full_precision, trainer.h:231-244). */
+int tcnn_trainer_set_params_full_precision(tcnn_trainer* t, const float* host_params, uint64_t n);
+/* Adam step counter (AdamOptimizer::step(), adam.h:200-202). */
+uint32_t tcnn_trainer_optimizer_step_count(const tcnn_trainer* t);
+/* Engine diagnostics: name of the path the trainer runs ("fused" / "unfused"). */
+const char* tcnn_trainer_engine(const tcnn_trainer* t);
+
+/* ---- per-phase hipEvent timing of training steps (measurement hook, not in the reference) ----
+ * Between begin and end every training_step records events around its phases on its stream:
+ * 0 fused grid-encode + MLP fwd/loss/bwd kernel, 1 weight-gradient reduction, 2 grid backward,
+ * 3 grid-gradient reduction, 4 loss sum, 5 Adam (only when the optimizer ran in that step).
+ * end() synchronises the device and writes the mean ms per phase over the complete steps. */
+int tcnn_trainer_profile_begin(tcnn_trainer* t);
+int tcnn_trainer_profile_end(tcnn_trainer* t, double* ms_per_phase, uint32_t n_phases, uint32_t* n_steps);
+
+/* ---- self test (layout probe for the MFMA / transpose-read operand maps) ---- */
+int tcnn_debug_probe(void* stream, float* mfma_out /* device [64*4] */, int16_t* tr_out /* device [64*8] */);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TCNN_MI355X_H */

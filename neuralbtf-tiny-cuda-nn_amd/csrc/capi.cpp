@@ -1,0 +1,298 @@
+// capi.cpp -- extern "C" boundary (include/tcnn_mi355x.h). Exceptions stop here and become return
+// codes + tcnn_last_error().
+#include "../../include/tcnn_mi355x.h"
+
+#include <algorithm>
+#include <cstring>
+
+#include "runtime.h"
+
+using namespace tcnn_amd;
+
+namespace {
+thread_local std::string g_last_error;
+thread_local std::string g_str;
+
+template <typename F>
+int guard(F&& f) {
+	try {
+		f();
+		return 0;
+	} catch (const std::exception& e) {
+		g_last_error = e.what();
+	} catch (...) {
+		g_last_error = "unknown C++ exception";
+	}
+	return 1;
+}
+
+template <typename T, typename F>
+T* guard_ptr(F&& f) {
+	try {
+		return f();
+	} catch (const std::exception& e) {
+		g_last_error = e.what();
+	} catch (...) {
+		g_last_error = "unknown C++ exception";
+	}
+	return nullptr;
+}
+
+json parse_json(const char* s) {
+	if (!s || !*s) return json::object();
+	return json::parse(std::string(s));
+}
+
+// ---- runtime module (cpp_api.cu:64-140) ----
+struct ModuleBase {
+	virtual ~ModuleBase() = default;
+	virtual void inference(hipStream_t st, uint32_t n, const float* in, void* out, const void* params) = 0;
+	virtual void forward(hipStream_t st, uint32_t n, const float* in, void* out, const void* params, bool prep) = 0;
+	virtual void backward(hipStream_t st, uint32_t n, float* dL_din, const void* dL_dout, void* dL_dparams, const float* in,
+	                      const void* out, const void* params) = 0;
+	virtual uint32_t n_input_dims() const = 0;
+	virtual uint32_t n_output_dims() const = 0;
+	virtual uint64_t n_params() const = 0;
+	virtual void initialize_params(uint64_t seed, float* params_fp32, float scale) = 0;
+	virtual json hyperparams() const = 0;
+	virtual std::string name() const = 0;
+	std::string scratch;
+};
+
+void check_batch(uint32_t n) {
+	TCNN_CHECK(n % BATCH_GRANULARITY == 0, "Batch size must be a multiple of " + std::to_string(BATCH_GRANULARITY));
+}
+
+struct ModuleNWIE : ModuleBase {
+	NetworkWithGridHost model;
+	StepWorkspace ws;
+	DevBuf grad32;
+	ModuleNWIE(uint32_t n_in, uint32_t n_out, const json& enc, const json& net) : model(n_in, n_out, enc, net) {}
+	void inference(hipStream_t st, uint32_t n, const float* in, void* out, const void* params) override {
+		check_batch(n);
+		model.inference(st, ws, n, in, params, out);
+	}
+	void forward(hipStream_t st, uint32_t n, const float* in, void* out, const void* params, bool prep) override {
+		TCNN_CHECK(!prep, "prepare_input_gradients (dL/dinput through the grid) is not implemented by the MI355X engine yet");
+		check_batch(n);
+		// The backward recomputes activations from the input, so the context carries nothing.
+		model.inference(st, ws, n, in, params, out);
+	}
+	void backward(hipStream_t st, uint32_t n, float* dL_din, const void* dL_dout, void* dL_dparams, const float* in,
+	              const void*, const void* params) override {
+		TCNN_CHECK(dL_din == nullptr, "dL/dinput through the grid is not implemented by the MI355X engine yet");
+		check_batch(n);
+		if (!dL_dparams) return;
+		grad32.reserve(n_params() * 4);
+		model.fwd_bwd(st, ws, n, in, nullptr, model.n_output_dims, 1.0f, params, dL_dout, nullptr, grad32.as<float>());
+		launch_cast_f32_f16(st, grad32.as<float>(), dL_dparams, n_params());
+	}
+	uint32_t n_input_dims() const override { return model.n_input_dims; }
+	uint32_t n_output_dims() const override { return model.mlp.padded_output; }
+	uint64_t n_params() const override { return model.n_params(); }
+	void initialize_params(uint64_t seed, float* p, float scale) override {
+		Pcg32 rng{seed};
+		std::vector<float> host(n_params());
+		model.initialize_params(rng, host.data(), scale);
+		TCNN_HIP_CHECK(hipMemcpy(p, host.data(), host.size() * 4, hipMemcpyHostToDevice));
+	}
+	json hyperparams() const override { return model.hyperparams(); }
+	std::string name() const override { return "NetworkWithInputEncoding"; }
+};
+
+struct ModuleGrid : ModuleBase {
+	GridEncodingHost grid;
+	DevBuf partial, grad32;
+	ModuleGrid(uint32_t n_in, const json& enc) : grid(n_in, enc) {}
+	void inference(hipStream_t st, uint32_t n, const float* in, void* out, const void* params) override {
+		check_batch(n);
+		const uint32_t W = grid.padded_output_width();
+		if (grid.n_to_pad) TCNN_HIP_CHECK(hipMemsetAsync(out, 0, (size_t)n * W * 2, st));
+		launch_grid_fwd(st, grid.desc.n_pos_dims, grid.desc.n_features_per_level, grid.desc.hash_type, n, grid.desc.n_levels,
+		                in, grid.desc.n_pos_dims, params, out, false, W, grid.dev_levels(), grid.hash_grid(), grid.desc.interp);
+	}
+	void forward(hipStream_t st, uint32_t n, const float* in, void* out, const void* params, bool prep) override {
+		TCNN_CHECK(!prep, "prepare_input_gradients (grid dy/dx) is not implemented by the MI355X engine yet");
+		inference(st, n, in, out, params);
+	}
+	void backward(hipStream_t st, uint32_t n, float* dL_din, const void* dL_dout, void* dL_dparams, const float* in,
+	              const void*, const void*) override {
+		TCNN_CHECK(dL_din == nullptr, "dL/dinput through the grid is not implemented by the MI355X engine yet");
+		check_batch(n);
+		TCNN_CHECK(!grid.stochastic, "stochastic_interpolation is not implemented by the MI355X engine yet");
+		if (!dL_dparams) return;
+		const uint32_t n_slices = (uint32_t)grid.slices.size();
+		uint32_t n_chunks = std::max(1u, 512u / n_slices);
+		n_chunks = std::min(n_chunks, std::max(1u, n / 4096));
+		partial.reserve((size_t)n_chunks * grid.n_params * 4);
+		grad32.reserve((size_t)grid.n_params * 4);
+		launch_grid_bwd(st, grid.desc.n_pos_dims, grid.desc.n_features_per_level, grid.desc.hash_type, n, in, grid.desc.n_pos_dims,
+		                dL_dout, 2, grid.padded_output_width(), grid.d_slices.as<GridSlice>(), n_slices, n_chunks,
+		                partial.as<float>(), grid.n_params, grid.dev_levels(), grid.hash_grid(), grid.desc.interp);
+		launch_reduce_partials(st, partial.as<float>(), n_chunks, grid.n_params, grid.n_params, grad32.as<float>());
+		launch_cast_f32_f16(st, grad32.as<float>(), dL_dparams, grid.n_params);
+	}
+	uint32_t n_input_dims() const override { return grid.desc.n_pos_dims; }
+	uint32_t n_output_dims() const override { return grid.padded_output_width(); }
+	uint64_t n_params() const override { return grid.n_params; }
+	void initialize_params(uint64_t seed, float* p, float scale) override {
+		Pcg32 rng{seed};
+		std::vector<float> host(n_params());
+		grid.initialize_params(rng, host.data(), scale);
+		TCNN_HIP_CHECK(hipMemcpy(p, host.data(), host.size() * 4, hipMemcpyHostToDevice));
+	}
+	json hyperparams() const override { return grid.hyperparams(); }
+	std::string name() const override { return "GridEncoding"; }
+};
+}  // namespace
+
+struct tcnn_module {
+	std::unique_ptr<ModuleBase> m;
+};
+struct tcnn_context {
+	uint32_t n = 0;
+};
+struct tcnn_trainer {
+	std::unique_ptr<TrainerHost> t;
+};
+
+extern "C" {
+
+const char* tcnn_last_error(void) { return g_last_error.c_str(); }
+const char* tcnn_version(void) { return "tcnn-mi355x 0.1 (gfx950)"; }
+uint32_t tcnn_batch_size_granularity(void) { return BATCH_GRANULARITY; }
+int tcnn_cuda_device(void) {
+	int d = -1;
+	if (hipGetDevice(&d) != hipSuccess) return -1;
+	return d;
+}
+int tcnn_set_cuda_device(int device) {
+	return guard([&] { TCNN_HIP_CHECK(hipSetDevice(device)); });
+}
+void tcnn_free_temporary_memory(void) {}
+int tcnn_has_networks(void) { return 1; }
+float tcnn_default_loss_scale(int precision) { return precision == TCNN_PRECISION_FP32 ? 1.0f : 128.0f; }
+int tcnn_preferred_precision(void) { return TCNN_PRECISION_FP16; }
+
+tcnn_module* tcnn_create_network_with_input_encoding(uint32_t n_in, uint32_t n_out, const char* enc, const char* net) {
+	return guard_ptr<tcnn_module>([&] {
+		auto* r = new tcnn_module;
+		r->m = std::make_unique<ModuleNWIE>(n_in, n_out, parse_json(enc), parse_json(net));
+		return r;
+	});
+}
+
+tcnn_module* tcnn_create_network(uint32_t n_in, uint32_t n_out, const char* net) {
+	(void)n_in; (void)n_out; (void)net;
+	g_last_error = "create_network (Identity encoding + MLP) is not implemented by the MI355X engine yet";
+	return nullptr;
+}
+
+tcnn_module* tcnn_create_encoding(uint32_t n_in, const char* enc, int precision) {
+	return guard_ptr<tcnn_module>([&] {
+		TCNN_CHECK(precision == TCNN_PRECISION_FP16, "create_encoding: only Fp16 precision is implemented by the MI355X engine");
+		json j = parse_json(enc);
+		const std::string ot = j.is_object() && j.find("otype") != j.end() ? j["otype"].get<std::string>() : "OneBlob";
+		TCNN_CHECK(ieq(ot, "HashGrid") || ieq(ot, "Grid") || ieq(ot, "TiledGrid") || ieq(ot, "DenseGrid"),
+		           "Encoding '" + ot + "' is not implemented by the MI355X engine yet");
+		auto* r = new tcnn_module;
+		r->m = std::make_unique<ModuleGrid>(n_in, j);
+		return r;
+	});
+}
+
+void tcnn_module_destroy(tcnn_module* m) { delete m; }
+
+int tcnn_module_inference(tcnn_module* m, void* stream, uint32_t n, const float* in, void* out, const void* params) {
+	return guard([&] { m->m->inference((hipStream_t)stream, n, in, out, params); });
+}
+
+tcnn_context* tcnn_module_forward(tcnn_module* m, void* stream, uint32_t n, const float* in, void* out, const void* params, int prep) {
+	return guard_ptr<tcnn_context>([&] {
+		m->m->forward((hipStream_t)stream, n, in, out, params, prep != 0);
+		auto* c = new tcnn_context;
+		c->n = n;
+		return c;
+	});
+}
+
+int tcnn_module_backward(tcnn_module* m, void* stream, const tcnn_context* ctx, uint32_t n, float* dL_din, const void* dL_dout,
+                         void* dL_dparams, const float* in, const void* out, const void* params) {
+	return guard([&] {
+		TCNN_CHECK(ctx != nullptr, "backward: null context");
+		m->m->backward((hipStream_t)stream, n, dL_din, dL_dout, dL_dparams, in, out, params);
+	});
+}
+
+void tcnn_context_destroy(tcnn_context* c) { delete c; }
+uint32_t tcnn_module_n_input_dims(const tcnn_module* m) { return m->m->n_input_dims(); }
+uint32_t tcnn_module_n_output_dims(const tcnn_module* m) { return m->m->n_output_dims(); }
+uint64_t tcnn_module_n_params(const tcnn_module* m) { return m->m->n_params(); }
+int tcnn_module_param_precision(const tcnn_module*) { return TCNN_PRECISION_FP16; }
+int tcnn_module_output_precision(const tcnn_module*) { return TCNN_PRECISION_FP16; }
+int tcnn_module_initialize_params(tcnn_module* m, uint64_t seed, float* p, float scale) {
+	return guard([&] { m->m->initialize_params(seed, p, scale); });
+}
+const char* tcnn_module_hyperparams(tcnn_module* m) {
+	m->m->scratch = m->m->hyperparams().dump();
+	return m->m->scratch.c_str();
+}
+const char* tcnn_module_name(tcnn_module* m) {
+	m->m->scratch = m->m->name();
+	return m->m->scratch.c_str();
+}
+
+tcnn_trainer* tcnn_trainer_create(uint32_t n_in, uint32_t n_out, const char* cfg, uint32_t seed) {
+	return guard_ptr<tcnn_trainer>([&] {
+		auto* r = new tcnn_trainer;
+		r->t = std::make_unique<TrainerHost>(n_in, n_out, parse_json(cfg), seed);
+		return r;
+	});
+}
+void tcnn_trainer_destroy(tcnn_trainer* t) { delete t; }
+int tcnn_trainer_training_step(tcnn_trainer* t, void* stream, uint32_t n, const float* in, const float* target, int run_opt) {
+	return guard([&] { t->t->training_step((hipStream_t)stream, n, in, target, run_opt != 0); });
+}
+int tcnn_trainer_optimizer_step(tcnn_trainer* t, void* stream) {
+	return guard([&] { t->t->optimizer_step((hipStream_t)stream); });
+}
+float tcnn_trainer_loss(tcnn_trainer* t, void* stream) {
+	float v = -1.0f;
+	if (guard([&] { v = t->t->loss((hipStream_t)stream); }) != 0) return -1.0f;
+	return v;
+}
+const float* tcnn_trainer_loss_device(tcnn_trainer* t) { return t->t->d_loss.as<float>(); }
+int tcnn_trainer_inference(tcnn_trainer* t, void* stream, uint32_t n, const float* in, float* out) {
+	return guard([&] { t->t->inference((hipStream_t)stream, n, in, out); });
+}
+uint64_t tcnn_trainer_n_params(const tcnn_trainer* t) { return t->t->n_params; }
+uint64_t tcnn_trainer_n_network_params(const tcnn_trainer* t) { return t->t->n_mlp; }
+float* tcnn_trainer_params_fp32(tcnn_trainer* t) { return t->t->w32.as<float>(); }
+void* tcnn_trainer_params(tcnn_trainer* t) { return t->t->w16.p; }
+void* tcnn_trainer_param_gradients(tcnn_trainer* t) { return t->t->g16.p; }
+float* tcnn_trainer_gradients_fp32(tcnn_trainer* t) { return t->t->g32.as<float>(); }
+int tcnn_trainer_set_gradient_scale(tcnn_trainer* t, float s) {
+	t->t->grad_scale = s;
+	return 0;
+}
+int tcnn_trainer_set_params_full_precision(tcnn_trainer* t, const float* host, uint64_t n) {
+	return guard([&] { t->t->set_params_full_precision(host, n); });
+}
+uint32_t tcnn_trainer_optimizer_step_count(const tcnn_trainer* t) { return t->t->adam_step; }
+const char* tcnn_trainer_engine(const tcnn_trainer* t) { return t->t->model->fused_ok() ? "fused" : "unsupported"; }
+
+int tcnn_trainer_profile_begin(tcnn_trainer* t) {
+	return guard([&] {
+		t->t->timer.reset();
+		t->t->timer.enabled = true;
+	});
+}
+int tcnn_trainer_profile_end(tcnn_trainer* t, double* ms, uint32_t n_phases, uint32_t* n_steps) {
+	return guard([&] { t->t->profile_end(ms, n_phases, n_steps); });
+}
+
+int tcnn_debug_probe(void* stream, float* mfma_out, int16_t* tr_out) {
+	return guard([&] { launch_probe((hipStream_t)stream, mfma_out, tr_out); });
+}
+
+}  // extern "C"

@@ -1,0 +1,65 @@
+// common.h -- shared device/host definitions of the MI355X (gfx950) engine.
+//
+// Written for CDNA4 only: wave64, MFMA f32_16x16x32_f16, packed-fp16 VALU, 160 KiB LDS per CU.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+namespace tcnn_amd {
+
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef short s4 __attribute__((ext_vector_type(4)));
+
+constexpr int WAVE = 64;
+constexpr uint32_t MAX_LEVELS = 64;
+constexpr uint32_t BATCH_GRANULARITY = 256;  // BATCH_SIZE_GRANULARITY, reference common.h:235
+
+#define TCNN_HIP_CHECK(x)                                                                          \
+	do {                                                                                       \
+		hipError_t _e = (x);                                                               \
+		if (_e != hipSuccess)                                                              \
+			throw std::runtime_error(std::string(#x " failed: ") + hipGetErrorString(_e) + \
+			                         " at " __FILE__ ":" + std::to_string(__LINE__));     \
+	} while (0)
+
+#define TCNN_CHECK(cond, msg)                                                                      \
+	do {                                                                                       \
+		if (!(cond)) throw std::runtime_error(std::string(msg));                          \
+	} while (0)
+
+// Per-level grid geometry handed to kernels (computed once on the host, so the kernels and the
+// offset table use bit-identical scales/resolutions; reference grid.h:694 vs grid.h:97-98).
+struct GridLevels {
+	uint32_t n_levels;
+	uint32_t offset[MAX_LEVELS + 1];  // in entries
+	float scale[MAX_LEVELS];
+	uint32_t res[MAX_LEVELS];
+	uint32_t dense_stride_ok[MAX_LEVELS];  // helper bitfield (unused by kernels)
+};
+
+enum class GridType : uint32_t { Hash = 0, Dense = 1, Tiled = 2 };
+enum class HashType : uint32_t { Prime = 0, CoherentPrime = 1, ReversedPrime = 2 };
+enum class Interp : uint32_t { Nearest = 0, Linear = 1, Smoothstep = 2 };
+
+struct GridDesc {
+	uint32_t n_pos_dims;
+	uint32_t n_features_per_level;
+	uint32_t n_levels;
+	uint32_t log2_hashmap_size;
+	uint32_t base_resolution;
+	float per_level_scale;
+	GridType grid_type;
+	HashType hash_type;
+	Interp interp;
+};
+
+inline uint32_t div_round_up(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+
+}  // namespace tcnn_amd

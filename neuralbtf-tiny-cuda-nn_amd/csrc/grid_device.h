@@ -1,0 +1,103 @@
+// grid_device.h -- multiresolution grid helpers for gfx950 kernels.
+//
+// Semantics follow the reference exactly where they decide *which* table entry is touched and how
+// the forward interpolation rounds:
+//   pos_fract            reference common_device.h:841-868 (pos = fmaf(scale, x, 0.5))
+//   grid_index / hashes  reference common_device.h:631-707 (stride loop, hash, % hashmap_size)
+//   corner order/weights reference grid.h:144-163 (fp32 weight product, (half)w, fp16 FMA chain)
+// The modulo by a runtime table size is specialised: power-of-two sizes (every hashed level) use a
+// mask, dense levels only divide in the rare wrap-around case.
+#pragma once
+
+#include "common.h"
+
+namespace tcnn_amd {
+
+struct LevelInfo {
+	float scale;
+	uint32_t res;
+	uint32_t offset;  // entries
+	uint32_t size;    // entries
+};
+
+template <HashType H>
+__device__ __forceinline__ uint32_t hash_prime(uint32_t d) {
+	if constexpr (H == HashType::Prime) {
+		constexpr uint32_t P[7] = {1958374283u, 2654435761u, 805459861u, 3674653429u, 2097192037u, 1434869437u, 2165219737u};
+		return P[d];
+	} else if constexpr (H == HashType::ReversedPrime) {
+		constexpr uint32_t P[7] = {2165219737u, 1434869437u, 2097192037u, 3674653429u, 805459861u, 2654435761u, 1958374283u};
+		return P[d];
+	} else {
+		constexpr uint32_t P[7] = {1u, 2654435761u, 805459861u, 3674653429u, 2097192037u, 1434869437u, 2165219737u};
+		return P[d];
+	}
+}
+
+template <uint32_t D, HashType H>
+__device__ __forceinline__ uint32_t grid_index(bool hash_grid, uint32_t size, uint32_t res, const uint32_t* pg) {
+	uint32_t stride = 1, index = 0;
+#pragma unroll
+	for (uint32_t d = 0; d < D; ++d) {
+		if (stride > size) break;
+		index += pg[d] * stride;
+		stride *= res;
+	}
+	if (hash_grid && size < stride) {
+		uint32_t h = 0;
+#pragma unroll
+		for (uint32_t d = 0; d < D; ++d) h ^= pg[d] * hash_prime<H>(d);
+		index = h;
+	}
+	if ((size & (size - 1)) == 0) return index & (size - 1);
+	return index < size ? index : index % size;
+}
+
+__device__ __forceinline__ void pos_fract(float x, float scale, Interp interp, float& pos, uint32_t& grid) {
+	float p = __builtin_fmaf(scale, x, 0.5f);
+	float t = floorf(p);
+	grid = (uint32_t)(int)t;
+	p -= t;
+	if (interp == Interp::Smoothstep) p = p * p * __builtin_fmaf(-2.0f, p, 3.0f);
+	pos = p;
+}
+
+// Linear interpolation of one level for F == 2 features (one half2 per table entry). Gathers are
+// issued together before the fp16 FMA chain so their latencies overlap.
+template <uint32_t D, HashType H>
+__device__ __forceinline__ h2 encode_level_f2(const uint32_t* __restrict__ table_u32, const LevelInfo& li,
+                                              bool hash_grid, Interp interp, const float* x) {
+	float pos[D];
+	uint32_t pg[D];
+#pragma unroll
+	for (uint32_t d = 0; d < D; ++d) pos_fract(x[d], li.scale, interp, pos[d], pg[d]);
+	if (interp == Interp::Nearest) {
+		uint32_t idx = grid_index<D, H>(hash_grid, li.size, li.res, pg);
+		uint32_t v = table_u32[li.offset + idx];
+		return __builtin_bit_cast(h2, v);
+	}
+	constexpr uint32_t NC = 1u << D;
+	uint32_t v[NC];
+	_Float16 w16[NC];
+#pragma unroll
+	for (uint32_t c = 0; c < NC; ++c) {
+		float w = 1.0f;
+		uint32_t local[D];
+#pragma unroll
+		for (uint32_t d = 0; d < D; ++d) {
+			if ((c & (1u << d)) == 0) { w *= 1.0f - pos[d]; local[d] = pg[d]; }
+			else { w *= pos[d]; local[d] = pg[d] + 1; }
+		}
+		w16[c] = (_Float16)w;
+		v[c] = table_u32[li.offset + grid_index<D, H>(hash_grid, li.size, li.res, local)];
+	}
+	h2 r = {(_Float16)0.0f, (_Float16)0.0f};
+#pragma unroll
+	for (uint32_t c = 0; c < NC; ++c) {
+		h2 wv = {w16[c], w16[c]};
+		r = __builtin_elementwise_fma(wv, __builtin_bit_cast(h2, v[c]), r);
+	}
+	return r;
+}
+
+}  // namespace tcnn_amd

@@ -1,0 +1,77 @@
+// kernels.h -- host-side launchers of the gfx950 kernels (defined in kernels.hip).
+#pragma once
+
+#include "common.h"
+
+namespace tcnn_amd {
+
+struct LevelInfo;
+
+// Workspace plan for the LDS-privatised grid backward: one work item per (level, entry slice).
+struct GridSlice {
+	uint32_t level;
+	uint32_t begin;  // entry range within the level
+	uint32_t end;
+};
+
+struct AdamArgs {
+	uint32_t n, n_matrix;
+	float loss_scale, grad_scale;  // grad_scale multiplies the fp32 gradient before fp16 rounding (1/N for N-rank sums)
+	float lr, beta1, beta2, eps, l2_reg, rel_decay, abs_decay, clip, nonmat_lr_factor;
+	float lower_lr_bound, upper_lr_bound;
+	int opt_matrix, opt_nonmatrix;
+};
+
+// Fused train step (grid encoding -> MLP fwd -> RelativeL2 -> MLP bwd -> dW partials, dL/denc).
+// With dout16 != NULL the loss is skipped and dL/d(output) fp16 [B][16] is read instead (Module::backward).
+// Returns false if no fused kernel exists for this shape.
+bool fused_train_supported(uint32_t W, uint32_t IN, uint32_t NH, uint32_t D, uint32_t F, uint32_t OUTP, int act, HashType h);
+size_t fused_train_lds_bytes(uint32_t W, uint32_t IN, uint32_t NH);
+uint32_t fused_train_n_blocks(uint32_t B);
+void launch_fused_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, uint32_t D, HashType h, int act,
+                        uint32_t B, uint32_t dims, float loss_scale, const void* params16, const void* table16,
+                        const float* pos, const float* target, void* out16, void* dLdenc_pairs,
+                        float* wgrad_partial, float* loss_partial, const LevelInfo* levels, bool hash_grid,
+                        Interp interp, uint32_t n_blocks, const void* dout16 = nullptr);
+
+// Forward-only MLP (inference): in fp16 SoA [IN][B] or AoS [B][IN] -> out fp16 [B][16].
+bool mlp_infer_supported(uint32_t W, uint32_t IN, uint32_t NH, uint32_t OUTP, int act);
+void launch_mlp_infer(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, int act, bool soa, uint32_t B,
+                      const void* params16, const void* in16, void* out16);
+// out[b*n_out + o] = (float)in[b*in_stride + o]  (reference trim_and_cast_from, object.cu:60-67)
+void launch_trim_cast(hipStream_t st, uint32_t B, uint32_t in_stride, uint32_t n_out, const void* in16, float* out);
+
+// Grid forward (standalone; reference kernel_grid layout): out SoA [(l*F+f)*B + i] when soa, else
+// AoS [i*out_stride + l*F + f].
+void launch_grid_fwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_t B, uint32_t L,
+                     const float* pos, uint32_t pos_stride, const void* table16, void* out16, bool soa,
+                     uint32_t out_stride, const LevelInfo* levels, bool hash_grid, Interp interp);
+
+// Grid backward: dLdy layout 0 = level-major pairs ([l][i][F] halves), 1 = SoA ([(l*F+f)*B + i]),
+// 2 = AoS ([i*dy_stride + l*F + f]).
+uint32_t grid_bwd_slice_entries(uint32_t F);
+void launch_grid_bwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_t B, const float* pos,
+                     uint32_t pos_stride, const void* dLdy16, int dy_layout, uint32_t dy_stride, const GridSlice* slices,
+                     uint32_t n_slices, uint32_t n_chunks, float* partial, uint32_t partial_stride,
+                     const LevelInfo* levels, bool hash_grid, Interp interp);
+
+// out[p] = sum_j in[j*stride + p] (p < n), optional fp16 copy
+void launch_reduce_partials(hipStream_t st, const float* in, uint32_t n_parts, uint32_t stride, uint32_t n,
+                            float* out);
+
+void launch_adam(hipStream_t st, const AdamArgs& a, float* w32, void* w16, const float* grad32, void* grad16,
+                 float* m1, float* m2, uint32_t* steps);
+
+void launch_cast_f32_f16(hipStream_t st, const float* in, void* out, size_t n);
+void launch_cast_f16_f32(hipStream_t st, const void* in, float* out, size_t n);
+
+// RelativeL2 (standalone, reference relative_l2.h:40-76): pred fp16 [B][stride] -> values, grads
+void launch_relative_l2(hipStream_t st, uint32_t B, uint32_t stride, uint32_t dims, float loss_scale,
+                        const void* pred16, const float* target, float* values, void* grads16);
+
+void launch_sum(hipStream_t st, const float* in, uint32_t n, float* out);
+
+// Debug probe: runs one MFMA 16x16x32 f16 and two ds_read_b64_tr_b16 with known data.
+void launch_probe(hipStream_t st, float* mfma_out, int16_t* tr_out);
+
+}  // namespace tcnn_amd

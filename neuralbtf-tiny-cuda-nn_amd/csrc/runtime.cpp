@@ -1,0 +1,513 @@
+// runtime.cpp -- host runtime: JSON config surface, parameter init, trainer orchestration.
+#include "runtime.h"
+
+#include <algorithm>
+#include <cctype>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <random>
+
+namespace tcnn_amd {
+
+// ------------------------------------------------------------------------------------------
+// PCG32 (stream semantics of dependencies/pcg32/pcg32.h)
+// ------------------------------------------------------------------------------------------
+static constexpr uint64_t PCG32_MULT = 0x5851f42d4c957f2dULL;
+
+void Pcg32::seed(uint64_t initstate, uint64_t initseq) {
+	state = 0u;
+	inc = (initseq << 1u) | 1u;
+	next_uint();
+	state += initstate;
+	next_uint();
+}
+
+uint32_t Pcg32::next_uint() {
+	uint64_t old = state;
+	state = old * PCG32_MULT + inc;
+	uint32_t xorshifted = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+	uint32_t rot = (uint32_t)(old >> 59u);
+	return (xorshifted >> rot) | (xorshifted << ((~rot + 1u) & 31));
+}
+
+float Pcg32::next_float() {
+	uint32_t u = (next_uint() >> 9) | 0x3f800000u;
+	float f;
+	std::memcpy(&f, &u, 4);
+	return f - 1.0f;
+}
+
+void Pcg32::advance(int64_t delta_) {
+	uint64_t cur_mult = PCG32_MULT, cur_plus = inc, acc_mult = 1u, acc_plus = 0u;
+	uint64_t delta = (uint64_t)delta_;
+	while (delta > 0) {
+		if (delta & 1) {
+			acc_mult *= cur_mult;
+			acc_plus = acc_plus * cur_mult + cur_plus;
+		}
+		cur_plus = (cur_mult + 1) * cur_plus;
+		cur_mult *= cur_mult;
+		delta /= 2;
+	}
+	state = acc_mult * state + acc_plus;
+}
+
+// generate_random_uniform's strided order (reference random.h:39-70), evaluated on the host.
+static void strided_uniform(Pcg32& rng, size_t n, float* out, float lo, float hi) {
+	const size_t n_gen = 4;
+	const size_t n_thr = (n + n_gen - 1) / n_gen;
+	const size_t n_threads = (n_thr + 127) / 128 * 128;
+	const float range = hi - lo;
+	for (size_t i = 0; i < n_thr; ++i) {
+		Pcg32 r = rng;
+		r.advance((int64_t)(i * n_gen));
+		for (size_t j = 0; j < n_gen; ++j) {
+			size_t idx = i + n_threads * j;
+			if (idx >= n) break;
+			out[idx] = std::fma(r.next_float(), range, lo);
+		}
+	}
+	rng.advance((int64_t)n);
+}
+
+// ------------------------------------------------------------------------------------------
+// DevBuf
+// ------------------------------------------------------------------------------------------
+DevBuf::~DevBuf() { release(); }
+
+void DevBuf::release() {
+	if (p) (void)hipFree(p);
+	p = nullptr;
+	bytes = 0;
+}
+
+void DevBuf::reserve(size_t n) {
+	if (n <= bytes && p) return;
+	release();
+	if (n == 0) n = 16;
+	TCNN_HIP_CHECK(hipMalloc(&p, n));
+	bytes = n;
+}
+
+bool ieq(const std::string& a, const std::string& b) {
+	if (a.size() != b.size()) return false;
+	for (size_t i = 0; i < a.size(); ++i)
+		if (std::tolower((unsigned char)a[i]) != std::tolower((unsigned char)b[i])) return false;
+	return true;
+}
+
+template <typename T>
+static T jval(const json& j, const char* key, T dflt) {
+	auto it = j.find(key);
+	if (it == j.end() || it->is_null()) return dflt;
+	return it->get<T>();
+}
+
+static bool jhas(const json& j, const char* key) { return j.is_object() && j.find(key) != j.end(); }
+
+// ------------------------------------------------------------------------------------------
+// Grid encoding (reference grid.h:652-1208)
+// ------------------------------------------------------------------------------------------
+static uint32_t powi_u32(uint32_t base, uint32_t exp) {
+	uint32_t r = 1;
+	for (uint32_t i = 0; i < exp; ++i) r *= base;
+	return r;
+}
+
+GridEncodingHost::GridEncodingHost(uint32_t n_dims, const json& enc) {
+	const std::string otype = jval<std::string>(enc, "otype", "Grid");
+	const std::string default_type = ieq(otype, "TiledGrid") ? "Tiled" : (ieq(otype, "DenseGrid") ? "Dense" : "Hash");
+	const uint32_t F = jval<uint32_t>(enc, "n_features_per_level", 2u);
+	TCNN_CHECK(F == 1 || F == 2 || F == 4 || F == 8, "GridEncoding: n_features_per_level must be 1, 2, 4, or 8.");
+	uint32_t n_feat;
+	if (jhas(enc, "n_features") || jhas(enc, "n_grid_features")) {
+		n_feat = jhas(enc, "n_features") ? enc["n_features"].get<uint32_t>() : enc["n_grid_features"].get<uint32_t>();
+		TCNN_CHECK(!jhas(enc, "n_levels"), "GridEncoding: may not specify n_features and n_levels simultaneously (one determines the other)");
+	} else {
+		n_feat = F * jval<uint32_t>(enc, "n_levels", 16u);
+	}
+	TCNN_CHECK(n_feat % F == 0, "GridEncoding: n_features must be a multiple of n_features_per_level");
+	const uint32_t L = n_feat / F;
+	TCNN_CHECK(L >= 1 && L <= MAX_LEVELS, "GridEncoding: too many levels");
+	const std::string type = jval<std::string>(enc, "type", default_type);
+	GridType gt;
+	if (ieq(type, "Hash")) gt = GridType::Hash;
+	else if (ieq(type, "Dense")) gt = GridType::Dense;
+	else if (ieq(type, "Tiled")) gt = GridType::Tiled;
+	else throw std::runtime_error("GridEncoding: invalid grid type " + type);
+	const uint32_t base = jval<uint32_t>(enc, "base_resolution", 16u);
+	const float default_scale = gt == GridType::Dense ? std::exp(std::log(256.0f / (float)base) / (float)(L - 1)) : 2.0f;
+	const std::string interp = jval<std::string>(enc, "interpolation", "Linear");
+	const std::string hash = jval<std::string>(enc, "hash", "CoherentPrime");
+	TCNN_CHECK(n_dims >= 2 && n_dims <= 4, "GridEncoding: number of input dims must be 2, 3 or 4.");
+
+	desc.n_pos_dims = n_dims;
+	desc.n_features_per_level = F;
+	desc.n_levels = L;
+	desc.log2_hashmap_size = jval<uint32_t>(enc, "log2_hashmap_size", 19u);
+	desc.base_resolution = base;
+	desc.per_level_scale = jval<float>(enc, "per_level_scale", default_scale);
+	desc.grid_type = gt;
+	if (ieq(hash, "Prime")) desc.hash_type = HashType::Prime;
+	else if (ieq(hash, "CoherentPrime")) desc.hash_type = HashType::CoherentPrime;
+	else if (ieq(hash, "ReversedPrime")) desc.hash_type = HashType::ReversedPrime;
+	else throw std::runtime_error("GridEncoding: unsupported hash type " + hash);
+	if (ieq(interp, "Nearest")) desc.interp = Interp::Nearest;
+	else if (ieq(interp, "Linear")) desc.interp = Interp::Linear;
+	else if (ieq(interp, "Smoothstep")) desc.interp = Interp::Smoothstep;
+	else throw std::runtime_error("GridEncoding: invalid interpolation " + interp);
+	stochastic = jval<bool>(enc, "stochastic_interpolation", false);
+	n_features = n_feat;
+
+	// offset table, grid.h:688-719 (host log2/exp2 in float, as the reference's host code)
+	const float log2_scale = std::log2(desc.per_level_scale);
+	uint32_t offset = 0;
+	levels.resize(L);
+	for (uint32_t l = 0; l < L; ++l) {
+		const float scale = exp2f((float)l * log2_scale) * (float)base - 1.0f;
+		const uint32_t res = (uint32_t)ceilf(scale) + 1;
+		const uint32_t max_params = std::numeric_limits<uint32_t>::max() / 2;
+		uint32_t params = std::pow((float)res, (float)n_dims) > (float)max_params ? max_params : powi_u32(res, n_dims);
+		params = (params + 7u) / 8u * 8u;
+		if (gt == GridType::Tiled) params = std::min(params, powi_u32(base, n_dims));
+		else if (gt == GridType::Hash) params = std::min(params, 1u << desc.log2_hashmap_size);
+		levels[l] = LevelInfo{scale, res, offset, params};
+		offset += params;
+	}
+	n_params = offset * F;
+
+	// LDS-privatised backward plan: slices of at most grid_bwd_slice_entries(F) entries per level
+	const uint32_t SL = grid_bwd_slice_entries(F);
+	for (uint32_t l = 0; l < L; ++l)
+		for (uint32_t b = 0; b < levels[l].size; b += SL) slices.push_back(GridSlice{l, b, std::min(levels[l].size, b + SL)});
+
+	d_levels.reserve(levels.size() * sizeof(LevelInfo));
+	TCNN_HIP_CHECK(hipMemcpy(d_levels.p, levels.data(), levels.size() * sizeof(LevelInfo), hipMemcpyHostToDevice));
+	d_slices.reserve(slices.size() * sizeof(GridSlice));
+	TCNN_HIP_CHECK(hipMemcpy(d_slices.p, slices.data(), slices.size() * sizeof(GridSlice), hipMemcpyHostToDevice));
+}
+
+void GridEncodingHost::initialize_params(Pcg32& rng, float* out, float scale) const {
+	strided_uniform(rng, n_params, out, -1e-4f * scale, 1e-4f * scale);
+}
+
+static const char* grid_type_str(GridType t) { return t == GridType::Hash ? "Hash" : t == GridType::Dense ? "Dense" : "Tiled"; }
+static const char* hash_str(HashType t) { return t == HashType::Prime ? "Prime" : t == HashType::ReversedPrime ? "ReversedPrime" : "CoherentPrime"; }
+static const char* interp_str(Interp t) { return t == Interp::Nearest ? "Nearest" : t == Interp::Smoothstep ? "Smoothstep" : "Linear"; }
+
+json GridEncodingHost::hyperparams() const {  // grid.h:1096-1114
+	json r = {
+		{"otype", "Grid"}, {"type", grid_type_str(desc.grid_type)}, {"n_levels", desc.n_levels},
+		{"n_features_per_level", desc.n_features_per_level}, {"base_resolution", desc.base_resolution},
+		{"per_level_scale", desc.per_level_scale}, {"interpolation", interp_str(desc.interp)}, {"hash", hash_str(desc.hash_type)},
+	};
+	if (desc.grid_type == GridType::Hash) r["log2_hashmap_size"] = desc.log2_hashmap_size;
+	return r;
+}
+
+// ------------------------------------------------------------------------------------------
+// MLP (reference src/network.cu:48-138, fully_fused_mlp.cu:635-678, 865-891)
+// ------------------------------------------------------------------------------------------
+static int parse_activation(const std::string& s) {
+	if (ieq(s, "None")) return 0;
+	if (ieq(s, "ReLU")) return 1;
+	throw std::runtime_error("activation '" + s + "' is not supported by the MI355X engine (None, ReLU)");
+}
+
+MlpHost::MlpHost(uint32_t n_input_dims, uint32_t n_output_dims, const json& net) {
+	otype = jval<std::string>(net, "otype", "MLP");
+	TCNN_CHECK(ieq(otype, "FullyFusedMLP") || ieq(otype, "MegakernelMLP") || ieq(otype, "MLP") || ieq(otype, "CutlassMLP"),
+	           "Invalid network type: " + otype);
+	width = jval<uint32_t>(net, "n_neurons", 128u);
+	n_hidden_layers = jval<uint32_t>(net, "n_hidden_layers", 5u);
+	TCNN_CHECK(n_hidden_layers >= 1, "FullyFusedMLP requires at least 1 hidden layer (3 layers in total).");
+	if (ieq(otype, "FullyFusedMLP") || ieq(otype, "MegakernelMLP"))
+		TCNN_CHECK(width == 16 || width == 32 || width == 64 || width == 128,
+		           "FullyFusedMLP only supports 16, 32, 64, and 128 neurons, but got " + std::to_string(width) + ". Use CutlassMLP instead if this is a requirement.");
+	activation = parse_activation(jval<std::string>(net, "activation", "ReLU"));
+	output_activation = parse_activation(jval<std::string>(net, "output_activation", "None"));
+	n_input = n_input_dims;
+	n_output = n_output_dims;
+	padded_output = (n_output + 15) / 16 * 16;  // REQUIRED_ALIGNMENT 16 (fully_fused_mlp.h:108-110)
+}
+
+static void xavier(Pcg32& rnd, uint32_t rows, uint32_t cols, float* out, float scale) {
+	scale *= std::sqrt(6.0f / (float)(cols + rows));
+	const size_t n = (size_t)rows * cols;
+	for (size_t i = 0; i < n; ++i) {
+		float t = rnd.next_float() * 2.0f;
+		t = t * scale;
+		out[i] = t - scale;
+	}
+}
+
+void MlpHost::initialize_params(Pcg32& rng, float* out, float scale) const {
+	xavier(rng, width, n_input, out, scale);
+	out += (size_t)width * n_input;
+	for (uint32_t i = 1; i < n_hidden_layers; ++i) {
+		xavier(rng, width, width, out, scale);
+		out += (size_t)width * width;
+	}
+	xavier(rng, padded_output, width, out, scale);
+}
+
+static const char* act_str(int a) { return a == 1 ? "ReLU" : "None"; }
+
+json MlpHost::hyperparams() const {
+	return {{"otype", ieq(otype, "CutlassMLP") || ieq(otype, "MLP") ? "CutlassMLP" : "FullyFusedMLP"},
+	        {"n_neurons", width}, {"n_hidden_layers", n_hidden_layers},
+	        {"activation", act_str(activation)}, {"output_activation", act_str(output_activation)}};
+}
+
+void AdamHost::update(const json& p) {  // adam.h:235-283
+	if (jhas(p, "beta1")) beta1 = p["beta1"].get<float>();
+	if (jhas(p, "beta2")) beta2 = p["beta2"].get<float>();
+	if (jhas(p, "epsilon")) epsilon = p["epsilon"].get<float>();
+	if (jhas(p, "learning_rate")) learning_rate = p["learning_rate"].get<float>();
+	if (jhas(p, "l2_reg")) l2_reg = p["l2_reg"].get<float>();
+	if (jhas(p, "adabound")) adabound = p["adabound"].get<bool>();
+	if (jhas(p, "relative_decay")) relative_decay = p["relative_decay"].get<float>();
+	if (jhas(p, "absolute_decay")) absolute_decay = p["absolute_decay"].get<float>();
+	if (jhas(p, "clipping_magnitude")) clipping_magnitude = p["clipping_magnitude"].get<float>();
+	if (jhas(p, "non_matrix_learning_rate_factor")) non_matrix_learning_rate_factor = p["non_matrix_learning_rate_factor"].get<float>();
+	if (jhas(p, "optimize_matrix_params")) optimize_matrix_params = p["optimize_matrix_params"].get<bool>();
+	if (jhas(p, "optimize_non_matrix_params")) optimize_non_matrix_params = p["optimize_non_matrix_params"].get<bool>();
+}
+
+json AdamHost::hyperparams() const {
+	return {{"otype", "Adam"}, {"beta1", beta1}, {"beta2", beta2}, {"epsilon", epsilon}, {"learning_rate", learning_rate},
+	        {"l2_reg", l2_reg}, {"adabound", adabound}, {"relative_decay", relative_decay}, {"absolute_decay", absolute_decay},
+	        {"clipping_magnitude", clipping_magnitude}, {"non_matrix_learning_rate_factor", non_matrix_learning_rate_factor},
+	        {"optimize_matrix_params", optimize_matrix_params}, {"optimize_non_matrix_params", optimize_non_matrix_params}};
+}
+
+// ------------------------------------------------------------------------------------------
+// NetworkWithInputEncoding (grid + fused MLP)
+// ------------------------------------------------------------------------------------------
+NetworkWithGridHost::NetworkWithGridHost(uint32_t n_in, uint32_t n_out, const json& enc, const json& net)
+	: n_input_dims(n_in), n_output_dims(n_out) {
+	const std::string eo = jval<std::string>(enc, "otype", "OneBlob");
+	TCNN_CHECK(ieq(eo, "HashGrid") || ieq(eo, "Grid") || ieq(eo, "TiledGrid") || ieq(eo, "DenseGrid"),
+	           "Encoding '" + eo + "' is not implemented by the MI355X engine yet (grid encodings only)");
+	grid = std::make_unique<GridEncodingHost>(n_in, enc);
+	grid->set_alignment(16);  // minimum_alignment(network) for FullyFusedMLP (network.cu:76-95)
+	mlp = MlpHost(grid->padded_output_width(), n_out, net);
+}
+
+bool NetworkWithGridHost::fused_ok() const {
+	return grid->n_to_pad == 0 && !grid->stochastic && mlp.output_activation == 0 &&
+	       fused_train_supported(mlp.width, mlp.n_input, mlp.n_hidden_layers, grid->desc.n_pos_dims,
+	                             grid->desc.n_features_per_level, mlp.padded_output, mlp.activation, grid->desc.hash_type);
+}
+
+void NetworkWithGridHost::initialize_params(Pcg32& rng, float* out, float scale) const {
+	mlp.initialize_params(rng, out, scale);
+	grid->initialize_params(rng, out + mlp.n_params(), scale);
+}
+
+json NetworkWithGridHost::hyperparams() const {
+	return {{"otype", "NetworkWithInputEncoding"}, {"encoding", grid->hyperparams()}, {"network", mlp.hyperparams()}};
+}
+
+void NetworkWithGridHost::inference(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const void* params16, void* out16) {
+	TCNN_CHECK(B % 16 == 0, "inference: batch must be a multiple of 16");
+	TCNN_CHECK(mlp_infer_supported(mlp.width, mlp.n_input, mlp.n_hidden_layers, mlp.padded_output, mlp.activation) && grid->n_to_pad == 0 &&
+	           mlp.output_activation == 0, "inference: network shape not supported by the MI355X engine yet");
+	const uint32_t IN = mlp.n_input;
+	ws.enc16.reserve((size_t)IN * B * 2);
+	const uint8_t* table = (const uint8_t*)params16 + (size_t)mlp.n_params() * 2;
+	launch_grid_fwd(st, grid->desc.n_pos_dims, grid->desc.n_features_per_level, grid->desc.hash_type, B, grid->desc.n_levels,
+	                pos, grid->desc.n_pos_dims, table, ws.enc16.p, true, 0, grid->dev_levels(), grid->hash_grid(), grid->desc.interp);
+	launch_mlp_infer(st, mlp.width, IN, mlp.n_hidden_layers, mlp.activation, true, B, params16, ws.enc16.p, out16);
+}
+
+void NetworkWithGridHost::fwd_bwd(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target,
+                                  uint32_t dims, float loss_scale, const void* params16, const void* dout16, void* out16, float* grad32,
+                                  const std::function<void(int)>& mark) {
+	TCNN_CHECK(fused_ok(), "training: network/encoding configuration not supported by the MI355X fused engine yet");
+	TCNN_CHECK(B % 32 == 0, "training: batch must be a multiple of 32");
+	const uint32_t n_mlp = mlp.n_params();
+	const uint32_t L = grid->desc.n_levels, F = grid->desc.n_features_per_level;
+	const uint32_t nb = fused_train_n_blocks(B);
+	ws.n_fused_blocks = nb;
+	ws.dLdenc.reserve((size_t)L * F * B * 2);
+	ws.wgrad_partial.reserve((size_t)nb * n_mlp * 4);
+	ws.loss_partial.reserve((size_t)nb * 4);
+	const uint32_t n_slices = (uint32_t)grid->slices.size();
+	uint32_t n_chunks = std::max(1u, 512u / n_slices);
+	n_chunks = std::min(n_chunks, std::max(1u, B / 4096));
+	ws.n_grid_chunks = n_chunks;
+	ws.grid_partial.reserve((size_t)n_chunks * grid->n_params * 4);
+
+	const uint8_t* table = (const uint8_t*)params16 + (size_t)n_mlp * 2;
+	launch_fused_train(st, mlp.width, mlp.n_input, mlp.n_hidden_layers, grid->desc.n_pos_dims, grid->desc.hash_type,
+	                   mlp.activation, B, dims, loss_scale, params16, table, pos, target, out16, ws.dLdenc.p,
+	                   ws.wgrad_partial.as<float>(), ws.loss_partial.as<float>(), grid->dev_levels(), grid->hash_grid(),
+	                   grid->desc.interp, nb, dout16);
+	if (mark) mark(1);
+	launch_reduce_partials(st, ws.wgrad_partial.as<float>(), nb, n_mlp, n_mlp, grad32);
+	if (mark) mark(2);
+	launch_grid_bwd(st, grid->desc.n_pos_dims, F, grid->desc.hash_type, B, pos, grid->desc.n_pos_dims, ws.dLdenc.p, 0, 0,
+	                grid->d_slices.as<GridSlice>(), n_slices, n_chunks, ws.grid_partial.as<float>(), grid->n_params,
+	                grid->dev_levels(), grid->hash_grid(), grid->desc.interp);
+	if (mark) mark(3);
+	launch_reduce_partials(st, ws.grid_partial.as<float>(), n_chunks, grid->n_params, grid->n_params, grad32 + n_mlp);
+	if (mark) mark(4);
+}
+
+// ------------------------------------------------------------------------------------------
+// Trainer (reference trainer.h:47-361, config.h:46-63)
+// ------------------------------------------------------------------------------------------
+TrainerHost::TrainerHost(uint32_t n_in, uint32_t n_out, const json& cfg, uint32_t seed)
+	: n_input_dims(n_in), n_output_dims(n_out), config(cfg) {
+	const json enc = jhas(cfg, "encoding") ? cfg["encoding"] : json::object();
+	const json net = jhas(cfg, "network") ? cfg["network"] : json::object();
+	const json opt = jhas(cfg, "optimizer") ? cfg["optimizer"] : json::object();
+	const json los = jhas(cfg, "loss") ? cfg["loss"] : json::object();
+	loss_otype = jval<std::string>(los, "otype", "RelativeL2");
+	TCNN_CHECK(ieq(loss_otype, "RelativeL2"), "Loss '" + loss_otype + "' is not implemented by the MI355X engine yet");
+	const std::string oo = jval<std::string>(opt, "otype", "Adam");
+	TCNN_CHECK(ieq(oo, "Adam"), "Optimizer '" + oo + "' is not implemented by the MI355X engine yet");
+	adam.update(opt);
+	model = std::make_unique<NetworkWithGridHost>(n_in, n_out, enc, net);
+	n_params = model->n_params();
+	n_mlp = model->mlp.n_params();
+	initialize_params(seed);
+}
+
+void TrainerHost::initialize_params(uint32_t seed) {
+	// trainer.h:52-55: pcg32{seed_seq{seed}.generate()[0]}
+	std::seed_seq seq{seed};
+	std::vector<uint32_t> seeds(2);
+	seq.generate(seeds.begin(), seeds.end());
+	Pcg32 rng{seeds.front()};
+	std::vector<float> host(n_params);
+	model->initialize_params(rng, host.data());
+	w32.reserve(n_params * 4);
+	w16.reserve(n_params * 2);
+	g16.reserve(n_params * 2);
+	g32.reserve(n_params * 4);
+	m1.reserve(n_params * 4);
+	m2.reserve(n_params * 4);
+	steps.reserve(n_params * 4);
+	d_loss.reserve(16);
+	TCNN_HIP_CHECK(hipMemcpy(w32.p, host.data(), n_params * 4, hipMemcpyHostToDevice));
+	TCNN_HIP_CHECK(hipMemset(g16.p, 0, n_params * 2));
+	TCNN_HIP_CHECK(hipMemset(g32.p, 0, n_params * 4));
+	TCNN_HIP_CHECK(hipMemset(m1.p, 0, n_params * 4));
+	TCNN_HIP_CHECK(hipMemset(m2.p, 0, n_params * 4));
+	TCNN_HIP_CHECK(hipMemset(steps.p, 0, n_params * 4));
+	TCNN_HIP_CHECK(hipMemset(d_loss.p, 0, 16));
+	launch_cast_f32_f16(nullptr, w32.as<float>(), w16.p, n_params);
+	TCNN_HIP_CHECK(hipDeviceSynchronize());
+	adam_step = 0;
+}
+
+void TrainerHost::set_params_full_precision(const float* host, uint64_t n) {
+	TCNN_CHECK(n == n_params, "Can't set fp params because buffer has the wrong size.");
+	TCNN_HIP_CHECK(hipMemcpy(w32.p, host, n * 4, hipMemcpyHostToDevice));
+	launch_cast_f32_f16(nullptr, w32.as<float>(), w16.p, n_params);
+	TCNN_HIP_CHECK(hipDeviceSynchronize());
+}
+
+void TrainerHost::training_step(hipStream_t st, uint32_t B, const float* input, const float* target, bool run_optimizer) {
+	TCNN_CHECK(B % BATCH_GRANULARITY == 0, "training_step: batch size must be a multiple of 256");
+	if (timer.enabled) timer.marks.push_back({-1, -1, -1, -1, -1, -1, -1});
+	mark(st, 0);
+	model->fwd_bwd(st, ws, B, input, target, n_output_dims, loss_scale, w16.p, nullptr, nullptr, g32.as<float>(),
+	               [&](int ph) { mark(st, ph); });
+	launch_sum(st, ws.loss_partial.as<float>(), ws.n_fused_blocks, d_loss.as<float>());
+	mark(st, 5);
+	last_B = B;
+	if (run_optimizer) optimizer_step(st);
+}
+
+hipEvent_t PhaseTimer::get() {
+	if (next == pool.size()) {
+		hipEvent_t e;
+		TCNN_HIP_CHECK(hipEventCreate(&e));
+		pool.push_back(e);
+	}
+	return pool[next++];
+}
+
+PhaseTimer::~PhaseTimer() {
+	for (auto e : pool) (void)hipEventDestroy(e);
+}
+
+void TrainerHost::mark(hipStream_t st, int phase) {
+	if (!timer.enabled || timer.marks.empty()) return;
+	const int idx = (int)timer.next;
+	TCNN_HIP_CHECK(hipEventRecord(timer.get(), st));
+	timer.marks.back()[phase] = idx;
+}
+
+void TrainerHost::profile_end(double* ms, uint32_t n_phases, uint32_t* n_steps) {
+	TCNN_HIP_CHECK(hipDeviceSynchronize());
+	const uint32_t P = std::min<uint32_t>(n_phases, PhaseTimer::N_PHASES);
+	for (uint32_t p = 0; p < n_phases; ++p) ms[p] = 0.0;
+	uint32_t counted = 0;
+	for (auto& m : timer.marks) {
+		bool ok = true;
+		for (uint32_t p = 0; p < P; ++p) {
+			if (m[p] < 0 || m[p + 1] < 0) { ok = false; break; }
+		}
+		if (!ok) continue;
+		for (uint32_t p = 0; p < P; ++p) {
+			float t = 0.0f;
+			TCNN_HIP_CHECK(hipEventElapsedTime(&t, timer.pool[m[p]], timer.pool[m[p + 1]]));
+			ms[p] += t;
+		}
+		++counted;
+	}
+	if (counted)
+		for (uint32_t p = 0; p < P; ++p) ms[p] /= counted;
+	if (n_steps) *n_steps = counted;
+	timer.enabled = false;
+	timer.reset();
+}
+
+void TrainerHost::optimizer_step(hipStream_t st) {  // AdamOptimizer::step, adam.h:150-188
+	++adam_step;
+	AdamArgs a{};
+	a.n = (uint32_t)n_params;
+	a.n_matrix = (uint32_t)n_mlp;  // layer_sizes() of the network only (grid.h:1084-1088)
+	a.loss_scale = loss_scale;
+	a.grad_scale = grad_scale;
+	a.lr = adam.learning_rate;
+	a.beta1 = adam.beta1;
+	a.beta2 = adam.beta2;
+	a.eps = adam.epsilon;
+	a.l2_reg = adam.l2_reg;
+	a.rel_decay = adam.relative_decay;
+	a.abs_decay = adam.absolute_decay;
+	a.clip = adam.clipping_magnitude;
+	a.nonmat_lr_factor = adam.non_matrix_learning_rate_factor;
+	a.lower_lr_bound = 0.0f;
+	a.upper_lr_bound = std::numeric_limits<float>::max();
+	if (adam.adabound) {
+		a.lower_lr_bound = 0.1f - 0.1f / ((1 - adam.beta2) * (float)adam_step + 1);
+		a.upper_lr_bound = 0.1f + 0.1f / ((1 - adam.beta2) * (float)adam_step);
+	}
+	a.opt_matrix = adam.optimize_matrix_params;
+	a.opt_nonmatrix = adam.optimize_non_matrix_params;
+	launch_adam(st, a, w32.as<float>(), w16.p, g32.as<float>(), g16.p, m1.as<float>(), m2.as<float>(), steps.as<uint32_t>());
+	mark(st, 6);
+}
+
+float TrainerHost::loss(hipStream_t st) {
+	float v = 0.0f;
+	TCNN_HIP_CHECK(hipMemcpyAsync(&v, d_loss.p, 4, hipMemcpyDeviceToHost, st));
+	TCNN_HIP_CHECK(hipStreamSynchronize(st));
+	return v;
+}
+
+void TrainerHost::inference(hipStream_t st, uint32_t B, const float* input, float* out) {
+	const uint32_t OUTP = model->mlp.padded_output;
+	ws.out16.reserve((size_t)B * OUTP * 2);
+	model->inference(st, ws, B, input, w16.p, ws.out16.p);
+	launch_trim_cast(st, B, OUTP, n_output_dims, ws.out16.p, out);
+}
+
+}  // namespace tcnn_amd

@@ -1,0 +1,154 @@
+// runtime.h -- host-side objects of the engine: JSON config -> grid encoding / fused MLP /
+// NetworkWithInputEncoding / Trainer, device buffers, workspace. The C-ABI (capi.cpp) and the
+// C++ template API (include/tiny-cuda-nn/*.h) are thin layers over these classes.
+#pragma once
+
+#include <json.hpp>
+
+#include <array>
+#include <functional>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "grid_device.h"
+#include "kernels.h"
+
+namespace tcnn_amd {
+
+using json = nlohmann::json;
+
+// ---- host PCG32 (same stream semantics as the reference's dependencies/pcg32/pcg32.h) ----
+struct Pcg32 {
+	uint64_t state = 0x853c49e6748fea9bULL, inc = 0xda3e39cb94b95bdbULL;
+	Pcg32() = default;
+	explicit Pcg32(uint64_t initstate, uint64_t initseq = 1u) { seed(initstate, initseq); }
+	void seed(uint64_t initstate, uint64_t initseq = 1u);
+	uint32_t next_uint();
+	float next_float();
+	void advance(int64_t delta);
+};
+
+// ---- grow-only device allocation ----
+struct DevBuf {
+	void* p = nullptr;
+	size_t bytes = 0;
+	DevBuf() = default;
+	DevBuf(const DevBuf&) = delete;
+	DevBuf& operator=(const DevBuf&) = delete;
+	~DevBuf();
+	void reserve(size_t n);  // contents are not preserved
+	void release();
+	template <typename T> T* as() const { return (T*)p; }
+};
+
+bool ieq(const std::string& a, const std::string& b);
+
+// ---- multiresolution grid (reference encodings/grid.h:652-1208) ----
+struct GridEncodingHost {
+	GridDesc desc{};
+	uint32_t n_features = 0;     // L * F
+	uint32_t n_to_pad = 0;       // alignment padding (reference set_padded_output_width)
+	uint32_t n_params = 0;       // offset[L] * F
+	bool stochastic = false;
+	std::vector<LevelInfo> levels;
+	std::vector<GridSlice> slices;
+	DevBuf d_levels, d_slices;
+
+	GridEncodingHost(uint32_t n_dims_to_encode, const json& enc);
+	uint32_t padded_output_width() const { return n_features + n_to_pad; }
+	void set_alignment(uint32_t a) { n_to_pad = (n_features + a - 1) / a * a - n_features; }
+	bool hash_grid() const { return desc.grid_type == GridType::Hash; }
+	// GridEncodingTemplated::initialize_params (grid.h:1059-1062) -> host fp32
+	void initialize_params(Pcg32& rng, float* host_out, float scale = 1.0f) const;
+	json hyperparams() const;
+	const LevelInfo* dev_levels() const { return d_levels.as<LevelInfo>(); }
+};
+
+// ---- fully fused MLP shape (reference networks/fully_fused_mlp.h) ----
+struct MlpHost {
+	uint32_t width = 64, n_input = 32, n_hidden_layers = 2, n_output = 16, padded_output = 16;
+	int activation = 1, output_activation = 0;
+	std::string otype = "FullyFusedMLP";
+	MlpHost() = default;
+	MlpHost(uint32_t n_input_dims, uint32_t n_output_dims, const json& net);
+	uint32_t n_params() const { return width * n_input + (n_hidden_layers - 1) * width * width + padded_output * width; }
+	void initialize_params(Pcg32& rng, float* host_out, float scale = 1.0f) const;  // Xavier (gpu_matrix.h:284-299)
+	json hyperparams() const;
+};
+
+struct AdamHost {
+	float learning_rate = 1e-3f, beta1 = 0.9f, beta2 = 0.999f, epsilon = 1e-8f, l2_reg = 1e-8f;
+	float relative_decay = 0.0f, absolute_decay = 0.0f, clipping_magnitude = 0.0f, non_matrix_learning_rate_factor = 1.0f;
+	bool adabound = false, optimize_matrix_params = true, optimize_non_matrix_params = true;
+	void update(const json& p);
+	json hyperparams() const;
+};
+
+// Workspace for one fused fwd/bwd over a batch of B (sizes grow only).
+struct StepWorkspace {
+	DevBuf dLdenc, wgrad_partial, loss_partial, grid_partial, grad32_tmp, out16, enc16;
+	uint32_t n_fused_blocks = 0, n_grid_chunks = 0;
+};
+
+// NetworkWithInputEncoding<__half> with a grid encoding and the fused MLP
+// (reference network_with_input_encoding.h:41-190).
+struct NetworkWithGridHost {
+	std::unique_ptr<GridEncodingHost> grid;
+	MlpHost mlp;
+	uint32_t n_input_dims = 0, n_output_dims = 0;
+	NetworkWithGridHost(uint32_t n_in, uint32_t n_out, const json& enc, const json& net);
+	uint64_t n_params() const { return (uint64_t)mlp.n_params() + grid->n_params; }
+	bool fused_ok() const;
+	void initialize_params(Pcg32& rng, float* host_out, float scale = 1.0f) const;  // network first (nwie.h:124-130)
+
+	// params16: [mlp | grid] fp16. out16: fp16 [B][padded_output].
+	void inference(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const void* params16, void* out16);
+	// fused forward+backward; dout16 == nullptr -> RelativeL2 on target, else external dL/dout.
+	// Writes fp32 gradient sums into grad32 ([mlp | grid]) and the per-block loss partials.
+	void fwd_bwd(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target, uint32_t dims,
+	             float loss_scale, const void* params16, const void* dout16, void* out16, float* grad32,
+	             const std::function<void(int)>& mark = nullptr);
+	json hyperparams() const;
+};
+
+// Per-phase hipEvent timing of the training step (bench.py's live per-kernel roofline source).
+struct PhaseTimer {
+	static constexpr int N_PHASES = 6;  // fused fwd/bwd, wgrad reduce, grid bwd, grid reduce, loss sum, adam
+	bool enabled = false;
+	std::vector<hipEvent_t> pool;
+	std::vector<std::array<int, N_PHASES + 1>> marks;  // event indices per step (-1 = not recorded)
+	size_t next = 0;
+	hipEvent_t get();
+	void reset() { next = 0; marks.clear(); }
+	~PhaseTimer();
+};
+
+struct TrainerHost {
+	uint32_t n_input_dims, n_output_dims;
+	PhaseTimer timer;
+	json config;
+	std::unique_ptr<NetworkWithGridHost> model;
+	AdamHost adam;
+	std::string loss_otype;
+	uint64_t n_params = 0, n_mlp = 0;
+	DevBuf w32, w16, g16, g32, m1, m2, steps, d_loss;
+	StepWorkspace ws;
+	uint32_t adam_step = 0;
+	float grad_scale = 1.0f;
+	float loss_scale = 128.0f;  // default_loss_scale<__half> (common.h:232)
+	uint32_t last_B = 0;
+
+	TrainerHost(uint32_t n_in, uint32_t n_out, const json& cfg, uint32_t seed);
+	void initialize_params(uint32_t seed);
+	void training_step(hipStream_t st, uint32_t B, const float* input, const float* target, bool run_optimizer);
+	void optimizer_step(hipStream_t st);
+	float loss(hipStream_t st);
+	void inference(hipStream_t st, uint32_t B, const float* input, float* out);
+	void set_params_full_precision(const float* host, uint64_t n);
+	void mark(hipStream_t st, int phase);  // records phase boundary when timing is enabled
+	void profile_end(double* ms, uint32_t n_phases, uint32_t* n_steps);
+};
+
+}  // namespace tcnn_amd

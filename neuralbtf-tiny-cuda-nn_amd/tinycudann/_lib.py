@@ -1,0 +1,97 @@
+"""ctypes binding of the C-ABI (include/tcnn_mi355x.h) exported by lib/libtcnn_mi355x.so.
+
+The HIP library is the only compute path: if it is missing this module raises immediately (there is
+no CPU / eager-PyTorch fallback).
+"""
+import ctypes
+import os
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_PKG, "lib", "libtcnn_mi355x.so")
+
+_lib = None
+
+c_void_p, c_float, c_int, c_uint32, c_uint64, c_char_p = (
+    ctypes.c_void_p, ctypes.c_float, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_char_p)
+
+_SIGS = {
+    "tcnn_last_error": (c_char_p, []),
+    "tcnn_version": (c_char_p, []),
+    "tcnn_batch_size_granularity": (c_uint32, []),
+    "tcnn_cuda_device": (c_int, []),
+    "tcnn_set_cuda_device": (c_int, [c_int]),
+    "tcnn_free_temporary_memory": (None, []),
+    "tcnn_has_networks": (c_int, []),
+    "tcnn_default_loss_scale": (c_float, [c_int]),
+    "tcnn_preferred_precision": (c_int, []),
+    "tcnn_create_network_with_input_encoding": (c_void_p, [c_uint32, c_uint32, c_char_p, c_char_p]),
+    "tcnn_create_network": (c_void_p, [c_uint32, c_uint32, c_char_p]),
+    "tcnn_create_encoding": (c_void_p, [c_uint32, c_char_p, c_int]),
+    "tcnn_module_destroy": (None, [c_void_p]),
+    "tcnn_module_inference": (c_int, [c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_void_p]),
+    "tcnn_module_forward": (c_void_p, [c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_int]),
+    "tcnn_module_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "tcnn_context_destroy": (None, [c_void_p]),
+    "tcnn_module_n_input_dims": (c_uint32, [c_void_p]),
+    "tcnn_module_n_output_dims": (c_uint32, [c_void_p]),
+    "tcnn_module_n_params": (c_uint64, [c_void_p]),
+    "tcnn_module_param_precision": (c_int, [c_void_p]),
+    "tcnn_module_output_precision": (c_int, [c_void_p]),
+    "tcnn_module_initialize_params": (c_int, [c_void_p, c_uint64, c_void_p, c_float]),
+    "tcnn_module_hyperparams": (c_char_p, [c_void_p]),
+    "tcnn_module_name": (c_char_p, [c_void_p]),
+    "tcnn_trainer_create": (c_void_p, [c_uint32, c_uint32, c_char_p, c_uint32]),
+    "tcnn_trainer_destroy": (None, [c_void_p]),
+    "tcnn_trainer_training_step": (c_int, [c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_int]),
+    "tcnn_trainer_optimizer_step": (c_int, [c_void_p, c_void_p]),
+    "tcnn_trainer_loss": (c_float, [c_void_p, c_void_p]),
+    "tcnn_trainer_loss_device": (c_void_p, [c_void_p]),
+    "tcnn_trainer_inference": (c_int, [c_void_p, c_void_p, c_uint32, c_void_p, c_void_p]),
+    "tcnn_trainer_n_params": (c_uint64, [c_void_p]),
+    "tcnn_trainer_n_network_params": (c_uint64, [c_void_p]),
+    "tcnn_trainer_params_fp32": (c_void_p, [c_void_p]),
+    "tcnn_trainer_params": (c_void_p, [c_void_p]),
+    "tcnn_trainer_param_gradients": (c_void_p, [c_void_p]),
+    "tcnn_trainer_gradients_fp32": (c_void_p, [c_void_p]),
+    "tcnn_trainer_set_gradient_scale": (c_int, [c_void_p, c_float]),
+    "tcnn_trainer_set_params_full_precision": (c_int, [c_void_p, c_void_p, c_uint64]),
+    "tcnn_trainer_optimizer_step_count": (c_uint32, [c_void_p]),
+    "tcnn_trainer_engine": (c_char_p, [c_void_p]),
+    "tcnn_trainer_profile_begin": (c_int, [c_void_p]),
+    "tcnn_trainer_profile_end": (c_int, [c_void_p, c_void_p, c_uint32, c_void_p]),
+    "tcnn_debug_probe": (c_int, [c_void_p, c_void_p, c_void_p]),
+}
+
+
+class TcnnError(RuntimeError):
+    pass
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"tinycudann (MI355X): HIP library not built: {LIB_PATH} is missing. "
+                "Run `make -C neuralbtf-tiny-cuda-nn_amd` or __graft_entry__.build().")
+        _lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(_lib, name)
+            f.restype = res
+            f.argtypes = args
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS.keys())
+
+
+def check(rc):
+    if rc != 0:
+        raise TcnnError(lib().tcnn_last_error().decode())
+
+
+def check_ptr(p):
+    if not p:
+        raise TcnnError(lib().tcnn_last_error().decode())
+    return p

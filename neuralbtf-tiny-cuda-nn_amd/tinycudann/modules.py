@@ -1,0 +1,214 @@
+"""torch.nn front-end mirroring reference bindings/torch/tinycudann/modules.py:91-329 on top of the
+C-ABI runtime module (include/tcnn_mi355x.h, which replaces reference src/cpp_api.cu +
+bindings/torch/tinycudann/bindings.cpp)."""
+import ctypes
+import gc
+import json
+import warnings
+
+import torch
+
+from tinycudann import _lib as L
+
+if not torch.cuda.is_available():
+    raise EnvironmentError("Unknown compute capability. Ensure PyTorch with ROCm support and an MI355X are available.")
+
+PRECISION_FP32 = 0
+PRECISION_FP16 = 1
+
+
+def _torch_precision(p):
+    return torch.half if p == PRECISION_FP16 else torch.float
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def free_temporary_memory():
+    gc.collect()
+    L.lib().tcnn_free_temporary_memory()
+
+
+class _NativeModule:
+    """Python twin of bindings.cpp's Module class (bindings.cpp:75-171)."""
+
+    def __init__(self, handle):
+        self.h = L.check_ptr(handle)
+        lib = L.lib()
+        self.n_input_dims = lib.tcnn_module_n_input_dims(self.h)
+        self.n_output_dims = lib.tcnn_module_n_output_dims(self.h)
+        self.n_params = lib.tcnn_module_n_params(self.h)
+
+    def __del__(self):
+        try:
+            L.lib().tcnn_module_destroy(self.h)
+        except Exception:
+            pass
+
+    def param_precision(self):
+        return L.lib().tcnn_module_param_precision(self.h)
+
+    def output_precision(self):
+        return L.lib().tcnn_module_output_precision(self.h)
+
+    def hyperparams(self):
+        return json.loads(L.lib().tcnn_module_hyperparams(self.h).decode())
+
+    def name(self):
+        return L.lib().tcnn_module_name(self.h).decode()
+
+    def initial_params(self, seed):
+        p = torch.zeros(self.n_params, dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        L.check(L.lib().tcnn_module_initialize_params(self.h, seed, _ptr(p), 1.0))
+        return p
+
+    def fwd(self, input, params):
+        assert input.dtype == torch.float32 and input.is_contiguous() and input.shape[1] == self.n_input_dims
+        assert params.dtype == _torch_precision(self.param_precision()) and params.numel() == self.n_params
+        B = input.shape[0]
+        out = torch.empty(B, self.n_output_dims, dtype=_torch_precision(self.output_precision()), device=input.device)
+        if not (input.requires_grad or params.requires_grad):
+            L.check(L.lib().tcnn_module_inference(self.h, _stream(), B, _ptr(input), _ptr(out), _ptr(params)))
+            return None, out
+        ctx = L.check_ptr(L.lib().tcnn_module_forward(self.h, _stream(), B, _ptr(input), _ptr(out), _ptr(params),
+                                                       int(input.requires_grad)))
+        return _NativeContext(ctx), out
+
+    def bwd(self, ctx, input, params, output, dL_doutput):
+        B = input.shape[0]
+        dL_dinput = torch.empty_like(input) if input.requires_grad else None
+        dL_dparams = torch.empty(self.n_params, dtype=_torch_precision(self.param_precision()), device=input.device) if params.requires_grad else None
+        dL_doutput = dL_doutput.to(_torch_precision(self.output_precision())).contiguous()
+        L.check(L.lib().tcnn_module_backward(self.h, _stream(), ctx.h, B, _ptr(dL_dinput), _ptr(dL_doutput),
+                                             _ptr(dL_dparams), _ptr(input), _ptr(output), _ptr(params)))
+        return dL_dinput, dL_dparams
+
+
+class _NativeContext:
+    def __init__(self, h):
+        self.h = h
+
+    def __del__(self):
+        try:
+            L.lib().tcnn_context_destroy(self.h)
+        except Exception:
+            pass
+
+
+def null_tensor_like(tensor):
+    return torch.empty([], dtype=tensor.dtype, device=tensor.device)
+
+
+def null_tensor_to_none(tensor):
+    if len(tensor.shape) == 0:
+        return None
+    return tensor
+
+
+class _module_function(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, native_tcnn_module, input, params, loss_scale):
+        ctx.set_materialize_grads(False)
+        native_ctx, output = native_tcnn_module.fwd(input, params)
+        ctx.save_for_backward(input, params, output)
+        ctx.native_tcnn_module = native_tcnn_module
+        ctx.native_ctx = native_ctx
+        ctx.loss_scale = loss_scale
+        return output
+
+    @staticmethod
+    def backward(ctx, doutput):
+        if doutput is None:
+            return None, None, None, None
+        if not doutput.is_cuda:
+            warnings.warn("doutput must be a CUDA tensor, but isn't. This indicates suboptimal performance.")
+            doutput = doutput.cuda()
+        input, params, output = ctx.saved_tensors
+        with torch.no_grad():
+            scaled_grad = doutput * ctx.loss_scale
+            input_grad, params_grad = ctx.native_tcnn_module.bwd(ctx.native_ctx, input, params, output, scaled_grad)
+            input_grad = None if input_grad is None else (input_grad / ctx.loss_scale)
+            params_grad = None if params_grad is None else (params_grad / ctx.loss_scale)
+        return None, input_grad, params_grad, None
+
+
+class Module(torch.nn.Module):
+    def __init__(self, seed=1337):
+        super().__init__()
+        self.native_tcnn_module = self._native_tcnn_module()
+        self.dtype = _torch_precision(self.native_tcnn_module.param_precision())
+        self.seed = seed
+        initial_params = self.native_tcnn_module.initial_params(seed)
+        self.params = torch.nn.Parameter(initial_params, requires_grad=True)
+        self.register_parameter(name="params", param=self.params)
+        self.loss_scale = L.lib().tcnn_default_loss_scale(self.native_tcnn_module.param_precision())
+
+    def forward(self, x):
+        if not x.is_cuda:
+            warnings.warn("input must be a CUDA tensor, but isn't. This indicates suboptimal performance.")
+            x = x.cuda()
+        batch_size = x.shape[0]
+        g = int(L.lib().tcnn_batch_size_granularity())
+        padded = (batch_size + g - 1) // g * g
+        x_padded = x if batch_size == padded else torch.nn.functional.pad(x, [0, 0, 0, padded - batch_size])
+        output = _module_function.apply(
+            self.native_tcnn_module,
+            x_padded.to(torch.float).contiguous(),
+            self.params.to(_torch_precision(self.native_tcnn_module.param_precision())).contiguous(),
+            self.loss_scale,
+        )
+        return output[:batch_size, :self.n_output_dims]
+
+    def extra_repr(self):
+        return (f"n_input_dims={self.n_input_dims}, n_output_dims={self.n_output_dims}, seed={self.seed}, "
+                f"dtype={self.dtype}, hyperparams={self.native_tcnn_module.hyperparams()}")
+
+
+class NetworkWithInputEncoding(Module):
+    def __init__(self, n_input_dims, n_output_dims, encoding_config, network_config, seed=1337):
+        self.n_input_dims = n_input_dims
+        self.n_output_dims = n_output_dims
+        self.encoding_config = encoding_config
+        self.network_config = network_config
+        super().__init__(seed=seed)
+
+    def _native_tcnn_module(self):
+        return _NativeModule(L.lib().tcnn_create_network_with_input_encoding(
+            self.n_input_dims, self.n_output_dims, json.dumps(self.encoding_config).encode(),
+            json.dumps(self.network_config).encode()))
+
+
+class Network(Module):
+    def __init__(self, n_input_dims, n_output_dims, network_config, seed=1337):
+        self.n_input_dims = n_input_dims
+        self.n_output_dims = n_output_dims
+        self.network_config = network_config
+        super().__init__(seed=seed)
+
+    def _native_tcnn_module(self):
+        return _NativeModule(L.lib().tcnn_create_network(self.n_input_dims, self.n_output_dims,
+                                                          json.dumps(self.network_config).encode()))
+
+
+class Encoding(Module):
+    def __init__(self, n_input_dims, encoding_config, seed=1337, dtype=None):
+        self.n_input_dims = n_input_dims
+        self.encoding_config = encoding_config
+        if dtype is None or dtype == torch.float16:
+            self.precision = PRECISION_FP16
+        elif dtype == torch.float32:
+            self.precision = PRECISION_FP32
+        else:
+            raise ValueError(f"Encoding only supports fp32 or fp16 precision, but got {dtype}")
+        super().__init__(seed=seed)
+        self.n_output_dims = self.native_tcnn_module.n_output_dims
+
+    def _native_tcnn_module(self):
+        return _NativeModule(L.lib().tcnn_create_encoding(self.n_input_dims, json.dumps(self.encoding_config).encode(),
+                                                           self.precision))

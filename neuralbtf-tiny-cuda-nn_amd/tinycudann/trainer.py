@@ -1,0 +1,98 @@
+"""create_from_config() / Trainer front-end (reference include/tiny-cuda-nn/config.h:46-63,
+trainer.h:47-361) over the C-ABI tcnn_trainer_* entry points. Inputs/outputs are torch CUDA tensors
+(device memory); the stream is torch's current stream."""
+import ctypes
+import json
+
+from tinycudann import _lib as L
+
+
+def _stream(stream=None):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+class Trainer:
+    def __init__(self, n_input_dims, n_output_dims, config, seed=1337):
+        self.n_input_dims = n_input_dims
+        self.n_output_dims = n_output_dims
+        self.config = config
+        self.h = L.check_ptr(L.lib().tcnn_trainer_create(n_input_dims, n_output_dims, json.dumps(config).encode(), seed))
+        self.n_params = L.lib().tcnn_trainer_n_params(self.h)
+        self.n_network_params = L.lib().tcnn_trainer_n_network_params(self.h)
+
+    def __del__(self):
+        try:
+            L.lib().tcnn_trainer_destroy(self.h)
+        except Exception:
+            pass
+
+    @property
+    def engine(self):
+        return L.lib().tcnn_trainer_engine(self.h).decode()
+
+    def training_step(self, input, target, run_optimizer=True, stream=None):
+        """input: float32 [B, n_in] CUDA, target float32 [B, n_out] CUDA (contiguous)."""
+        assert input.is_contiguous() and target.is_contiguous()
+        L.check(L.lib().tcnn_trainer_training_step(self.h, _stream(stream), input.shape[0], ctypes.c_void_p(input.data_ptr()),
+                                                   ctypes.c_void_p(target.data_ptr()), int(run_optimizer)))
+
+    def optimizer_step(self, stream=None):
+        L.check(L.lib().tcnn_trainer_optimizer_step(self.h, _stream(stream)))
+
+    def loss(self, stream=None):
+        v = L.lib().tcnn_trainer_loss(self.h, _stream(stream))
+        if v < 0:
+            raise L.TcnnError(L.lib().tcnn_last_error().decode())
+        return v
+
+    def inference(self, input, stream=None):
+        import torch
+        out = torch.empty(input.shape[0], self.n_output_dims, dtype=torch.float32, device=input.device)
+        L.check(L.lib().tcnn_trainer_inference(self.h, _stream(stream), input.shape[0], ctypes.c_void_p(input.data_ptr()),
+                                               ctypes.c_void_p(out.data_ptr())))
+        return out
+
+    def set_gradient_scale(self, s):
+        L.check(L.lib().tcnn_trainer_set_gradient_scale(self.h, float(s)))
+
+    def set_params_full_precision(self, host_params):
+        import numpy as np
+        a = np.ascontiguousarray(host_params, dtype=np.float32)
+        L.check(L.lib().tcnn_trainer_set_params_full_precision(self.h, a.ctypes.data_as(ctypes.c_void_p), a.size))
+
+    @property
+    def optimizer_step_count(self):
+        return L.lib().tcnn_trainer_optimizer_step_count(self.h)
+
+    def _view(self, ptr, n, dtype):
+        """torch view of a trainer-owned device buffer (via __cuda_array_interface__)."""
+        import torch
+        typestr = {torch.float32: "<f4", torch.float16: "<f2", torch.int32: "<i4"}[dtype]
+
+        class _Iface:
+            __cuda_array_interface__ = {"shape": (n,), "typestr": typestr, "data": (ptr, False), "version": 2}
+
+        return torch.as_tensor(_Iface(), device="cuda")
+
+    def params_fp32(self):
+        import torch
+        return self._view(L.lib().tcnn_trainer_params_fp32(self.h), self.n_params, torch.float32)
+
+    def params(self):
+        import torch
+        return self._view(L.lib().tcnn_trainer_params(self.h), self.n_params, torch.float16)
+
+    def param_gradients(self):
+        import torch
+        return self._view(L.lib().tcnn_trainer_param_gradients(self.h), self.n_params, torch.float16)
+
+    def gradients_fp32(self):
+        import torch
+        return self._view(L.lib().tcnn_trainer_gradients_fp32(self.h), self.n_params, torch.float32)
+
+
+def create_from_config(n_input_dims, n_output_dims, config, seed=1337):
+    """TrainableModel equivalent: returns the Trainer (which owns loss, optimizer and network)."""
+    return Trainer(n_input_dims, n_output_dims, config, seed)

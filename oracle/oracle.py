@@ -1,0 +1,303 @@
+"""ctypes front-end of the CPU restatement (oracle/tcnn_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg, always as the checker / CPU baseline and never as the thing measured or shipped. The product
+package (neuralbtf-tiny-cuda-nn_amd/) never imports this module.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libtcnn_oracle.so")
+_lib = None
+
+MAX_LEVELS = 128
+
+
+class Pcg32(ctypes.Structure):
+    _fields_ = [("state", ctypes.c_uint64), ("inc", ctypes.c_uint64)]
+
+
+class GridCfg(ctypes.Structure):
+    _fields_ = [
+        ("n_pos_dims", ctypes.c_uint32), ("n_features_per_level", ctypes.c_uint32),
+        ("n_levels", ctypes.c_uint32), ("log2_hashmap_size", ctypes.c_uint32),
+        ("base_resolution", ctypes.c_uint32), ("per_level_scale", ctypes.c_float),
+        ("grid_type", ctypes.c_uint32), ("hash_type", ctypes.c_uint32), ("interpolation", ctypes.c_uint32),
+        ("offsets", ctypes.c_uint32 * (MAX_LEVELS + 1)), ("scales", ctypes.c_float * MAX_LEVELS),
+        ("res", ctypes.c_uint32 * MAX_LEVELS), ("n_params", ctypes.c_uint32),
+    ]
+
+
+class AdamCfg(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_float) for n in (
+        "learning_rate", "beta1", "beta2", "epsilon", "l2_reg", "relative_decay", "absolute_decay",
+        "clipping_magnitude", "non_matrix_learning_rate_factor")] + [
+        (n, ctypes.c_int) for n in ("adabound", "optimize_matrix_params", "optimize_non_matrix_params")]
+
+
+class Model(ctypes.Structure):
+    _fields_ = [
+        ("grid", GridCfg), ("W", ctypes.c_uint32), ("NH", ctypes.c_uint32), ("OUTP", ctypes.c_uint32),
+        ("n_output_dims", ctypes.c_uint32), ("activation", ctypes.c_uint32), ("adam", AdamCfg),
+        ("n_params", ctypes.c_uint32), ("n_mlp_params", ctypes.c_uint32), ("adam_step", ctypes.c_uint32),
+        ("w32", ctypes.POINTER(ctypes.c_float)), ("w16", ctypes.POINTER(ctypes.c_uint16)),
+        ("grad16", ctypes.POINTER(ctypes.c_uint16)), ("grad32", ctypes.POINTER(ctypes.c_float)),
+        ("m1", ctypes.POINTER(ctypes.c_float)), ("m2", ctypes.POINTER(ctypes.c_float)),
+        ("steps", ctypes.POINTER(ctypes.c_uint32)),
+    ]
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE], stdout=subprocess.DEVNULL)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        _lib = ctypes.CDLL(_LIB_PATH)
+        _lib.orc_h2f.restype = ctypes.c_float
+        _lib.orc_f2h.restype = ctypes.c_uint16
+        _lib.orc_f2h.argtypes = [ctypes.c_float]
+        _lib.orc_pcg32_next_float.restype = ctypes.c_float
+        _lib.orc_pcg32_next_uint.restype = ctypes.c_uint32
+        _lib.orc_pcg32_seed.argtypes = [ctypes.POINTER(Pcg32), ctypes.c_uint64, ctypes.c_uint64]
+        _lib.orc_pcg32_advance.argtypes = [ctypes.POINTER(Pcg32), ctypes.c_int64]
+        _lib.orc_generate_uniform.argtypes = [ctypes.POINTER(Pcg32), ctypes.c_size_t, ctypes.c_void_p, ctypes.c_float, ctypes.c_float]
+        _lib.orc_xavier_uniform.argtypes = [ctypes.POINTER(Pcg32), ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_float]
+        _lib.orc_grid_index.restype = ctypes.c_uint32
+        _lib.orc_grid_index.argtypes = [ctypes.POINTER(GridCfg), ctypes.c_uint32, ctypes.c_void_p]
+        _lib.orc_coherent_prime_hash.restype = ctypes.c_uint32
+        _lib.orc_coherent_prime_hash.argtypes = [ctypes.c_uint32, ctypes.c_void_p]
+        _lib.orc_grid_fwd.argtypes = [ctypes.POINTER(GridCfg), ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        _lib.orc_grid_bwd.argtypes = [ctypes.POINTER(GridCfg), ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        _lib.orc_mlp_n_params.restype = ctypes.c_uint32
+        _lib.orc_mlp_fwd.argtypes = [ctypes.c_uint32] * 5 + [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int,
+                                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        _lib.orc_mlp_bwd.argtypes = [ctypes.c_uint32] * 5 + [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int,
+                                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        _lib.orc_relative_l2.restype = ctypes.c_double
+        _lib.orc_relative_l2.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_float,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        _lib.orc_adam_step.argtypes = [ctypes.POINTER(AdamCfg), ctypes.c_uint32, ctypes.c_uint32, ctypes.c_float, ctypes.c_uint32] + [ctypes.c_void_p] * 6
+        _lib.orc_model_init.argtypes = [ctypes.POINTER(Model), ctypes.c_uint32]
+        _lib.orc_model_free.argtypes = [ctypes.POINTER(Model)]
+        _lib.orc_train_step.restype = ctypes.c_double
+        _lib.orc_train_step.argtypes = [ctypes.POINTER(Model), ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        _lib.orc_model_inference.argtypes = [ctypes.POINTER(Model), ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        _lib.orc_seed_seq.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
+        _lib.orc_hfma.restype = ctypes.c_uint16
+        _lib.orc_hfma.argtypes = [ctypes.c_uint16] * 3
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+# ---------------------------------------------------------------------------------------------
+# config helpers (JSON keys / defaults as in grid.h:1143-1208, src/network.cu:97-138, adam.h)
+# ---------------------------------------------------------------------------------------------
+GRID_TYPES = {"hash": 0, "dense": 1, "tiled": 2}
+HASH_TYPES = {"prime": 0, "coherentprime": 1, "reversedprime": 2}
+INTERP = {"nearest": 0, "linear": 1, "smoothstep": 2}
+
+
+def grid_cfg(enc, n_pos_dims):
+    g = GridCfg()
+    otype = enc.get("otype", "Grid").lower()
+    default_type = "tiled" if otype == "tiledgrid" else ("dense" if otype == "densegrid" else "hash")
+    F = int(enc.get("n_features_per_level", 2))
+    L = int(enc.get("n_levels", 16))
+    base = int(enc.get("base_resolution", 16))
+    gtype = enc.get("type", default_type).lower()
+    if gtype == "dense":
+        default_scale = float(np.exp(np.log(np.float32(256.0) / np.float32(base)) / (L - 1)))
+    else:
+        default_scale = 2.0
+    g.n_pos_dims = n_pos_dims
+    g.n_features_per_level = F
+    g.n_levels = L
+    g.log2_hashmap_size = int(enc.get("log2_hashmap_size", 19))
+    g.base_resolution = base
+    g.per_level_scale = float(enc.get("per_level_scale", default_scale))
+    g.grid_type = GRID_TYPES[gtype]
+    g.hash_type = HASH_TYPES[enc.get("hash", "CoherentPrime").lower()]
+    g.interpolation = INTERP[enc.get("interpolation", "Linear").lower()]
+    assert lib().orc_grid_init(ctypes.byref(g)) == 0
+    return g
+
+
+def adam_cfg(opt):
+    c = AdamCfg()
+    lib().orc_adam_default(ctypes.byref(c))
+    keys = {"learning_rate": "learning_rate", "beta1": "beta1", "beta2": "beta2", "epsilon": "epsilon",
+            "l2_reg": "l2_reg", "relative_decay": "relative_decay", "absolute_decay": "absolute_decay",
+            "clipping_magnitude": "clipping_magnitude",
+            "non_matrix_learning_rate_factor": "non_matrix_learning_rate_factor"}
+    for k, f in keys.items():
+        if k in opt:
+            setattr(c, f, float(opt[k]))
+    for k in ("adabound", "optimize_matrix_params", "optimize_non_matrix_params"):
+        if k in opt:
+            setattr(c, k, int(bool(opt[k])))
+    return c
+
+
+# ---------------------------------------------------------------------------------------------
+# numpy-level wrappers
+# ---------------------------------------------------------------------------------------------
+def f2h(x):
+    """fp32 -> fp16 bits (RNE), as uint16 array"""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.empty(x.shape, dtype=np.uint16)
+    lib().orc_f2h_array(_p(x), _p(out), ctypes.c_size_t(x.size))
+    return out
+
+
+def h2f(h):
+    h = np.ascontiguousarray(h, dtype=np.uint16)
+    out = np.empty(h.shape, dtype=np.float32)
+    lib().orc_h2f_array(_p(h), _p(out), ctypes.c_size_t(h.size))
+    return out
+
+
+def seed_seq(seeds, n_out):
+    s = np.ascontiguousarray(seeds, dtype=np.uint32)
+    out = np.empty(n_out, dtype=np.uint32)
+    lib().orc_seed_seq(_p(s), len(s), _p(out), n_out)
+    return out
+
+
+def pcg32(initstate, initseq=1):
+    r = Pcg32()
+    lib().orc_pcg32_seed(ctypes.byref(r), initstate, initseq)
+    return r
+
+
+def generate_uniform(rng, n, lo=0.0, hi=1.0):
+    out = np.empty(n, dtype=np.float32)
+    lib().orc_generate_uniform(ctypes.byref(rng), n, _p(out), lo, hi)
+    return out
+
+
+def grid_fwd(g, pos, table16):
+    """pos: float32 [B, D] (CM), table16 uint16 [n_params] -> enc uint16 [L*F, B] (SoA)"""
+    pos = np.ascontiguousarray(pos, dtype=np.float32)
+    B = pos.shape[0]
+    table16 = np.ascontiguousarray(table16, dtype=np.uint16)
+    enc = np.empty((g.n_levels * g.n_features_per_level, B), dtype=np.uint16)
+    lib().orc_grid_fwd(ctypes.byref(g), B, _p(pos), _p(table16), _p(enc))
+    return enc
+
+
+def grid_bwd(g, pos, dL_dy16):
+    pos = np.ascontiguousarray(pos, dtype=np.float32)
+    B = pos.shape[0]
+    dL_dy16 = np.ascontiguousarray(dL_dy16, dtype=np.uint16)
+    grad = np.zeros(g.n_params, dtype=np.float32)
+    lib().orc_grid_bwd(ctypes.byref(g), B, _p(pos), _p(dL_dy16), _p(grad))
+    return grad
+
+
+def mlp_n_params(W, IN, NH, OUTP):
+    return lib().orc_mlp_n_params(W, IN, NH, OUTP)
+
+
+def mlp_fwd(W, IN, NH, OUTP, params16, x16, input_soa=True, activation=1, want_hidden=True, n_threads=1):
+    x16 = np.ascontiguousarray(x16, dtype=np.uint16)
+    B = x16.shape[1] if input_soa else x16.shape[0]
+    out = np.empty((B, OUTP), dtype=np.uint16)
+    hidden = np.empty((NH, B, W), dtype=np.uint16) if want_hidden else None
+    lib().orc_mlp_fwd(W, IN, NH, OUTP, activation, _p(np.ascontiguousarray(params16, dtype=np.uint16)), B, _p(x16),
+                      int(input_soa), _p(out), _p(hidden) if hidden is not None else None, n_threads)
+    return out, hidden
+
+
+def mlp_bwd(W, IN, NH, OUTP, params16, x16, hidden16, dout16, input_soa=True, activation=1, want_dinput=True, n_threads=1):
+    x16 = np.ascontiguousarray(x16, dtype=np.uint16)
+    B = x16.shape[1] if input_soa else x16.shape[0]
+    wgrad = np.zeros(mlp_n_params(W, IN, NH, OUTP), dtype=np.float32)
+    din = np.empty(x16.shape, dtype=np.uint16) if want_dinput else None
+    lib().orc_mlp_bwd(W, IN, NH, OUTP, activation, _p(np.ascontiguousarray(params16, dtype=np.uint16)), B, _p(x16),
+                      int(input_soa), _p(np.ascontiguousarray(hidden16)), _p(np.ascontiguousarray(dout16, dtype=np.uint16)),
+                      _p(wgrad), _p(din) if din is not None else None, n_threads)
+    return wgrad, din
+
+
+def relative_l2(pred16, target, loss_scale=128.0, want_values=False):
+    """pred16 uint16 [B, stride] CM; target float32 [B, dims]"""
+    pred16 = np.ascontiguousarray(pred16, dtype=np.uint16)
+    target = np.ascontiguousarray(target, dtype=np.float32)
+    B, stride = pred16.shape
+    dims = target.shape[1]
+    grads = np.empty_like(pred16)
+    values = np.empty((B, stride), dtype=np.float32) if want_values else None
+    s = lib().orc_relative_l2(B, stride, dims, loss_scale, _p(pred16), _p(target),
+                              _p(values) if values is not None else None, _p(grads))
+    return s, grads, values
+
+
+def adam_step(cfg, n_matrix, loss_scale, current_step, w32, w16, grad16, m1, m2, steps):
+    lib().orc_adam_step(ctypes.byref(cfg), len(w32), n_matrix, loss_scale, current_step,
+                        _p(w32), _p(w16), _p(grad16), _p(m1), _p(m2), _p(steps))
+
+
+class OracleModel:
+    """Trainer<float,__half,__half> over NetworkWithInputEncoding<Grid, FullyFusedMLP> on the CPU."""
+
+    def __init__(self, config, n_input_dims, n_output_dims, seed=1337):
+        self.m = Model()
+        enc, net, opt = config["encoding"], config["network"], config.get("optimizer", {})
+        self.m.grid = grid_cfg(enc, n_input_dims)
+        self.m.W = int(net.get("n_neurons", 128))
+        self.m.NH = int(net.get("n_hidden_layers", 5))
+        self.m.n_output_dims = n_output_dims
+        self.m.OUTP = (n_output_dims + 15) // 16 * 16
+        act = net.get("activation", "ReLU").lower()
+        self.m.activation = {"none": 0, "relu": 1}[act]
+        self.m.adam = adam_cfg(opt)
+        assert lib().orc_model_init(ctypes.byref(self.m), seed) == 0
+        self.n_params = self.m.n_params
+        self.n_mlp_params = self.m.n_mlp_params
+
+    def __del__(self):
+        try:
+            lib().orc_model_free(ctypes.byref(self.m))
+        except Exception:
+            pass
+
+    def _arr(self, ptr, dtype):
+        return np.ctypeslib.as_array(ptr, shape=(self.n_params,)).view(dtype)
+
+    @property
+    def w32(self):
+        return np.ctypeslib.as_array(self.m.w32, shape=(self.n_params,))
+
+    @property
+    def w16(self):
+        return np.ctypeslib.as_array(self.m.w16, shape=(self.n_params,))
+
+    @property
+    def grad16(self):
+        return np.ctypeslib.as_array(self.m.grad16, shape=(self.n_params,))
+
+    @property
+    def grad32(self):
+        return np.ctypeslib.as_array(self.m.grad32, shape=(self.n_params,))
+
+    def train_step(self, pos, target, run_optimizer=True, n_threads=1):
+        pos = np.ascontiguousarray(pos, dtype=np.float32)
+        target = np.ascontiguousarray(target, dtype=np.float32)
+        return lib().orc_train_step(ctypes.byref(self.m), pos.shape[0], _p(pos), _p(target), int(run_optimizer), n_threads)
+
+    def inference(self, pos, n_threads=1):
+        pos = np.ascontiguousarray(pos, dtype=np.float32)
+        out = np.empty((pos.shape[0], self.m.OUTP), dtype=np.uint16)
+        lib().orc_model_inference(ctypes.byref(self.m), pos.shape[0], _p(pos), _p(out), n_threads)
+        return out

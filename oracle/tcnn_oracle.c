@@ -1,0 +1,699 @@
+/*
+ * tcnn_oracle.c -- CPU restatement of the reference hot path. TEST INFRASTRUCTURE ONLY: the parity
+ * checker and the CPU baseline; never linked into the product. See tcnn_oracle.h for the contract.
+ *
+ * Compiled with -ffp-contract=off: every fused multiply-add below is an explicit fmaf() placed
+ * where nvcc (default --fmad=true, no --use_fast_math: reference CMakeLists.txt:225,
+ * bindings/torch/setup.py:110) contracts the reference's device expressions.
+ */
+#include "tcnn_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* ------------------------------------------------------------------------------------------ */
+/* fp16                                                                                        */
+/* ------------------------------------------------------------------------------------------ */
+
+uint16_t orc_f2h(float f) {
+	uint32_t x;
+	memcpy(&x, &f, 4);
+	uint32_t sign = (x >> 16) & 0x8000u;
+	uint32_t ax = x & 0x7fffffffu;
+	if (ax >= 0x7f800000u) { /* inf / nan */
+		return (uint16_t)(sign | 0x7c00u | (ax > 0x7f800000u ? 0x200u | ((ax >> 13) & 0x3ffu) : 0u));
+	}
+	if (ax >= 0x477ff000u) { /* rounds to >= 65520 -> inf */
+		return (uint16_t)(sign | 0x7c00u);
+	}
+	if (ax < 0x38800000u) { /* result is subnormal (or zero) in fp16: value < 2^-14 */
+		if (ax < 0x33000000u) { /* < 2^-25: rounds to zero (2^-25 exactly is a tie -> even 0) */
+			return (uint16_t)sign;
+		}
+		uint32_t e = ax >> 23;                 /* biased exponent, 102..112 */
+		uint32_t m = (ax & 0x7fffffu) | 0x800000u;
+		uint32_t shift = 126 - e;              /* value = m * 2^(e-150); half ulp unit 2^-24 */
+		uint32_t q = m >> shift;
+		uint32_t rem = m & ((1u << shift) - 1u);
+		uint32_t halfway = 1u << (shift - 1);
+		if (rem > halfway || (rem == halfway && (q & 1u))) q++;
+		return (uint16_t)(sign | q);
+	}
+	/* normal */
+	uint32_t e = (ax >> 23) - 112;           /* rebias 127 -> 15 */
+	uint32_t m = ax & 0x7fffffu;
+	uint32_t q = (e << 10) | (m >> 13);
+	uint32_t rem = m & 0x1fffu;
+	if (rem > 0x1000u || (rem == 0x1000u && (q & 1u))) q++; /* carry into exponent is correct */
+	return (uint16_t)(sign | q);
+}
+
+float orc_h2f(uint16_t h) {
+	uint32_t sign = ((uint32_t)h & 0x8000u) << 16;
+	uint32_t e = (h >> 10) & 0x1fu;
+	uint32_t m = h & 0x3ffu;
+	uint32_t x;
+	if (e == 0) {
+		if (m == 0) {
+			x = sign;
+		} else { /* subnormal: normalise */
+			int sh = 0;
+			while (!(m & 0x400u)) { m <<= 1; ++sh; }
+			m &= 0x3ffu;
+			x = sign | ((uint32_t)(113 - sh) << 23) | (m << 13);
+		}
+	} else if (e == 31) {
+		x = sign | 0x7f800000u | (m << 13);
+	} else {
+		x = sign | ((e + 112) << 23) | (m << 13);
+	}
+	float f;
+	memcpy(&f, &x, 4);
+	return f;
+}
+
+void orc_f2h_array(const float* in, uint16_t* out, size_t n) {
+	for (size_t i = 0; i < n; ++i) out[i] = orc_f2h(in[i]);
+}
+void orc_h2f_array(const uint16_t* in, float* out, size_t n) {
+	for (size_t i = 0; i < n; ++i) out[i] = orc_h2f(in[i]);
+}
+
+/* Round a double to fp16 (RNE). Used for the fp16 FMA emulation: a*b is exact in double and the
+ * sum with c is exact whenever the exponent gap is below ~30 bits (always the case for the
+ * grid's |w| <= 1 interpolation); the single rounding then equals __hfma/__hfma2. */
+static uint16_t d2h(double d) {
+	/* Convert via float only when that is exact; otherwise round directly. */
+	float f = (float)d;
+	if ((double)f == d) return orc_f2h(f);
+	/* d is not representable in fp32: decide rounding on the double. Find the two fp16
+	 * neighbours via the fp32-rounded value, then compare distances exactly in double. */
+	uint16_t h = orc_f2h(f);
+	double hv = (double)orc_h2f(h);
+	if (hv == d) return h;
+	/* neighbour in the direction of d */
+	uint16_t n;
+	int pos = d > hv;
+	int neg_sign = (h & 0x8000u) != 0;
+	if (h == 0x0000u || h == 0x8000u) {
+		n = (uint16_t)(pos ? 0x0001u : 0x8001u);
+	} else if (pos != neg_sign) {
+		n = (uint16_t)(h + 1);
+	} else {
+		n = (uint16_t)(h - 1);
+	}
+	double nv = (double)orc_h2f(n);
+	double dh = fabs(d - hv), dn = fabs(d - nv);
+	if (dn < dh) return n;
+	if (dn > dh) return h;
+	return (n & 1u) ? h : n; /* tie: even mantissa */
+}
+
+uint16_t orc_hfma(uint16_t a, uint16_t b, uint16_t c) {
+	return d2h((double)orc_h2f(a) * (double)orc_h2f(b) + (double)orc_h2f(c));
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* PCG32 -- dependencies/pcg32/pcg32.h:40-200                                                  */
+/* ------------------------------------------------------------------------------------------ */
+#define PCG32_MULT 0x5851f42d4c957f2dULL
+
+uint32_t orc_pcg32_next_uint(orc_pcg32* r) { /* pcg32.h:62-69 */
+	uint64_t old = r->state;
+	r->state = old * PCG32_MULT + r->inc;
+	uint32_t xorshifted = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+	uint32_t rot = (uint32_t)(old >> 59u);
+	return (xorshifted >> rot) | (xorshifted << ((~rot + 1u) & 31));
+}
+
+void orc_pcg32_seed(orc_pcg32* r, uint64_t initstate, uint64_t initseq) { /* pcg32.h:53-59 */
+	r->state = 0u;
+	r->inc = (initseq << 1u) | 1u;
+	orc_pcg32_next_uint(r);
+	r->state += initstate;
+	orc_pcg32_next_uint(r);
+}
+
+float orc_pcg32_next_float(orc_pcg32* r) { /* pcg32.h:100-110 */
+	uint32_t u = (orc_pcg32_next_uint(r) >> 9) | 0x3f800000u;
+	float f;
+	memcpy(&f, &u, 4);
+	return f - 1.0f;
+}
+
+void orc_pcg32_advance(orc_pcg32* r, int64_t delta_) { /* pcg32.h:139-158 */
+	uint64_t cur_mult = PCG32_MULT, cur_plus = r->inc, acc_mult = 1u, acc_plus = 0u;
+	uint64_t delta = (uint64_t)delta_;
+	while (delta > 0) {
+		if (delta & 1) {
+			acc_mult *= cur_mult;
+			acc_plus = acc_plus * cur_mult + cur_plus;
+		}
+		cur_plus = (cur_mult + 1) * cur_plus;
+		cur_mult *= cur_mult;
+		delta /= 2;
+	}
+	r->state = acc_mult * r->state + acc_plus;
+}
+
+void orc_seed_seq(const uint32_t* v, size_t s, uint32_t* b, size_t n) {
+	if (n == 0) return;
+	for (size_t i = 0; i < n; ++i) b[i] = 0x8b8b8b8bu;
+	size_t t = (n >= 623) ? 11 : (n >= 68) ? 7 : (n >= 39) ? 5 : (n >= 7) ? 3 : (n - 1) / 2;
+	size_t p = (n - t) / 2, q = p + t;
+	size_t m = (s + 1 > n) ? s + 1 : n;
+	for (size_t k = 0; k < m; ++k) {
+		uint32_t x = b[k % n] ^ b[(k + p) % n] ^ b[(k + n - 1) % n];
+		uint32_t r1 = 1664525u * (x ^ (x >> 27));
+		uint32_t r2;
+		if (k == 0) r2 = r1 + (uint32_t)s;
+		else if (k <= s) r2 = r1 + (uint32_t)(k % n) + v[k - 1];
+		else r2 = r1 + (uint32_t)(k % n);
+		b[(k + p) % n] += r1;
+		b[(k + q) % n] += r2;
+		b[k % n] = r2;
+	}
+	for (size_t k = m; k < m + n; ++k) {
+		uint32_t x = b[k % n] + b[(k + p) % n] + b[(k + n - 1) % n];
+		uint32_t r3 = 1566083941u * (x ^ (x >> 27));
+		uint32_t r4 = r3 - (uint32_t)(k % n);
+		b[(k + p) % n] ^= r3;
+		b[(k + q) % n] ^= r4;
+		b[k % n] = r4;
+	}
+}
+
+/* random.h:39-70. generate_random_kernel<T, RNG, 4>: thread i advances by 4i and writes
+ * out[i + n_threads*j]; n_threads = blocks*128 with blocks = ceil(ceil(n/4)/128). The transform
+ * `val * (upper - lower) + lower` is a device lambda -> nvcc contracts it to one fma. */
+void orc_generate_uniform(orc_pcg32* r, size_t n, float* out, float lo, float hi) {
+	const size_t n_gen = 4;
+	size_t n_thr_needed = (n + n_gen - 1) / n_gen;
+	size_t n_threads = ((n_thr_needed + 127) / 128) * 128;
+	float range = hi - lo;
+	for (size_t i = 0; i < n_thr_needed; ++i) {
+		orc_pcg32 rr = *r;
+		orc_pcg32_advance(&rr, (int64_t)(i * n_gen));
+		for (size_t j = 0; j < n_gen; ++j) {
+			size_t idx = i + n_threads * j;
+			if (idx >= n) break;
+			out[idx] = fmaf(orc_pcg32_next_float(&rr), range, lo);
+		}
+	}
+	orc_pcg32_advance(r, (int64_t)n);
+}
+
+/* gpu_matrix.h:284-299 (fan_in = cols, fan_out = rows, gpu_matrix.h:227-231). Host code: no
+ * contraction. */
+void orc_xavier_uniform(orc_pcg32* r, uint32_t rows, uint32_t cols, float* out, float scale) {
+	scale *= sqrtf(6.0f / (float)(cols + rows));
+	size_t n = (size_t)rows * cols;
+	for (size_t i = 0; i < n; ++i) {
+		float t = orc_pcg32_next_float(r) * 2.0f;
+		t = t * scale;
+		out[i] = t - scale;
+	}
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Grid encoding                                                                                */
+/* ------------------------------------------------------------------------------------------ */
+
+static uint32_t powi_u32(uint32_t base, uint32_t exp) {
+	uint32_t r = 1;
+	for (uint32_t i = 0; i < exp; ++i) r *= base;
+	return r;
+}
+
+/* GridEncodingTemplated constructor, grid.h:668-730; grid_scale/grid_resolution
+ * common_device.h:709-718. log2 is std::log2(float) on the host (grid.h:694, 784). */
+int orc_grid_init(orc_grid* g) {
+	uint32_t D = g->n_pos_dims, F = g->n_features_per_level, L = g->n_levels;
+	if (L > ORC_MAX_LEVELS || D < 1 || D > 7 || F == 0) return -1;
+	float log2_scale = log2f(g->per_level_scale);
+	uint32_t offset = 0;
+	for (uint32_t l = 0; l < L; ++l) {
+		float scale = exp2f((float)l * log2_scale) * (float)g->base_resolution - 1.0f;
+		uint32_t res = (uint32_t)ceilf(scale) + 1;
+		uint32_t max_params = 0xffffffffu / 2;
+		uint32_t params = powf((float)res, (float)D) > (float)max_params ? max_params : powi_u32(res, D);
+		params = (params + 7u) / 8u * 8u;
+		if (g->grid_type == ORC_GRID_TILED) {
+			uint32_t t = powi_u32(g->base_resolution, D);
+			if (t < params) params = t;
+		} else if (g->grid_type == ORC_GRID_HASH) {
+			uint32_t t = 1u << g->log2_hashmap_size;
+			if (t < params) params = t;
+		}
+		g->scales[l] = scale;
+		g->res[l] = res;
+		g->offsets[l] = offset;
+		offset += params;
+	}
+	g->offsets[L] = offset;
+	g->n_params = offset * F;
+	return 0;
+}
+
+/* common_device.h:631-655 */
+static const uint32_t PRIMES[7] = {1958374283u, 2654435761u, 805459861u, 3674653429u, 2097192037u, 1434869437u, 2165219737u};
+static const uint32_t COHERENT_PRIMES[7] = {1u, 2654435761u, 805459861u, 3674653429u, 2097192037u, 1434869437u, 2165219737u};
+static const uint32_t REVERSED_PRIMES[7] = {2165219737u, 1434869437u, 2097192037u, 3674653429u, 805459861u, 2654435761u, 1958374283u};
+
+uint32_t orc_coherent_prime_hash(uint32_t d, const uint32_t* pos_grid) {
+	uint32_t r = 0;
+	for (uint32_t i = 0; i < d; ++i) r ^= pos_grid[i] * COHERENT_PRIMES[i];
+	return r;
+}
+
+/* grid_index, common_device.h:690-707 */
+uint32_t orc_grid_index(const orc_grid* g, uint32_t level, const uint32_t* pos_grid) {
+	uint32_t size = g->offsets[level + 1] - g->offsets[level];
+	uint32_t res = g->res[level];
+	uint32_t stride = 1, index = 0;
+	for (uint32_t dim = 0; dim < g->n_pos_dims && stride <= size; ++dim) {
+		index += pos_grid[dim] * stride;
+		stride *= res;
+	}
+	if (g->grid_type == ORC_GRID_HASH && size < stride) {
+		const uint32_t* pr = g->hash_type == ORC_HASH_PRIME ? PRIMES
+			: g->hash_type == ORC_HASH_REVERSED_PRIME ? REVERSED_PRIMES : COHERENT_PRIMES;
+		uint32_t r = 0;
+		for (uint32_t i = 0; i < g->n_pos_dims; ++i) r ^= pos_grid[i] * pr[i];
+		index = r;
+	}
+	return index % size;
+}
+
+/* pos_fract, common_device.h:841-868 (identity or smoothstep interpolation) */
+static void pos_fract(float x, float scale, int smooth, float* pos, uint32_t* grid) {
+	float p = fmaf(scale, x, 0.5f);
+	float t = floorf(p);
+	*grid = (uint32_t)(int)t;
+	p -= t;
+	if (smooth) { /* smoothstep, common_device.h:801-803: v*v*(3-2v); nvcc contracts 3-2v */
+		p = p * p * fmaf(-2.0f, p, 3.0f);
+	}
+	*pos = p;
+}
+
+/* kernel_grid, grid.h:48-212 (encoded_positions part; dy_dx not restated here) */
+void orc_grid_fwd(const orc_grid* g, uint32_t B, const float* pos_in, const uint16_t* table, uint16_t* enc) {
+	const uint32_t D = g->n_pos_dims, F = g->n_features_per_level, L = g->n_levels;
+	for (uint32_t l = 0; l < L; ++l) {
+		const uint16_t* grid = table + (size_t)g->offsets[l] * F;
+		const float scale = g->scales[l];
+		for (uint32_t i = 0; i < B; ++i) {
+			float pos[8];
+			uint32_t pg[8], local[8];
+			for (uint32_t d = 0; d < D; ++d) pos_fract(pos_in[(size_t)i * D + d], scale, g->interpolation == ORC_INTERP_SMOOTHSTEP, &pos[d], &pg[d]);
+			uint16_t result[8] = {0};
+			if (g->interpolation == ORC_INTERP_NEAREST) {
+				uint32_t idx = orc_grid_index(g, l, pg) * F;
+				for (uint32_t f = 0; f < F; ++f) result[f] = grid[idx + f];
+			} else {
+				for (uint32_t c = 0; c < (1u << D); ++c) {
+					float w = 1.0f;
+					for (uint32_t d = 0; d < D; ++d) {
+						if ((c & (1u << d)) == 0) { w *= 1.0f - pos[d]; local[d] = pg[d]; }
+						else { w *= pos[d]; local[d] = pg[d] + 1; }
+					}
+					uint16_t wh = orc_f2h(w);
+					uint32_t idx = orc_grid_index(g, l, local) * F;
+					for (uint32_t f = 0; f < F; ++f) result[f] = orc_hfma(wh, grid[idx + f], result[f]);
+				}
+			}
+			for (uint32_t f = 0; f < F; ++f) enc[(size_t)(l * F + f) * B + i] = result[f];
+		}
+	}
+}
+
+/* kernel_grid_backward, grid.h:214-320, ideal precision (fp32 sums of exact products). */
+void orc_grid_bwd(const orc_grid* g, uint32_t B, const float* pos_in, const uint16_t* dL_dy, float* grad) {
+	const uint32_t D = g->n_pos_dims, F = g->n_features_per_level, L = g->n_levels;
+	for (uint32_t l = 0; l < L; ++l) {
+		float* gg = grad + (size_t)g->offsets[l] * F;
+		const float scale = g->scales[l];
+		for (uint32_t i = 0; i < B; ++i) {
+			float pos[8], dy[8];
+			uint32_t pg[8], local[8];
+			for (uint32_t d = 0; d < D; ++d) pos_fract(pos_in[(size_t)i * D + d], scale, g->interpolation == ORC_INTERP_SMOOTHSTEP, &pos[d], &pg[d]);
+			for (uint32_t f = 0; f < F; ++f) dy[f] = orc_h2f(dL_dy[(size_t)(l * F + f) * B + i]);
+			if (g->interpolation == ORC_INTERP_NEAREST) {
+				uint32_t idx = orc_grid_index(g, l, pg) * F;
+				for (uint32_t f = 0; f < F; ++f) gg[idx + f] += dy[f];
+				continue;
+			}
+			for (uint32_t c = 0; c < (1u << D); ++c) {
+				float w = 1.0f;
+				for (uint32_t d = 0; d < D; ++d) {
+					if ((c & (1u << d)) == 0) { w *= 1.0f - pos[d]; local[d] = pg[d]; }
+					else { w *= pos[d]; local[d] = pg[d] + 1; }
+				}
+				float wh = orc_h2f(orc_f2h(w));
+				uint32_t idx = orc_grid_index(g, l, local) * F;
+				for (uint32_t f = 0; f < F; ++f) gg[idx + f] += wh * dy[f];
+			}
+		}
+	}
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Fully fused MLP                                                                              */
+/* ------------------------------------------------------------------------------------------ */
+
+uint32_t orc_mlp_n_params(uint32_t W, uint32_t IN, uint32_t NH, uint32_t OUTP) {
+	return W * IN + (NH - 1) * W * W + OUTP * W;
+}
+
+static inline float act_fwd(uint32_t act, float x) { return act == 1 ? (x > 0.0f ? x : 0.0f) : x; }
+/* ReLU transfer from the post-activation value (common_device.h:240-297) */
+static inline int act_pass(uint32_t act, float y) { return act == 1 ? (y > 0.0f) : 1; }
+
+typedef struct {
+	uint32_t W, IN, NH, OUTP;
+	float* wf; /* fp32 copy of fp16 weights */
+	size_t off[64];
+} mlp_view;
+
+static void mlp_view_init(mlp_view* v, uint32_t W, uint32_t IN, uint32_t NH, uint32_t OUTP, const uint16_t* params) {
+	v->W = W; v->IN = IN; v->NH = NH; v->OUTP = OUTP;
+	size_t n = orc_mlp_n_params(W, IN, NH, OUTP);
+	v->wf = (float*)malloc(n * sizeof(float));
+	orc_h2f_array(params, v->wf, n);
+	size_t o = 0;
+	v->off[0] = 0; o += (size_t)W * IN;
+	for (uint32_t k = 1; k < NH; ++k) { v->off[k] = o; o += (size_t)W * W; }
+	v->off[NH] = o;
+}
+
+static inline float in_at(const uint16_t* input, int soa, uint32_t IN, uint32_t B, uint32_t i, uint32_t k) {
+	return orc_h2f(soa ? input[(size_t)k * B + i] : input[(size_t)i * IN + k]);
+}
+
+/* one sample forward; h: NH*W floats (fp16-rounded post-activations); out: OUTP fp16 */
+static void mlp_fwd_sample(const mlp_view* v, uint32_t act, const float* x, float* h, uint16_t* out) {
+	const uint32_t W = v->W, IN = v->IN, NH = v->NH, OUTP = v->OUTP;
+	const float* W0 = v->wf + v->off[0];
+	for (uint32_t n = 0; n < W; ++n) {
+		float acc = 0.0f;
+		for (uint32_t k = 0; k < IN; ++k) acc += W0[(size_t)n * IN + k] * x[k];
+		h[n] = orc_h2f(orc_f2h(act_fwd(act, acc)));
+	}
+	for (uint32_t l = 1; l < NH; ++l) {
+		const float* Wl = v->wf + v->off[l];
+		const float* hp = h + (size_t)(l - 1) * W;
+		float* hn = h + (size_t)l * W;
+		for (uint32_t n = 0; n < W; ++n) {
+			float acc = 0.0f;
+			for (uint32_t k = 0; k < W; ++k) acc += Wl[(size_t)n * W + k] * hp[k];
+			hn[n] = orc_h2f(orc_f2h(act_fwd(act, acc)));
+		}
+	}
+	const float* Wo = v->wf + v->off[NH];
+	const float* hl = h + (size_t)(NH - 1) * W;
+	for (uint32_t o = 0; o < OUTP; ++o) {
+		float acc = 0.0f;
+		for (uint32_t k = 0; k < W; ++k) acc += Wo[(size_t)o * W + k] * hl[k];
+		out[o] = orc_f2h(acc); /* output activation None */
+	}
+}
+
+void orc_mlp_fwd(uint32_t W, uint32_t IN, uint32_t NH, uint32_t OUTP, uint32_t act,
+                 const uint16_t* params, uint32_t B, const uint16_t* input, int input_soa,
+                 uint16_t* out, uint16_t* hidden, int n_threads) {
+	mlp_view v;
+	mlp_view_init(&v, W, IN, NH, OUTP, params);
+#ifdef _OPENMP
+	if (n_threads <= 0) n_threads = 1;
+#pragma omp parallel num_threads(n_threads)
+#endif
+	{
+		float* x = (float*)malloc(sizeof(float) * IN);
+		float* h = (float*)malloc(sizeof(float) * NH * W);
+#ifdef _OPENMP
+#pragma omp for schedule(static)
+#endif
+		for (int64_t ii = 0; ii < (int64_t)B; ++ii) {
+			uint32_t i = (uint32_t)ii;
+			for (uint32_t k = 0; k < IN; ++k) x[k] = in_at(input, input_soa, IN, B, i, k);
+			mlp_fwd_sample(&v, act, x, h, out + (size_t)i * OUTP);
+			if (hidden) {
+				for (uint32_t l = 0; l < NH; ++l)
+					for (uint32_t n = 0; n < W; ++n) hidden[(size_t)l * W * B + (size_t)i * W + n] = orc_f2h(h[(size_t)l * W + n]);
+			}
+		}
+		free(x); free(h);
+	}
+	free(v.wf);
+}
+
+/* backward of one sample: g fp16 dL/dout (OUTP), h hidden (NH*W). Accumulates wgrad (fp32),
+ * writes dx (fp16 rounded, IN) if dx != NULL. delta scratch: 2*W floats. */
+static void mlp_bwd_sample(const mlp_view* v, uint32_t act, const float* x, const float* h, const float* g,
+                           float* wgrad, float* dx, float* scratch) {
+	const uint32_t W = v->W, IN = v->IN, NH = v->NH, OUTP = v->OUTP;
+	float* d_cur = scratch;      /* delta of layer being processed (fp16-rounded) */
+	float* d_nxt = scratch + W;
+	/* output layer: dWout[o][k] += g[o] * h_last[k]; delta_H = act'(h_H) * Wout^T g */
+	const float* Wo = v->wf + v->off[NH];
+	const float* hl = h + (size_t)(NH - 1) * W;
+	float* gWo = wgrad + v->off[NH];
+	for (uint32_t o = 0; o < OUTP; ++o) {
+		if (g[o] == 0.0f) continue;
+		for (uint32_t k = 0; k < W; ++k) gWo[(size_t)o * W + k] += g[o] * hl[k];
+	}
+	for (uint32_t k = 0; k < W; ++k) {
+		float acc = 0.0f;
+		for (uint32_t o = 0; o < OUTP; ++o) acc += Wo[(size_t)o * W + k] * g[o];
+		d_cur[k] = act_pass(act, hl[k]) ? orc_h2f(orc_f2h(acc)) : 0.0f;
+	}
+	/* hidden layers, from the last to the first hidden matmul */
+	for (uint32_t l = NH - 1; l >= 1; --l) {
+		const float* Wl = v->wf + v->off[l];
+		const float* hin = h + (size_t)(l - 1) * W;
+		float* gWl = wgrad + v->off[l];
+		for (uint32_t n = 0; n < W; ++n) {
+			float dn = d_cur[n];
+			if (dn == 0.0f) continue;
+			for (uint32_t k = 0; k < W; ++k) gWl[(size_t)n * W + k] += dn * hin[k];
+		}
+		for (uint32_t k = 0; k < W; ++k) {
+			float acc = 0.0f;
+			for (uint32_t n = 0; n < W; ++n) acc += Wl[(size_t)n * W + k] * d_cur[n];
+			d_nxt[k] = act_pass(act, hin[k]) ? orc_h2f(orc_f2h(acc)) : 0.0f;
+		}
+		float* t = d_cur; d_cur = d_nxt; d_nxt = t;
+	}
+	/* first layer: dW0[n][k] += delta_1[n] * x[k]; dx = W0^T delta_1 */
+	const float* W0 = v->wf + v->off[0];
+	float* gW0 = wgrad + v->off[0];
+	for (uint32_t n = 0; n < W; ++n) {
+		float dn = d_cur[n];
+		if (dn == 0.0f) continue;
+		for (uint32_t k = 0; k < IN; ++k) gW0[(size_t)n * IN + k] += dn * x[k];
+	}
+	if (dx) {
+		for (uint32_t k = 0; k < IN; ++k) {
+			float acc = 0.0f;
+			for (uint32_t n = 0; n < W; ++n) acc += W0[(size_t)n * IN + k] * d_cur[n];
+			dx[k] = orc_h2f(orc_f2h(acc));
+		}
+	}
+}
+
+void orc_mlp_bwd(uint32_t W, uint32_t IN, uint32_t NH, uint32_t OUTP, uint32_t act,
+                 const uint16_t* params, uint32_t B, const uint16_t* input, int input_soa,
+                 const uint16_t* hidden, const uint16_t* dL_dout, float* wgrad,
+                 uint16_t* dL_dinput, int n_threads) {
+	mlp_view v;
+	mlp_view_init(&v, W, IN, NH, OUTP, params);
+	size_t np = orc_mlp_n_params(W, IN, NH, OUTP);
+	if (n_threads <= 0) n_threads = 1;
+	float* partial = (float*)calloc((size_t)n_threads * np, sizeof(float));
+#ifdef _OPENMP
+#pragma omp parallel num_threads(n_threads)
+#endif
+	{
+		int tid = 0;
+#ifdef _OPENMP
+		tid = omp_get_thread_num();
+#endif
+		float* wg = partial + (size_t)tid * np;
+		float* x = (float*)malloc(sizeof(float) * IN);
+		float* h = (float*)malloc(sizeof(float) * NH * W);
+		float* g = (float*)malloc(sizeof(float) * OUTP);
+		float* dx = (float*)malloc(sizeof(float) * IN);
+		float* scratch = (float*)malloc(sizeof(float) * 2 * W);
+#ifdef _OPENMP
+#pragma omp for schedule(static)
+#endif
+		for (int64_t ii = 0; ii < (int64_t)B; ++ii) {
+			uint32_t i = (uint32_t)ii;
+			for (uint32_t k = 0; k < IN; ++k) x[k] = in_at(input, input_soa, IN, B, i, k);
+			for (uint32_t l = 0; l < NH; ++l)
+				for (uint32_t n = 0; n < W; ++n) h[(size_t)l * W + n] = orc_h2f(hidden[(size_t)l * W * B + (size_t)i * W + n]);
+			for (uint32_t o = 0; o < OUTP; ++o) g[o] = orc_h2f(dL_dout[(size_t)i * OUTP + o]);
+			mlp_bwd_sample(&v, act, x, h, g, wg, dL_dinput ? dx : NULL, scratch);
+			if (dL_dinput) {
+				for (uint32_t k = 0; k < IN; ++k) {
+					uint16_t hv = orc_f2h(dx[k]);
+					if (input_soa) dL_dinput[(size_t)k * B + i] = hv; else dL_dinput[(size_t)i * IN + k] = hv;
+				}
+			}
+		}
+		free(x); free(h); free(g); free(dx); free(scratch);
+	}
+	for (size_t p = 0; p < np; ++p) {
+		float s = 0.0f;
+		for (int t = 0; t < n_threads; ++t) s += partial[(size_t)t * np + p];
+		wgrad[p] = s;
+	}
+	free(partial);
+	free(v.wf);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* RelativeL2 -- losses/relative_l2.h:40-76                                                     */
+/* ------------------------------------------------------------------------------------------ */
+double orc_relative_l2(uint32_t B, uint32_t stride, uint32_t dims, float loss_scale,
+                       const uint16_t* pred, const float* target, float* values, uint16_t* grads) {
+	const uint32_t n_elements = B * stride;
+	const uint32_t n_total = n_elements / stride * dims;
+	double sum = 0.0;
+	for (uint32_t i = 0; i < n_elements; ++i) {
+		uint32_t intra = i % stride, inter = i / stride;
+		if (intra >= dims) {
+			if (values) values[i] = 0.0f;
+			grads[i] = 0;
+			continue;
+		}
+		uint32_t ti = inter * dims + intra;
+		float p = orc_h2f(pred[i]);
+		float pse = fmaf(p, p, 0.01f);
+		float d = p - target[ti];
+		float val = d * d / pse / 1.0f / (float)n_total;
+		float gr = 2.0f * d / pse / 1.0f;
+		if (values) values[i] = val;
+		sum += val;
+		grads[i] = orc_f2h(loss_scale * gr / (float)n_total);
+	}
+	return sum;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Adam -- optimizers/adam.h:47-188                                                            */
+/* ------------------------------------------------------------------------------------------ */
+void orc_adam_default(orc_adam_cfg* c) { /* adam.h:309-325 */
+	c->learning_rate = 1e-3f; c->beta1 = 0.9f; c->beta2 = 0.999f; c->epsilon = 1e-8f; c->l2_reg = 1e-8f;
+	c->relative_decay = 0.0f; c->absolute_decay = 0.0f; c->clipping_magnitude = 0.0f;
+	c->non_matrix_learning_rate_factor = 1.0f;
+	c->adabound = 0; c->optimize_matrix_params = 1; c->optimize_non_matrix_params = 1;
+}
+
+void orc_adam_step(const orc_adam_cfg* c, uint32_t n, uint32_t n_matrix, float loss_scale,
+                   uint32_t current_step, float* w32, uint16_t* w16, const uint16_t* grad16,
+                   float* m1, float* m2, uint32_t* steps) {
+	float lower = 0.0f, upper = 3.402823466e+38f;
+	if (c->adabound) { /* adam.h:156-159 */
+		lower = 0.1f - 0.1f / ((1 - c->beta2) * (float)current_step + 1);
+		upper = 0.1f + 0.1f / ((1 - c->beta2) * (float)current_step);
+	}
+	for (uint32_t i = 0; i < n; ++i) {
+		float gradient = orc_h2f(grad16[i]) / loss_scale;
+		if (i >= n_matrix) {
+			if (!c->optimize_non_matrix_params || gradient == 0) continue;
+		} else {
+			if (!c->optimize_matrix_params) continue;
+		}
+		const float wfp = w32[i];
+		if (i < n_matrix) gradient = fmaf(c->l2_reg, wfp, gradient);
+		const float gsq = gradient * gradient;
+		const float mm1 = m1[i] = fmaf(c->beta1, m1[i], (1 - c->beta1) * gradient);
+		const float mm2 = m2[i] = fmaf(c->beta2, m2[i], (1 - c->beta2) * gsq);
+		float lr = c->learning_rate;
+		if (i >= n_matrix) lr *= c->non_matrix_learning_rate_factor;
+		const uint32_t st = ++steps[i];
+		lr *= sqrtf(1 - powf(c->beta2, (float)st)) / (1 - powf(c->beta1, (float)st));
+		const float eff = fminf(fmaxf(lr / (sqrtf(mm2) + c->epsilon), lower), upper);
+		/* weight_decay, common_device.h:870-873 */
+		const float decayed = fmaf(1 - c->relative_decay * lr, wfp, -copysignf(c->absolute_decay * lr, wfp));
+		float nw = fmaf(-eff, mm1, decayed);
+		if (c->clipping_magnitude != 0.0f) {
+			nw = fminf(fmaxf(nw, -c->clipping_magnitude), c->clipping_magnitude);
+		}
+		w32[i] = nw;
+		w16[i] = orc_f2h(nw);
+	}
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Trainer (trainer.h:50-190) for NetworkWithInputEncoding<Grid, FullyFusedMLP>                  */
+/* ------------------------------------------------------------------------------------------ */
+
+int orc_model_init(orc_model* m, uint32_t seed) {
+	if (orc_grid_init(&m->grid) != 0) return -1;
+	const uint32_t IN = m->grid.n_levels * m->grid.n_features_per_level;
+	m->n_mlp_params = orc_mlp_n_params(m->W, IN, m->NH, m->OUTP);
+	m->n_params = m->n_mlp_params + m->grid.n_params;
+	m->adam_step = 0;
+	size_t n = m->n_params;
+	m->w32 = (float*)calloc(n, 4); m->w16 = (uint16_t*)calloc(n, 2);
+	m->grad16 = (uint16_t*)calloc(n, 2); m->grad32 = (float*)calloc(n, 4);
+	m->m1 = (float*)calloc(n, 4); m->m2 = (float*)calloc(n, 4); m->steps = (uint32_t*)calloc(n, 4);
+	/* trainer.h:52-55: rng = pcg32{seed_seq{seed}[0]} */
+	uint32_t s[2];
+	orc_seed_seq(&seed, 1, s, 2);
+	orc_pcg32 rng;
+	orc_pcg32_seed(&rng, s[0], 1u);
+	/* NWIE::initialize_params (network_with_input_encoding.h:124-130): network first */
+	float* p = m->w32;
+	orc_xavier_uniform(&rng, m->W, IN, p, 1.0f); p += (size_t)m->W * IN;
+	for (uint32_t k = 1; k < m->NH; ++k) { orc_xavier_uniform(&rng, m->W, m->W, p, 1.0f); p += (size_t)m->W * m->W; }
+	orc_xavier_uniform(&rng, m->OUTP, m->W, p, 1.0f); p += (size_t)m->OUTP * m->W;
+	/* GridEncodingTemplated::initialize_params (grid.h:1059-1062) */
+	orc_generate_uniform(&rng, m->grid.n_params, p, -1e-4f, 1e-4f);
+	orc_f2h_array(m->w32, m->w16, n); /* trainer.h:83-85 */
+	return 0;
+}
+
+void orc_model_free(orc_model* m) {
+	free(m->w32); free(m->w16); free(m->grad16); free(m->grad32); free(m->m1); free(m->m2); free(m->steps);
+	memset(m, 0, sizeof(*m));
+}
+
+void orc_model_inference(orc_model* m, uint32_t B, const float* pos, uint16_t* out, int n_threads) {
+	const uint32_t IN = m->grid.n_levels * m->grid.n_features_per_level;
+	uint16_t* enc = (uint16_t*)malloc((size_t)IN * B * 2);
+	orc_grid_fwd(&m->grid, B, pos, m->w16 + m->n_mlp_params, enc);
+	orc_mlp_fwd(m->W, IN, m->NH, m->OUTP, m->activation, m->w16, B, enc, 1, out, NULL, n_threads);
+	free(enc);
+}
+
+double orc_train_step(orc_model* m, uint32_t B, const float* pos, const float* target, int run_optimizer, int n_threads) {
+	const uint32_t IN = m->grid.n_levels * m->grid.n_features_per_level;
+	const float loss_scale = 128.0f; /* default_loss_scale<__half> (common.h:232) */
+	uint16_t* enc = (uint16_t*)malloc((size_t)IN * B * 2);
+	uint16_t* out = (uint16_t*)malloc((size_t)m->OUTP * B * 2);
+	uint16_t* hidden = (uint16_t*)malloc((size_t)m->NH * m->W * B * 2);
+	uint16_t* dout = (uint16_t*)malloc((size_t)m->OUTP * B * 2);
+	uint16_t* denc = (uint16_t*)malloc((size_t)IN * B * 2);
+	orc_grid_fwd(&m->grid, B, pos, m->w16 + m->n_mlp_params, enc);
+	orc_mlp_fwd(m->W, IN, m->NH, m->OUTP, m->activation, m->w16, B, enc, 1, out, hidden, n_threads);
+	double loss = orc_relative_l2(B, m->OUTP, m->n_output_dims, loss_scale, out, target, NULL, dout);
+	orc_mlp_bwd(m->W, IN, m->NH, m->OUTP, m->activation, m->w16, B, enc, 1, hidden, dout, m->grad32, denc, n_threads);
+	memset(m->grad32 + m->n_mlp_params, 0, (size_t)m->grid.n_params * 4);
+	orc_grid_bwd(&m->grid, B, pos, denc, m->grad32 + m->n_mlp_params);
+	orc_f2h_array(m->grad32, m->grad16, m->n_params);
+	if (run_optimizer) {
+		m->adam_step++;
+		orc_adam_step(&m->adam, m->n_params, m->n_mlp_params, loss_scale, m->adam_step,
+		              m->w32, m->w16, m->grad16, m->m1, m->m2, m->steps);
+	}
+	free(enc); free(out); free(hidden); free(dout); free(denc);
+	return loss;
+}

@@ -1,0 +1,71 @@
+"""Shared test helpers: seeded synthetic batches (reference sample's pcg32{1337} strided RNG for
+positions, an analytic RGB field for targets) and device<->host plumbing for trainer buffers."""
+import ctypes
+import json
+import os
+
+import numpy as np
+
+from oracle import oracle as O
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+CONFIG_HASH = json.load(open(os.path.join(GOLD, "config_hash.json")))
+
+
+def rgb_field(pos):
+    """Smooth synthetic RGB image on [0,1)^2 (stands in for albert.jpg's bilinear texture fetch)."""
+    x, y = pos[:, 0].astype(np.float64), pos[:, 1].astype(np.float64)
+    r = 0.5 + 0.5 * np.sin(9.0 * x) * np.cos(7.0 * y)
+    g = 0.5 + 0.4 * np.sin(23.0 * x * y + 1.0)
+    b = 0.5 + 0.3 * np.cos(31.0 * x) * np.sin(17.0 * y) + 0.1 * ((x * 40).astype(np.int64) % 2)
+    return np.stack([r, g, b], axis=1).astype(np.float32)
+
+
+def make_batch(B, seed=1337, step=0):
+    """positions [B,2] from pcg32{seed} in generate_random_uniform order (random.h:39-70),
+    advanced by `step` batches; targets from rgb_field."""
+    r = O.pcg32(seed)
+    if step:
+        O.lib().orc_pcg32_advance(ctypes.byref(r), 2 * B * step)
+    pos = O.generate_uniform(r, 2 * B).reshape(B, 2)
+    return pos, rgb_field(pos)
+
+
+_hip = None
+
+
+def hip():
+    global _hip
+    if _hip is None:
+        import torch  # noqa: F401  (loads the HIP runtime torch uses; same SONAME as ours)
+        _hip = ctypes.CDLL("libamdhip64.so.7")
+        _hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        _hip.hipDeviceSynchronize.argtypes = []
+    return _hip
+
+
+def d2h(ptr, n, dtype):
+    """copy n elements of dtype from a device pointer to a numpy array"""
+    out = np.empty(n, dtype=dtype)
+    hip().hipDeviceSynchronize()
+    rc = hip().hipMemcpy(out.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(ptr), out.nbytes, 2)  # D2H
+    assert rc == 0
+    return out
+
+
+def trainer_arrays(t):
+    from tinycudann import _lib as L
+    lib = L.lib()
+    n = t.n_params
+    return {
+        "w32": d2h(lib.tcnn_trainer_params_fp32(t.h), n, np.float32),
+        "w16": d2h(lib.tcnn_trainer_params(t.h), n, np.uint16),
+        "g16": d2h(lib.tcnn_trainer_param_gradients(t.h), n, np.uint16),
+        "g32": d2h(lib.tcnn_trainer_gradients_fp32(t.h), n, np.float32),
+    }
+
+
+def rel_err(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))

@@ -1,0 +1,44 @@
+"""CPU checks of the C-ABI boundary: the HIP library loads (no GPU needed to dlopen) and exports
+every entry point include/tcnn_mi355x.h declares, with the ctypes table in tinycudann._lib covering
+all of them. No compute calls are made here."""
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import REPO
+
+HDR = os.path.join(REPO, "include", "tcnn_mi355x.h")
+LIB = os.path.join(REPO, "neuralbtf-tiny-cuda-nn_amd", "lib", "libtcnn_mi355x.so")
+
+
+def header_functions():
+    txt = open(HDR).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(tcnn_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_header_parses():
+    fns = header_functions()
+    assert "tcnn_trainer_training_step" in fns and "tcnn_module_backward" in fns
+    assert len(fns) > 40
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="library not built")
+def test_library_exports_every_declared_symbol():
+    out = subprocess.check_output(["nm", "-D", "--defined-only", LIB]).decode()
+    exported = set(l.split()[-1] for l in out.splitlines() if l.strip())
+    missing = [f for f in header_functions() if f not in exported]
+    assert not missing, missing
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="library not built")
+def test_ctypes_table_covers_header_and_loads():
+    from tinycudann import _lib
+    assert sorted(_lib.exported_symbols()) == header_functions()
+    L = _lib.lib()
+    assert L.tcnn_batch_size_granularity() == 256
+    assert L.tcnn_default_loss_scale(1) == 128.0 and L.tcnn_default_loss_scale(0) == 1.0
+    assert L.tcnn_has_networks() == 1
+    assert b"gfx950" in L.tcnn_version()

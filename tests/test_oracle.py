@@ -1,0 +1,108 @@
+"""Oracle pinning: the CPU restatement (oracle/) against the reference's own compiled sources
+(tests/golden/ref_known_answers.json, produced by oracle/_ref from /root/reference's pcg32.h +
+std::seed_seq) and the SURVEY.md §8(c) known answers."""
+import json
+import os
+
+import numpy as np
+
+from oracle import oracle as O
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+KA = json.load(open(os.path.join(GOLD, "ref_known_answers.json")))
+CONFIG_HASH = json.load(open(os.path.join(GOLD, "config_hash.json")))
+
+
+def test_seed_seq():
+    assert list(O.seed_seq([1337], 2)) == KA["seed_seq_1337"] == [2150097757, 2293033019]
+
+
+def test_pcg32_stream():
+    L = O.lib()
+    r = O.pcg32(1337)
+    assert L.orc_pcg32_next_uint(O.ctypes.byref(r)) == KA["pcg32_1337_next_uint"]
+    assert np.float32(L.orc_pcg32_next_float(O.ctypes.byref(r))) == np.float32(KA["pcg32_1337_next_float"])
+    r = O.pcg32(1337)
+    L.orc_pcg32_advance(O.ctypes.byref(r), 1000003)
+    assert L.orc_pcg32_next_uint(O.ctypes.byref(r)) == KA["pcg32_1337_advance_1000003_next_uint"]
+
+
+def _ends(v, k):
+    return np.concatenate([v[:k], v[-k:]])
+
+
+def test_trainer_init_matches_reference_rng():
+    m = O.OracleModel(CONFIG_HASH, 2, 3)
+    w = m.w32
+    assert m.n_mlp_params == 64 * 32 + 64 * 64 + 16 * 64 == 7168
+    assert m.n_params == 7168 + 708368
+    w0, w1, wo = w[:2048], w[2048:2048 + 4096], w[6144:7168]
+    np.testing.assert_array_equal(_ends(w0, 16), np.float32(KA["xavier_w0_ends16"]))
+    np.testing.assert_array_equal(_ends(w1, 16), np.float32(KA["xavier_w1_ends16"]))
+    np.testing.assert_array_equal(_ends(wo, 16), np.float32(KA["xavier_wout_ends16"]))
+    grid = w[7168:]
+    np.testing.assert_array_equal(_ends(grid, 64), np.float32(KA["grid_init_ends64"]))
+    assert abs(float(np.sum(grid.astype(np.float64))) - KA["grid_init_sum"]) < 1e-12
+
+
+def test_batch_rng_strided_order():
+    r = O.pcg32(1337)
+    b = O.generate_uniform(r, 1 << 19)
+    np.testing.assert_array_equal(_ends(b, 64), np.float32(KA["batch_2p19_ends64"]))
+    assert O.lib().orc_pcg32_next_uint(O.ctypes.byref(r)) == KA["batch_rng_after_next_uint"]
+
+
+def test_grid_offset_table_config_hash():
+    g = O.grid_cfg(CONFIG_HASH["encoding"], 2)
+    sizes = [g.offsets[l + 1] - g.offsets[l] for l in range(16)]
+    assert sizes == [256, 576, 1296, 2920, 6568, 14888] + [32768] * 10
+    assert g.n_params == 708368
+    for l, (sc, res) in enumerate(KA["grid_levels_s1_5"]):
+        assert np.float32(g.scales[l]) == np.float32(sc) and g.res[l] == res
+
+
+def test_grid_offset_table_log2t19():
+    enc = dict(CONFIG_HASH["encoding"], log2_hashmap_size=19, per_level_scale=2.0)
+    g = O.grid_cfg(enc, 2)
+    for l, (sc, res) in enumerate(KA["grid_levels_s2_0"]):
+        assert np.float32(g.scales[l]) == np.float32(sc) and g.res[l] == res
+    assert g.n_params == 11184640
+
+
+def test_survey_helper_known_answers():
+    # grid_scale(6, log2 1.5, 16) = 181.249985 (res 183),
+    # coherent_prime_hash<2>({183,7}) = 1401181024, grid_index<2,CoherentPrime>(Hash, 32768, 183, {183,7}) = 21344
+    g = O.grid_cfg(CONFIG_HASH["encoding"], 2)
+    assert np.float32(g.scales[6]) == np.float32(181.249985) and g.res[6] == 183
+    pg = np.array([183, 7], dtype=np.uint32)
+    assert O.lib().orc_coherent_prime_hash(2, O._p(pg)) == 1401181024
+    assert O.lib().orc_grid_index(O.ctypes.byref(g), 6, O._p(pg)) == 21344
+    # pos_fract(0.3, scale_6) -> pos 0.874996185, grid 54 (fmaf(scale, x, 0.5))
+    p = np.float32(np.float64(np.float32(g.scales[6])) * np.float64(np.float32(0.3)) + 0.5)  # exact product, one rounding = fmaf
+    assert int(np.floor(p)) == 54 and np.float32(p - np.floor(p)) == np.float32(0.874996185)
+
+
+def test_fp16_roundtrip_and_rne():
+    x = np.array([0.0, -0.0, 1.0, 65504.0, 65520.0, 1e-8, 5.960464477539063e-08, 2.98e-8,
+                  3.0e-8, 6.1e-5, 0.333333, -2.5e-6, np.inf, -np.inf], dtype=np.float32)
+    h = O.f2h(x)
+    ref = x.astype(np.float16).view(np.uint16)
+    np.testing.assert_array_equal(h, ref)
+    rng = np.random.default_rng(0)
+    y = (rng.standard_normal(200000) * np.exp(rng.uniform(-20, 12, 200000))).astype(np.float32)
+    np.testing.assert_array_equal(O.f2h(y), y.astype(np.float16).view(np.uint16))
+    hh = np.arange(0, 65536, dtype=np.uint32).astype(np.uint16)
+    finite = (hh & 0x7c00) != 0x7c00
+    np.testing.assert_array_equal(O.h2f(hh[finite]), hh[finite].view(np.float16).astype(np.float32))
+
+
+def test_hfma_single_rounding():
+    rng = np.random.default_rng(1)
+    a = rng.uniform(0, 1, 5000).astype(np.float16)
+    b = (rng.standard_normal(5000) * 1e-3).astype(np.float16)
+    c = (rng.standard_normal(5000) * 1e-3).astype(np.float16)
+    L = O.lib()
+    for i in range(5000):
+        got = L.orc_hfma(int(a[i].view(np.uint16)), int(b[i].view(np.uint16)), int(c[i].view(np.uint16)))
+        exact = np.float64(a[i]) * np.float64(b[i]) + np.float64(c[i])
+        assert got == np.float16(exact).view(np.uint16), i
