@@ -123,6 +123,8 @@ int tcnn_trainer_profile_end(tcnn_trainer* t, double* ms_per_phase, uint32_t n_p
 
 /* ---- self test (layout probe for the MFMA / transpose-read operand maps) ---- */
 int tcnn_debug_probe(void* stream, float* mfma_out /* device [64*4] */, int16_t* tr_out /* device [64*8] */);
+/* out[i] = fma(a[i], b[i], c[i]) with the packed-fp16 FMA the grid forward uses (n_pairs half2 values) */
+int tcnn_debug_hfma(void* stream, const void* a, const void* b, const void* c, void* out, uint32_t n_pairs);
 
 #ifdef __cplusplus
 }

@@ -291,6 +291,10 @@ int tcnn_trainer_profile_end(tcnn_trainer* t, double* ms, uint32_t n_phases, uin
 	return guard([&] { t->t->profile_end(ms, n_phases, n_steps); });
 }
 
+int tcnn_debug_hfma(void* stream, const void* a, const void* b, const void* c, void* out, uint32_t n_pairs) {
+	return guard([&] { launch_probe_hfma((hipStream_t)stream, a, b, c, out, n_pairs); });
+}
+
 int tcnn_debug_probe(void* stream, float* mfma_out, int16_t* tr_out) {
 	return guard([&] { launch_probe((hipStream_t)stream, mfma_out, tr_out); });
 }

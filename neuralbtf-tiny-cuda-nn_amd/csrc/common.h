@@ -62,4 +62,18 @@ struct GridDesc {
 
 inline uint32_t div_round_up(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
+// Grow-only scratch allocation owned by a launcher (not stream-ordered: callers on one stream).
+struct DevBufLite {
+	void* p = nullptr;
+	size_t bytes = 0;
+	void* get(size_t n) {
+		if (n > bytes) {
+			if (p) (void)hipFree(p);
+			TCNN_HIP_CHECK(hipMalloc(&p, n));
+			bytes = n;
+		}
+		return p;
+	}
+};
+
 }  // namespace tcnn_amd

@@ -13,6 +13,16 @@
 
 namespace tcnn_amd {
 
+// Packed fp16 FMA with ONE rounding (CUDA __hfma2 semantics, reference grid.h:162 / vec.h:370-376).
+// Pinned as v_pk_fma_f16: left to itself hipcc may select v_fma_mix{lo,hi}_f16, whose fp32-internal
+// result is rounded twice and differs from __hfma2 in ~1e-5 of cases.
+__device__ __forceinline__ h2 pk_fma_f16(h2 a, h2 b, h2 c) {
+	uint32_t r;
+	asm("v_pk_fma_f16 %0, %1, %2, %3" : "=v"(r) : "v"(__builtin_bit_cast(uint32_t, a)), "v"(__builtin_bit_cast(uint32_t, b)),
+	    "v"(__builtin_bit_cast(uint32_t, c)));
+	return __builtin_bit_cast(h2, r);
+}
+
 struct LevelInfo {
 	float scale;
 	uint32_t res;
@@ -95,7 +105,7 @@ __device__ __forceinline__ h2 encode_level_f2(const uint32_t* __restrict__ table
 #pragma unroll
 	for (uint32_t c = 0; c < NC; ++c) {
 		h2 wv = {w16[c], w16[c]};
-		r = __builtin_elementwise_fma(wv, __builtin_bit_cast(h2, v[c]), r);
+		r = pk_fma_f16(wv, __builtin_bit_cast(h2, v[c]), r);
 	}
 	return r;
 }

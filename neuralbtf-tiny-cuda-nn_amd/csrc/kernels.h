@@ -32,12 +32,15 @@ void launch_fused_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, ui
                         uint32_t B, uint32_t dims, float loss_scale, const void* params16, const void* table16,
                         const float* pos, const float* target, void* out16, void* dLdenc_pairs,
                         float* wgrad_partial, float* loss_partial, const LevelInfo* levels, bool hash_grid,
-                        Interp interp, uint32_t n_blocks, const void* dout16 = nullptr);
+                        Interp interp, uint32_t n_blocks, const void* dout16, const void* wimage);
+// LDS weight image of the fused kernels, built once per parameter update.
+size_t fused_weight_image_bytes(uint32_t W, uint32_t IN, uint32_t NH);
+void launch_pack_weights(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, const void* params16, void* image);
 
 // Forward-only MLP (inference): in fp16 SoA [IN][B] or AoS [B][IN] -> out fp16 [B][16].
 bool mlp_infer_supported(uint32_t W, uint32_t IN, uint32_t NH, uint32_t OUTP, int act);
 void launch_mlp_infer(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, int act, bool soa, uint32_t B,
-                      const void* params16, const void* in16, void* out16);
+                      const void* wimage, const void* in16, void* out16);
 // out[b*n_out + o] = (float)in[b*in_stride + o]  (reference trim_and_cast_from, object.cu:60-67)
 void launch_trim_cast(hipStream_t st, uint32_t B, uint32_t in_stride, uint32_t n_out, const void* in16, float* out);
 
@@ -71,6 +74,7 @@ void launch_relative_l2(hipStream_t st, uint32_t B, uint32_t stride, uint32_t di
 
 void launch_sum(hipStream_t st, const float* in, uint32_t n, float* out);
 
+void launch_probe_hfma(hipStream_t st, const void* a, const void* b, const void* c, void* out, uint32_t n_pairs);
 // Debug probe: runs one MFMA 16x16x32 f16 and two ds_read_b64_tr_b16 with known data.
 void launch_probe(hipStream_t st, float* mfma_out, int16_t* tr_out);
 

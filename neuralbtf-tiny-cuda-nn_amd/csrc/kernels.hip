@@ -33,6 +33,25 @@ bool fused_train_supported(uint32_t W, uint32_t IN, uint32_t NH, uint32_t D, uin
 	return false;
 }
 
+size_t fused_weight_image_bytes(uint32_t W, uint32_t IN, uint32_t NH) {
+#define X(w, in, nh) if (W == w && IN == in && NH == nh) return (size_t)FusedLayout<w, in, nh>::oStage * 2;
+	TCNN_FUSED_SHAPES(X)
+#undef X
+	return 0;
+}
+
+void launch_pack_weights(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, const void* params16, void* image) {
+#define X(w, in, nh)                                                                                               \
+	if (W == w && IN == in && NH == nh) {                                                                          \
+		hipLaunchKernelGGL((k_pack_weights<w, in, nh>), dim3(8), dim3(256), 0, st, (const _Float16*)params16, (_Float16*)image); \
+		TCNN_HIP_CHECK(hipGetLastError());                                                                         \
+		return;                                                                                                    \
+	}
+	TCNN_FUSED_SHAPES(X)
+#undef X
+	throw std::runtime_error("pack weights: unsupported shape");
+}
+
 size_t fused_train_lds_bytes(uint32_t W, uint32_t IN, uint32_t NH) {
 #define X(w, in, nh) if (W == w && IN == in && NH == nh) return FusedLayout<w, in, nh>::BYTES;
 	TCNN_FUSED_SHAPES(X)
@@ -41,7 +60,7 @@ size_t fused_train_lds_bytes(uint32_t W, uint32_t IN, uint32_t NH) {
 }
 
 uint32_t fused_train_n_blocks(uint32_t B) {
-	// 4 waves x 32 samples per workgroup iteration; 2 workgroups per CU on 256 CUs.
+	// 4 waves x 32 samples per workgroup iteration; 2 workgroups per CU on 256 CUs, persistent.
 	uint32_t n_iter_blocks = div_round_up(B, 128);
 	return n_iter_blocks < 512 ? n_iter_blocks : 512;
 }
@@ -84,9 +103,10 @@ void launch_fused_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, ui
                         uint32_t B, uint32_t dims, float loss_scale, const void* params16, const void* table16,
                         const float* pos, const float* target, void* out16, void* dLdenc_pairs,
                         float* wgrad_partial, float* loss_partial, const LevelInfo* levels, bool hash_grid,
-                        Interp interp, uint32_t n_blocks, const void* dout16) {
+                        Interp interp, uint32_t n_blocks, const void* dout16, const void* wimage) {
 	TCNN_CHECK(B % 32 == 0, "fused train: batch must be a multiple of 32");
 	FusedTrainArgs a;
+	a.wimage = (const _Float16*)wimage;
 	a.dout = (const _Float16*)dout16;
 	a.B = B;
 	a.dims = dims;
@@ -110,7 +130,7 @@ void launch_fused_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, ui
 }
 
 template <int W, int IN, int NH, Act A, bool SOA>
-static void launch_infer_t(hipStream_t st, uint32_t B, const void* params, const void* in, void* out) {
+static void launch_infer_t(hipStream_t st, uint32_t B, const void* wimage, const void* in, void* out) {
 	constexpr size_t bytes = (size_t)FusedLayout<W, IN, NH>::oStage * 2;
 	static bool attr = false;
 	if (!attr) {
@@ -119,7 +139,7 @@ static void launch_infer_t(hipStream_t st, uint32_t B, const void* params, const
 	}
 	uint32_t nb = div_round_up(B, 64);
 	if (nb > 1024) nb = 1024;
-	hipLaunchKernelGGL((k_mlp_infer<W, IN, NH, A, SOA>), dim3(nb), dim3(256), bytes, st, B, (const _Float16*)params,
+	hipLaunchKernelGGL((k_mlp_infer<W, IN, NH, A, SOA>), dim3(nb), dim3(256), bytes, st, B, (const _Float16*)wimage,
 	                   (const _Float16*)in, (_Float16*)out);
 	TCNN_HIP_CHECK(hipGetLastError());
 }
@@ -133,15 +153,15 @@ bool mlp_infer_supported(uint32_t W, uint32_t IN, uint32_t NH, uint32_t OUTP, in
 }
 
 void launch_mlp_infer(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, int act, bool soa, uint32_t B,
-                      const void* params16, const void* in16, void* out16) {
+                      const void* wimage, const void* in16, void* out16) {
 	TCNN_CHECK(B % 16 == 0, "mlp inference: batch must be a multiple of 16");
 	if (B == 0) return;
 #define X(w, in, nh)                                                                                      \
 	if (W == w && IN == in && NH == nh) {                                                                 \
-		if (act == 1) { if (soa) launch_infer_t<w, in, nh, Act::ReLU, true>(st, B, params16, in16, out16);   \
-		                else launch_infer_t<w, in, nh, Act::ReLU, false>(st, B, params16, in16, out16); }    \
-		else { if (soa) launch_infer_t<w, in, nh, Act::None, true>(st, B, params16, in16, out16);            \
-		       else launch_infer_t<w, in, nh, Act::None, false>(st, B, params16, in16, out16); }             \
+		if (act == 1) { if (soa) launch_infer_t<w, in, nh, Act::ReLU, true>(st, B, wimage, in16, out16);   \
+		                else launch_infer_t<w, in, nh, Act::ReLU, false>(st, B, wimage, in16, out16); }    \
+		else { if (soa) launch_infer_t<w, in, nh, Act::None, true>(st, B, wimage, in16, out16);            \
+		       else launch_infer_t<w, in, nh, Act::None, false>(st, B, wimage, in16, out16); }             \
 		return;                                                                                           \
 	}
 	TCNN_FUSED_SHAPES(X)
@@ -207,10 +227,21 @@ __global__ __launch_bounds__(256) void k_grid_fwd(uint32_t B, const float* __res
 			w16[c] = (_Float16)w;
 			v[c] = tv[li.offset + grid_index<D, H>(hash_grid != 0, li.size, li.res, local)];
 		}
+		// packed fp16 FMA (v_pk_fma_f16: one rounding, = CUDA __hfma2 of grid.h:162); the scalar
+		// _Float16 fma is lowered through fp32 and would double-round.
 #pragma unroll
-		for (uint32_t c = 0; c < NC; ++c)
+		for (uint32_t c = 0; c < NC; ++c) {
+			const h2 wv = {w16[c], w16[c]};
 #pragma unroll
-			for (uint32_t f = 0; f < F; ++f) r[f] = __builtin_elementwise_fma(w16[c], v[c].v[f], r[f]);
+			for (uint32_t f = 0; f < F; f += 2) {
+				h2 vv, rr;
+				vv[0] = v[c].v[f]; vv[1] = (f + 1 < F) ? v[c].v[f + 1] : (_Float16)0.0f;
+				rr[0] = r[f]; rr[1] = (f + 1 < F) ? r[f + 1] : (_Float16)0.0f;
+				rr = pk_fma_f16(wv, vv, rr);
+				r[f] = rr[0];
+				if (f + 1 < F) r[f + 1] = rr[1];
+			}
+		}
 	}
 	if (soa) {
 #pragma unroll
@@ -263,70 +294,94 @@ void launch_grid_fwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_
 // grid backward: LDS-privatised slices
 // =============================================================================================
 
-constexpr uint32_t GRID_BWD_THREADS = 512;
+// LDS accumulators are int64 fixed point (2^-40 resolution, +-2^23 range): gfx950 executes LDS
+// float atomics (ds_add_f32 / ds_pk_add_f16) at ~195 cycles per wave-instruction per CU but
+// ds_add_u64 at ~12 (tools/lds_atomic_bench.hip), and integer sums are order-independent, so the
+// gradient is bit-reproducible (the reference's fp16 atomics, grid.h:252-255, are not).
+constexpr uint32_t GRID_BWD_THREADS = 1024;
 constexpr uint32_t GRID_BWD_LDS_BYTES = 128 * 1024;
+constexpr float GRID_FIX_SCALE = 1099511627776.0f;       // 2^40
+constexpr double GRID_FIX_INV = 1.0 / 1099511627776.0;  // 2^-40
 
-uint32_t grid_bwd_slice_entries(uint32_t F) { return GRID_BWD_LDS_BYTES / (4 * F); }
+uint32_t grid_bwd_slice_entries(uint32_t F) { return GRID_BWD_LDS_BYTES / (8 * F); }
+
+__device__ __forceinline__ void lds_add_fix(unsigned long long* acc, float v) {
+	const long long iv = (long long)(v * GRID_FIX_SCALE);
+	__hip_atomic_fetch_add(acc, (unsigned long long)iv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 template <uint32_t D, uint32_t F, HashType H, int LAYOUT>
 __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_sliced(
 	uint32_t B, const float* __restrict__ pos, uint32_t pstride, const _Float16* __restrict__ dLdy, uint32_t dy_stride,
 	const GridSlice* __restrict__ slices, float* __restrict__ partial, uint32_t partial_stride,
 	const LevelInfo* __restrict__ levels, uint32_t hash_grid, uint32_t interp_u, uint32_t pts_per_chunk) {
-	extern __shared__ __attribute__((aligned(16))) float acc[];
+	extern __shared__ __attribute__((aligned(16))) unsigned long long acc[];
 	const GridSlice sl = slices[blockIdx.x];
 	const LevelInfo li = levels[sl.level];
 	const uint32_t len = sl.end - sl.begin;
 	const Interp interp = (Interp)interp_u;
-	for (uint32_t j = threadIdx.x; j < len * F; j += blockDim.x) acc[j] = 0.0f;
+	for (uint32_t j = threadIdx.x; j < len * F; j += blockDim.x) acc[j] = 0ull;
 	__syncthreads();
 	const uint32_t i0 = blockIdx.y * pts_per_chunk;
 	const uint32_t i1 = min(B, i0 + pts_per_chunk);
-	for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-		float p[D];
-		uint32_t pg[D];
+	constexpr uint32_t U = 4;  // points in flight per thread
+	for (uint32_t base = i0 + threadIdx.x; base < i1; base += U * blockDim.x) {
+		float xs[U][D], dy[U][F];
 #pragma unroll
-		for (uint32_t d = 0; d < D; ++d) pos_fract(pos[(size_t)i * pstride + d], li.scale, interp, p[d], pg[d]);
-		float dy[F];
-		if constexpr (LAYOUT == 0) {  // level-major feature pairs [l][i][F]
-			const HVec<F> v = ((const HVec<F>*)dLdy)[(size_t)sl.level * B + i];
+		for (uint32_t u = 0; u < U; ++u) {
+			const uint32_t i = base + u * blockDim.x;
+			const bool ok = i < i1;
 #pragma unroll
-			for (uint32_t f = 0; f < F; ++f) dy[f] = (float)v.v[f];
-		} else if constexpr (LAYOUT == 1) {  // SoA [(l*F+f)*B + i] (reference RM layout)
+			for (uint32_t d = 0; d < D; ++d) xs[u][d] = ok ? pos[(size_t)i * pstride + d] : 0.0f;
+			if constexpr (LAYOUT == 0) {  // level-major feature pairs [l][i][F]
+				HVec<F> v;
+				if (ok) v = ((const HVec<F>*)dLdy)[(size_t)sl.level * B + i];
 #pragma unroll
-			for (uint32_t f = 0; f < F; ++f) dy[f] = (float)dLdy[(size_t)(sl.level * F + f) * B + i];
-		} else {  // AoS [i*stride + l*F + f] (reference CM layout)
+				for (uint32_t f = 0; f < F; ++f) dy[u][f] = ok ? (float)v.v[f] : 0.0f;
+			} else if constexpr (LAYOUT == 1) {  // SoA [(l*F+f)*B + i] (reference RM layout)
 #pragma unroll
-			for (uint32_t f = 0; f < F; ++f) dy[f] = (float)dLdy[(size_t)i * dy_stride + sl.level * F + f];
-		}
-		if (interp == Interp::Nearest) {
-			const uint32_t rel = grid_index<D, H>(hash_grid != 0, li.size, li.res, pg) - sl.begin;
-			if (rel < len) {
+				for (uint32_t f = 0; f < F; ++f) dy[u][f] = ok ? (float)dLdy[(size_t)(sl.level * F + f) * B + i] : 0.0f;
+			} else {  // AoS [i*stride + l*F + f] (reference CM layout)
 #pragma unroll
-				for (uint32_t f = 0; f < F; ++f) atomicAdd(&acc[rel * F + f], dy[f]);
+				for (uint32_t f = 0; f < F; ++f) dy[u][f] = ok ? (float)dLdy[(size_t)i * dy_stride + sl.level * F + f] : 0.0f;
 			}
-			continue;
 		}
 #pragma unroll
-		for (uint32_t c = 0; c < (1u << D); ++c) {
-			float w = 1.0f;
-			uint32_t local[D];
+		for (uint32_t u = 0; u < U; ++u) {
+			if (base + u * blockDim.x >= i1) break;
+			float p[D];
+			uint32_t pg[D];
 #pragma unroll
-			for (uint32_t d = 0; d < D; ++d) {
-				if ((c & (1u << d)) == 0) { w *= 1.0f - p[d]; local[d] = pg[d]; }
-				else { w *= p[d]; local[d] = pg[d] + 1; }
+			for (uint32_t d = 0; d < D; ++d) pos_fract(xs[u][d], li.scale, interp, p[d], pg[d]);
+			if (interp == Interp::Nearest) {
+				const uint32_t rel = grid_index<D, H>(hash_grid != 0, li.size, li.res, pg) - sl.begin;
+				if (rel < len) {
+#pragma unroll
+					for (uint32_t f = 0; f < F; ++f) lds_add_fix(&acc[rel * F + f], dy[u][f]);
+				}
+				continue;
 			}
-			const uint32_t rel = grid_index<D, H>(hash_grid != 0, li.size, li.res, local) - sl.begin;
-			if (rel < len) {
-				const float wh = (float)(_Float16)w;
 #pragma unroll
-				for (uint32_t f = 0; f < F; ++f) atomicAdd(&acc[rel * F + f], wh * dy[f]);
+			for (uint32_t c = 0; c < (1u << D); ++c) {
+				float w = 1.0f;
+				uint32_t local[D];
+#pragma unroll
+				for (uint32_t d = 0; d < D; ++d) {
+					if ((c & (1u << d)) == 0) { w *= 1.0f - p[d]; local[d] = pg[d]; }
+					else { w *= p[d]; local[d] = pg[d] + 1; }
+				}
+				const uint32_t rel = grid_index<D, H>(hash_grid != 0, li.size, li.res, local) - sl.begin;
+				if (rel < len) {
+					const float wh = (float)(_Float16)w;
+#pragma unroll
+					for (uint32_t f = 0; f < F; ++f) lds_add_fix(&acc[rel * F + f], wh * dy[u][f]);
+				}
 			}
 		}
 	}
 	__syncthreads();
 	float* dst = partial + (size_t)blockIdx.y * partial_stride + (size_t)(li.offset + sl.begin) * F;
-	for (uint32_t j = threadIdx.x; j < len * F; j += blockDim.x) dst[j] = acc[j];
+	for (uint32_t j = threadIdx.x; j < len * F; j += blockDim.x) dst[j] = (float)((double)(long long)acc[j] * GRID_FIX_INV);
 }
 
 template <uint32_t D, uint32_t F, HashType H, int LAYOUT>
@@ -381,7 +436,7 @@ void launch_grid_bwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_
 	if (B == 0 || n_slices == 0) return;
 	const uint32_t ppc = div_round_up(B, n_chunks);
 	dim3 g(n_slices, n_chunks);
-	const size_t lds = (size_t)grid_bwd_slice_entries(F) * F * 4;
+	const size_t lds = (size_t)grid_bwd_slice_entries(F) * F * 8;
 	const _Float16* dy = (const _Float16*)dLdy16;
 	switch (D) {
 		case 2: grid_bwd_f<2>(st, F, h, dy_layout, dy_stride, g, lds, B, pos, pos_stride, dy, slices, partial, partial_stride, levels, hash_grid, (uint32_t)interp, ppc); break;
@@ -396,26 +451,45 @@ void launch_grid_bwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_
 // reductions, Adam, casts, loss
 // =============================================================================================
 
-__global__ __launch_bounds__(256) void k_reduce_partials(const float* __restrict__ in, uint32_t n_parts, uint32_t stride,
-                                                          uint32_t n, float* __restrict__ out) {
+// Sum of fp32 partial slabs, at most two deterministic passes: (param block, part group) -> group
+// sums, then groups -> out. Every thread issues 4-wide loads over one group of parts.
+__global__ __launch_bounds__(256) void k_reduce_groups(const float* __restrict__ in, uint32_t n_parts, uint32_t group,
+                                                        uint32_t stride, uint32_t n, float* __restrict__ out, uint32_t out_stride) {
 	const uint32_t p4 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
 	if (p4 >= n) return;
-	if (p4 + 4 <= n && (stride % 4) == 0) {
+	const uint32_t j0 = blockIdx.y * group;
+	const uint32_t j1 = min(n_parts, j0 + group);
+	float* dst = out + (size_t)blockIdx.y * out_stride;
+	if (p4 + 4 <= n && (stride % 4) == 0 && (out_stride % 4) == 0) {
 		f4 s = {0.0f, 0.0f, 0.0f, 0.0f};
-		for (uint32_t j = 0; j < n_parts; ++j) s += *(const f4*)(in + (size_t)j * stride + p4);
-		*(f4*)(out + p4) = s;
+		for (uint32_t j = j0; j < j1; ++j) s += *(const f4*)(in + (size_t)j * stride + p4);
+		*(f4*)(dst + p4) = s;
 	} else {
 		for (uint32_t p = p4; p < n && p < p4 + 4; ++p) {
 			float s = 0.0f;
-			for (uint32_t j = 0; j < n_parts; ++j) s += in[(size_t)j * stride + p];
-			out[p] = s;
+			for (uint32_t j = j0; j < j1; ++j) s += in[(size_t)j * stride + p];
+			dst[p] = s;
 		}
 	}
 }
 
+static DevBufLite g_red_tmp;
+
 void launch_reduce_partials(hipStream_t st, const float* in, uint32_t n_parts, uint32_t stride, uint32_t n, float* out) {
 	if (n == 0) return;
-	hipLaunchKernelGGL(k_reduce_partials, dim3(div_round_up(div_round_up(n, 4), 256)), dim3(256), 0, st, in, n_parts, stride, n, out);
+	constexpr uint32_t MAXG = 16;
+	const uint32_t bx = div_round_up(div_round_up(n, 4), 256);
+	if (n_parts <= MAXG) {
+		hipLaunchKernelGGL(k_reduce_groups, dim3(bx, 1), dim3(256), 0, st, in, n_parts, n_parts, stride, n, out, 0u);
+	} else {
+		const uint32_t group = div_round_up(n_parts, MAXG);
+		const uint32_t G = div_round_up(n_parts, group);
+		const uint32_t ostride = (n + 3) / 4 * 4;
+		float* tmp = (float*)g_red_tmp.get((size_t)G * ostride * 4);
+		hipLaunchKernelGGL(k_reduce_groups, dim3(bx, G), dim3(256), 0, st, in, n_parts, group, stride, n, tmp, ostride);
+		TCNN_HIP_CHECK(hipGetLastError());
+		hipLaunchKernelGGL(k_reduce_groups, dim3(bx, 1), dim3(256), 0, st, tmp, G, G, ostride, n, out, 0u);
+	}
 	TCNN_HIP_CHECK(hipGetLastError());
 }
 
@@ -528,12 +602,10 @@ void launch_sum(hipStream_t st, const float* in, uint32_t n, float* out) {
 // layout probe (MFMA f16 operand maps + ds_read_b64_tr_b16), checked by tests/test_gpu_probe.py
 // =============================================================================================
 __global__ void k_probe(float* mfma_out, int16_t* tr_out) {
-	__shared__ __attribute__((aligned(16))) _Float16 S[32 * 24];
+	extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
+	uint16_t* S = (uint16_t*)smem;
 	const int l = threadIdx.x, c = l & 15, q = l >> 4;
-	for (int j = l; j < 32 * 24; j += 64) {
-		const int row = j / 24, col = j % 24;
-		S[j] = __builtin_bit_cast(_Float16, (int16_t)(row * 64 + col));
-	}
+	for (int j = l; j < 32 * 24; j += 64) S[j] = (uint16_t)((j / 24) * 64 + (j % 24));
 	__syncthreads();
 	h8 av, bv;
 	for (int e = 0; e < 8; ++e) {
@@ -543,12 +615,22 @@ __global__ void k_probe(float* mfma_out, int16_t* tr_out) {
 	}
 	const f4 d = mfma16(av, bv, f4{0.0f, 0.0f, 0.0f, 0.0f});
 	for (int r = 0; r < 4; ++r) mfma_out[l * 4 + r] = d[r];
-	const h8 t = lds_trfrag(S, 24, q, c, 0);
-	for (int e = 0; e < 8; ++e) tr_out[l * 8 + e] = __builtin_bit_cast(int16_t, t[e]);
+	const h8 t = lds_trfrag(smem, 24, q, c, 0);
+	*(uint4*)(tr_out + l * 8) = __builtin_bit_cast(uint4, t);
+}
+
+__global__ void k_probe_hfma(const h2* a, const h2* b, const h2* c, h2* out, uint32_t n) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i < n) out[i] = pk_fma_f16(a[i], b[i], c[i]);
+}
+
+void launch_probe_hfma(hipStream_t st, const void* a, const void* b, const void* c, void* out, uint32_t n_pairs) {
+	hipLaunchKernelGGL(k_probe_hfma, dim3(div_round_up(n_pairs, 256)), dim3(256), 0, st, (const h2*)a, (const h2*)b, (const h2*)c, (h2*)out, n_pairs);
+	TCNN_HIP_CHECK(hipGetLastError());
 }
 
 void launch_probe(hipStream_t st, float* mfma_out, int16_t* tr_out) {
-	hipLaunchKernelGGL(k_probe, dim3(1), dim3(64), 0, st, mfma_out, tr_out);
+	hipLaunchKernelGGL(k_probe, dim3(1), dim3(64), 32 * 24 * 2, st, mfma_out, tr_out);
 	TCNN_HIP_CHECK(hipGetLastError());
 }
 

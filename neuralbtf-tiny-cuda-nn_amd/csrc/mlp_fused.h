@@ -130,7 +130,22 @@ __device__ __forceinline__ void load_weights_lds(_Float16* smem, const _Float16*
 	}
 }
 
+// The LDS weight image (W, W^T, padded rows) is built once per step by k_pack_weights into global
+// memory; every workgroup then copies it with 16-byte loads instead of re-transposing the weights.
+template <int W, int IN, int NH>
+__global__ void k_pack_weights(const _Float16* __restrict__ params, _Float16* __restrict__ image) {
+	load_weights_lds<W, IN, NH>(image, params, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x);
+}
+
+__device__ __forceinline__ void copy_image_to_lds(_Float16* smem, const _Float16* __restrict__ image, int n_halves, int tid, int nthreads) {
+	const uint4* src = (const uint4*)image;
+	uint4* dst = (uint4*)smem;
+	const int n16 = n_halves / 8;
+	for (int k = tid; k < n16; k += nthreads) dst[k] = src[k];
+}
+
 struct FusedTrainArgs {
+	const _Float16* wimage; // packed LDS weight image (k_pack_weights)
 	uint32_t B;
 	uint32_t dims;          // target width (n_output_dims)
 	float loss_scale;
@@ -160,7 +175,7 @@ __global__ __launch_bounds__(256, 2) void k_fused_train_grid(const FusedTrainArg
 	const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 	const int c = lane & 15, q = lane >> 4;
 
-	load_weights_lds<W, IN, NH>(smem, a.params, tid, 256);
+	copy_image_to_lds(smem, a.wimage, L::oStage, tid, 256);
 	LevelInfo* sLvl = (LevelInfo*)((char*)smem + L::LVL_BYTES);
 	for (int l = tid; l < NLVL; l += 256) sLvl[l] = a.levels[l];
 	__syncthreads();
@@ -391,35 +406,50 @@ __global__ __launch_bounds__(256, 2) void k_fused_train_grid(const FusedTrainArg
 	}
 
 	// ---------------- workgroup reduction of dW and loss -> partial slabs ----------------
+	// Waves add their register accumulators into one LDS slab in fixed wave order (plain LDS
+	// loads/stores: gfx950 LDS float atomics are ~24x slower than integer ones, and a fixed order
+	// keeps the partial bit-reproducible).
 	__syncthreads();
 	float* red = (float*)smem;
-	for (int p = tid; p < L::N_MLP + 1; p += 256) red[p] = 0.0f;
-	__syncthreads();
 	constexpr int oH = W * IN, oO = W * IN + NHM * W * W;
 #pragma unroll
-	for (int mt = 0; mt < NT; ++mt) {
-#pragma unroll
-		for (int r = 0; r < 4; ++r) {
-			const int n = 16 * mt + 4 * q + r;
-#pragma unroll
-			for (int u = 0; u < NTI; ++u) atomicAdd(&red[n * IN + 16 * u + c], accW0[mt][u][r]);
-#pragma unroll
-			for (int j = 0; j < NHM; ++j)
-#pragma unroll
-				for (int nt = 0; nt < NT; ++nt) atomicAdd(&red[oH + j * W * W + n * W + 16 * nt + c], accH[j][mt][nt][r]);
-		}
-	}
-#pragma unroll
-	for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-		for (int r = 0; r < 4; ++r) atomicAdd(&red[oO + (4 * q + r) * W + 16 * nt + c], accWo[nt][r]);
-#pragma unroll
 	for (int off = 32; off > 0; off >>= 1) loss_acc += __shfl_xor(loss_acc, off);
-	if (lane == 0) atomicAdd(&red[L::N_MLP], loss_acc);
-	__syncthreads();
+	for (int w = 0; w < 4; ++w) {
+		if (wave == w) {
+			const bool first = (w == 0);
+#pragma unroll
+			for (int mt = 0; mt < NT; ++mt) {
+#pragma unroll
+				for (int r = 0; r < 4; ++r) {
+					const int n = 16 * mt + 4 * q + r;
+#pragma unroll
+					for (int u = 0; u < NTI; ++u) {
+						float* p = &red[n * IN + 16 * u + c];
+						*p = first ? accW0[mt][u][r] : *p + accW0[mt][u][r];
+					}
+#pragma unroll
+					for (int j = 0; j < NHM; ++j)
+#pragma unroll
+						for (int nt = 0; nt < NT; ++nt) {
+							float* p = &red[oH + j * W * W + n * W + 16 * nt + c];
+							*p = first ? accH[j][mt][nt][r] : *p + accH[j][mt][nt][r];
+						}
+				}
+			}
+#pragma unroll
+			for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+				for (int r = 0; r < 4; ++r) {
+					float* p = &red[oO + (4 * q + r) * W + 16 * nt + c];
+					*p = first ? accWo[nt][r] : *p + accWo[nt][r];
+				}
+			if (lane == 0) red[L::N_MLP + w] = loss_acc;
+		}
+		__syncthreads();
+	}
 	float* dst = a.wgrad_partial + (size_t)blockIdx.x * L::N_MLP;
 	for (int p = tid; p < L::N_MLP; p += 256) dst[p] = red[p];
-	if (tid == 0) a.loss_partial[blockIdx.x] = red[L::N_MLP];
+	if (tid == 0) a.loss_partial[blockIdx.x] = red[L::N_MLP] + red[L::N_MLP + 1] + red[L::N_MLP + 2] + red[L::N_MLP + 3];
 }
 
 
@@ -427,14 +457,14 @@ __global__ __launch_bounds__(256, 2) void k_fused_train_grid(const FusedTrainArg
 // encoding's layout) or AoS ([B][IN]); output fp16 [B][16] (the reference's CM [16 x B]).
 // Reference: kernel_mlp_fused<..., INFERENCE=true> (fully_fused_mlp.cu:499-557).
 template <int W, int IN, int NH, Act ACT, bool SOA>
-__global__ __launch_bounds__(256, 2) void k_mlp_infer(uint32_t B, const _Float16* __restrict__ params,
+__global__ __launch_bounds__(256, 2) void k_mlp_infer(uint32_t B, const _Float16* __restrict__ wimage,
                                                       const _Float16* __restrict__ in, _Float16* __restrict__ out) {
 	using L = FusedLayout<W, IN, NH>;
 	constexpr int NT = L::NT, KW = L::KW, NTI = L::NTI, KI = L::KI;
 	extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
 	const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 	const int c = lane & 15, q = lane >> 4;
-	load_weights_lds<W, IN, NH>(smem, params, tid, 256);
+	copy_image_to_lds(smem, wimage, L::oStage, tid, 256);
 	__syncthreads();
 	const _Float16* sW0 = smem + L::oW0;
 	const _Float16* sWh = smem + L::oWh;

@@ -319,7 +319,9 @@ void NetworkWithGridHost::inference(hipStream_t st, StepWorkspace& ws, uint32_t 
 	const uint8_t* table = (const uint8_t*)params16 + (size_t)mlp.n_params() * 2;
 	launch_grid_fwd(st, grid->desc.n_pos_dims, grid->desc.n_features_per_level, grid->desc.hash_type, B, grid->desc.n_levels,
 	                pos, grid->desc.n_pos_dims, table, ws.enc16.p, true, 0, grid->dev_levels(), grid->hash_grid(), grid->desc.interp);
-	launch_mlp_infer(st, mlp.width, IN, mlp.n_hidden_layers, mlp.activation, true, B, params16, ws.enc16.p, out16);
+	ws.wimage.reserve(fused_weight_image_bytes(mlp.width, IN, mlp.n_hidden_layers));
+	launch_pack_weights(st, mlp.width, IN, mlp.n_hidden_layers, params16, ws.wimage.p);
+	launch_mlp_infer(st, mlp.width, IN, mlp.n_hidden_layers, mlp.activation, true, B, ws.wimage.p, ws.enc16.p, out16);
 }
 
 void NetworkWithGridHost::fwd_bwd(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target,
@@ -341,10 +343,12 @@ void NetworkWithGridHost::fwd_bwd(hipStream_t st, StepWorkspace& ws, uint32_t B,
 	ws.grid_partial.reserve((size_t)n_chunks * grid->n_params * 4);
 
 	const uint8_t* table = (const uint8_t*)params16 + (size_t)n_mlp * 2;
+	ws.wimage.reserve(fused_weight_image_bytes(mlp.width, mlp.n_input, mlp.n_hidden_layers));
+	launch_pack_weights(st, mlp.width, mlp.n_input, mlp.n_hidden_layers, params16, ws.wimage.p);
 	launch_fused_train(st, mlp.width, mlp.n_input, mlp.n_hidden_layers, grid->desc.n_pos_dims, grid->desc.hash_type,
 	                   mlp.activation, B, dims, loss_scale, params16, table, pos, target, out16, ws.dLdenc.p,
 	                   ws.wgrad_partial.as<float>(), ws.loss_partial.as<float>(), grid->dev_levels(), grid->hash_grid(),
-	                   grid->desc.interp, nb, dout16);
+	                   grid->desc.interp, nb, dout16, ws.wimage.p);
 	if (mark) mark(1);
 	launch_reduce_partials(st, ws.wgrad_partial.as<float>(), nb, n_mlp, n_mlp, grad32);
 	if (mark) mark(2);

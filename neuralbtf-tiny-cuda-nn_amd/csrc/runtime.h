@@ -88,7 +88,7 @@ struct AdamHost {
 
 // Workspace for one fused fwd/bwd over a batch of B (sizes grow only).
 struct StepWorkspace {
-	DevBuf dLdenc, wgrad_partial, loss_partial, grid_partial, grad32_tmp, out16, enc16;
+	DevBuf dLdenc, wgrad_partial, loss_partial, grid_partial, grad32_tmp, out16, enc16, wimage;
 	uint32_t n_fused_blocks = 0, n_grid_chunks = 0;
 };
 
