@@ -80,6 +80,9 @@ def main():
     ap.add_argument("--config", default=os.path.join(REPO, "tests", "golden", "config_hash.json"))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (rehearsal)")
+    ap.add_argument("--all-ranks-on-device0", action="store_true",
+                    help="rehearse N>1 on a 1-GPU box (gloo); never used for measurements")
     args = ap.parse_args()
 
     import torch
@@ -88,10 +91,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
+    dev = 0 if args.all_ranks_on_device0 else local_rank
+    torch.cuda.set_device(dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(args.dist_backend)
 
     from tinycudann import Trainer
     import ctypes
@@ -108,19 +115,12 @@ def main():
         pos = torch.rand(B, 2, device="cuda", generator=g).contiguous()
         batches.append((pos, rgb_field_torch(pos)))
 
-    grads = None
-    if world > 1:
-        grads = trainer.gradients_fp32()
-        trainer.set_gradient_scale(1.0 / world)
+    from tinycudann.parallel import DataParallelTrainer
+    dp = DataParallelTrainer(trainer)
 
     def step(i):
         pos, tgt = batches[i % NB]
-        if world == 1:
-            trainer.training_step(pos, tgt, run_optimizer=True)
-        else:
-            trainer.training_step(pos, tgt, run_optimizer=False)
-            dist.all_reduce(grads)
-            trainer.optimizer_step()
+        dp.training_step(pos, tgt)
 
     for i in range(args.warmup):
         step(i)
@@ -139,7 +139,7 @@ def main():
         dist.barrier()
     elapsed = t1 - t0
     if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
 

@@ -59,8 +59,15 @@ __device__ __forceinline__ uint32_t grid_index(bool hash_grid, uint32_t size, ui
 		for (uint32_t d = 0; d < D; ++d) h ^= pg[d] * hash_prime<H>(d);
 		index = h;
 	}
+	// index % size (common_device.h:706) without an integer division: hashed levels have
+	// power-of-two sizes; a dense level's index is < res^D + res^(D-1) + ... < 2 * size, so one
+	// conditional subtraction is exact; only tiled grids (size capped at base^D) may need more.
 	if ((size & (size - 1)) == 0) return index & (size - 1);
-	return index < size ? index : index % size;
+	if (index >= size) {
+		index -= size;
+		if (index >= size) index %= size;
+	}
+	return index;
 }
 
 __device__ __forceinline__ void pos_fract(float x, float scale, Interp interp, float& pos, uint32_t& grid) {

@@ -164,3 +164,19 @@ def test_module_backward_matches_oracle(torch_mod):
     assert rel_err(got, ref) <= 1e-3, rel_err(got, ref)
     lib.tcnn_context_destroy(ctx)
     lib.tcnn_module_destroy(m)
+
+
+def test_trainer_buffer_views_alias_device_memory(torch_mod):
+    """The torch views of trainer buffers (used by the data-parallel all-reduce) alias the
+    engine's device memory."""
+    torch = torch_mod
+    from tinycudann import Trainer
+    t = Trainer(2, 3, CONFIG_HASH, seed=1337)
+    pos, tgt = make_batch(1024)
+    t.training_step(torch.from_numpy(pos).cuda(), torch.from_numpy(tgt).cuda(), run_optimizer=False)
+    g = t.gradients_fp32()
+    a = trainer_arrays(t)
+    np.testing.assert_array_equal(g.cpu().numpy(), a["g32"])
+    g.mul_(2.0)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(trainer_arrays(t)["g32"], a["g32"] * 2.0)
