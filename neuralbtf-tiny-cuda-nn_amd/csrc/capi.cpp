@@ -291,6 +291,35 @@ int tcnn_trainer_profile_end(tcnn_trainer* t, double* ms, uint32_t n_phases, uin
 	return guard([&] { t->t->profile_end(ms, n_phases, n_steps); });
 }
 
+int tcnn_debug_fused_phase_cycles(tcnn_trainer* t, void* stream, uint32_t n, const float* input, const float* target,
+                                  uint64_t* host_cycles8) {
+	return guard([&] {
+		auto& tr = *t->t;
+		auto& m = *tr.model;
+		TCNN_CHECK(m.mlp.width == 64 && m.mlp.n_input == 32 && m.mlp.n_hidden_layers == 2 && m.grid->desc.n_pos_dims == 2,
+		           "phase profile: config_hash shape only");
+		hipStream_t st = (hipStream_t)stream;
+		// run one normal step first so the workspace is sized
+		tr.training_step(st, n, input, target, false);
+		const uint32_t nb = fused_train_n_blocks(64, 32, 2, 2, tr.n_output_dims, false, n);
+		constexpr size_t WV = 8;  // waves per workgroup of the pipelined kernel
+		DevBuf prof;
+		prof.reserve((size_t)nb * WV * 8 * 8);
+		TCNN_HIP_CHECK(hipMemsetAsync(prof.p, 0, (size_t)nb * WV * 8 * 8, st));
+		launch_fused_train_profile(st, n, tr.n_output_dims, tr.w16.p, (const uint8_t*)tr.w16.p + tr.n_mlp * 2, input, target,
+		                           tr.ws.dLdenc.p, tr.ws.wgrad_partial.as<float>(), tr.ws.loss_partial.as<float>(),
+		                           m.grid->dev_levels(), nb, tr.ws.wimage.p, prof.as<unsigned long long>());
+		std::vector<unsigned long long> h((size_t)nb * WV * 8);
+		TCNN_HIP_CHECK(hipMemcpyAsync(h.data(), prof.p, h.size() * 8, hipMemcpyDeviceToHost, st));
+		TCNN_HIP_CHECK(hipStreamSynchronize(st));
+		for (int k = 0; k < 8; ++k) {
+			unsigned long long sum = 0;
+			for (size_t w = 0; w < (size_t)nb * WV; ++w) sum += h[w * 8 + k];
+			host_cycles8[k] = sum;
+		}
+	});
+}
+
 int tcnn_debug_hfma(void* stream, const void* a, const void* b, const void* c, void* out, uint32_t n_pairs) {
 	return guard([&] { launch_probe_hfma((hipStream_t)stream, a, b, c, out, n_pairs); });
 }

@@ -79,6 +79,36 @@ __device__ __forceinline__ void pos_fract(float x, float scale, Interp interp, f
 	pos = p;
 }
 
+// Corner indices (absolute entry index) and fp16 weights of one level; no memory access, so a
+// caller can issue the gathers of many levels back to back before consuming any of them.
+template <uint32_t D, HashType H>
+__device__ __forceinline__ void level_corners(const LevelInfo& li, bool hash_grid, Interp interp, const float* x,
+                                              uint32_t* idx, _Float16* w16) {
+	float pos[D];
+	uint32_t pg[D];
+#pragma unroll
+	for (uint32_t d = 0; d < D; ++d) pos_fract(x[d], li.scale, interp, pos[d], pg[d]);
+	constexpr uint32_t NC = 1u << D;
+	if (interp == Interp::Nearest) {
+		const uint32_t i0 = li.offset + grid_index<D, H>(hash_grid, li.size, li.res, pg);
+#pragma unroll
+		for (uint32_t c = 0; c < NC; ++c) { idx[c] = i0; w16[c] = (_Float16)(c == 0 ? 1.0f : 0.0f); }
+		return;
+	}
+#pragma unroll
+	for (uint32_t c = 0; c < NC; ++c) {
+		float w = 1.0f;
+		uint32_t local[D];
+#pragma unroll
+		for (uint32_t d = 0; d < D; ++d) {
+			if ((c & (1u << d)) == 0) { w *= 1.0f - pos[d]; local[d] = pg[d]; }
+			else { w *= pos[d]; local[d] = pg[d] + 1; }
+		}
+		w16[c] = (_Float16)w;
+		idx[c] = li.offset + grid_index<D, H>(hash_grid, li.size, li.res, local);
+	}
+}
+
 // Linear interpolation of one level for F == 2 features (one half2 per table entry). Gathers are
 // issued together before the fp16 FMA chain so their latencies overlap.
 template <uint32_t D, HashType H>

@@ -26,8 +26,8 @@ struct AdamArgs {
 // With dout16 != NULL the loss is skipped and dL/d(output) fp16 [B][16] is read instead (Module::backward).
 // Returns false if no fused kernel exists for this shape.
 bool fused_train_supported(uint32_t W, uint32_t IN, uint32_t NH, uint32_t D, uint32_t F, uint32_t OUTP, int act, HashType h);
-size_t fused_train_lds_bytes(uint32_t W, uint32_t IN, uint32_t NH);
-uint32_t fused_train_n_blocks(uint32_t B);
+// Workgroups the fused launch uses (= partial slabs it writes) for this shape and batch.
+uint32_t fused_train_n_blocks(uint32_t W, uint32_t IN, uint32_t NH, uint32_t D, uint32_t dims, bool ext_dout, uint32_t B);
 void launch_fused_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, uint32_t D, HashType h, int act,
                         uint32_t B, uint32_t dims, float loss_scale, const void* params16, const void* table16,
                         const float* pos, const float* target, void* out16, void* dLdenc_pairs,
@@ -75,6 +75,11 @@ void launch_relative_l2(hipStream_t st, uint32_t B, uint32_t stride, uint32_t di
 void launch_sum(hipStream_t st, const float* in, uint32_t n, float* out);
 
 void launch_probe_hfma(hipStream_t st, const void* a, const void* b, const void* c, void* out, uint32_t n_pairs);
+// Diagnostic: the config_hash fused (pipelined) kernel with s_memtime phase stamps (prof: [blocks*8][8] u64).
+void launch_fused_train_profile(hipStream_t st, uint32_t B, uint32_t dims, const void* params16, const void* table16,
+                                const float* pos, const float* target, void* dLdenc, float* wgrad_partial,
+                                float* loss_partial, const LevelInfo* levels, uint32_t n_blocks, const void* wimage,
+                                unsigned long long* prof);
 // Debug probe: runs one MFMA 16x16x32 f16 and two ds_read_b64_tr_b16 with known data.
 void launch_probe(hipStream_t st, float* mfma_out, int16_t* tr_out);
 

@@ -52,22 +52,51 @@ void launch_pack_weights(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, c
 	throw std::runtime_error("pack weights: unsupported shape");
 }
 
-size_t fused_train_lds_bytes(uint32_t W, uint32_t IN, uint32_t NH) {
-#define X(w, in, nh) if (W == w && IN == in && NH == nh) return FusedLayout<w, in, nh>::BYTES;
-	TCNN_FUSED_SHAPES(X)
-#undef X
-	return 0;
+static uint32_t device_cu_count() {
+	int dev = 0, n = 0;
+	TCNN_HIP_CHECK(hipGetDevice(&dev));
+	static int cached_dev = -1;
+	static uint32_t cached = 0;
+	if (dev != cached_dev) {
+		TCNN_HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+		cached = n > 0 ? (uint32_t)n : 1u;
+		cached_dev = dev;
+	}
+	return cached;
 }
 
-uint32_t fused_train_n_blocks(uint32_t B) {
-	// 4 waves x 32 samples per workgroup iteration; 2 workgroups per CU on 256 CUs, persistent.
-	uint32_t n_iter_blocks = div_round_up(B, 128);
-	return n_iter_blocks < 512 ? n_iter_blocks : 512;
+// The pipelined 8-wave kernel serves 2D grids whose LDS budget fits and whose targets (<= 3 dims)
+// ride the LDS-DMA path; everything else takes the register-gather kernel.
+static bool fused_use_pipe(uint32_t W, uint32_t IN, uint32_t NH, uint32_t D, uint32_t dims, bool ext_dout) {
+	if (D != 2 || (!ext_dout && dims > 3)) return false;
+#define X(w, in, nh) if (W == w && IN == in && NH == nh) return PipeLayout<w, in, nh>::FITS;
+	TCNN_FUSED_SHAPES(X)
+#undef X
+	return false;
+}
+
+uint32_t fused_train_n_blocks(uint32_t W, uint32_t IN, uint32_t NH, uint32_t D, uint32_t dims, bool ext_dout, uint32_t B) {
+	const uint32_t n_cu = device_cu_count();
+	if (fused_use_pipe(W, IN, NH, D, dims, ext_dout)) {
+		// one persistent 8-wave workgroup per CU
+		const uint32_t nb = div_round_up(B / 32, 8);
+		return nb < n_cu ? nb : n_cu;
+	}
+	// 4 waves x 32 samples per workgroup iteration; 2 workgroups per CU, persistent.
+	const uint32_t nb = div_round_up(B, 128);
+	return nb < 2 * n_cu ? nb : 2 * n_cu;
 }
 
 template <int W, int IN, int NH, uint32_t D, HashType H, Act A, bool EXT>
 static void launch_fused_e(hipStream_t st, const FusedTrainArgs& args, uint32_t n_blocks) {
-	constexpr size_t bytes = FusedLayout<W, IN, NH>::BYTES;
+	if constexpr (D == 2 && PipeLayout<W, IN, NH>::FITS) {
+		if (EXT || args.dims <= 3) {
+			hipLaunchKernelGGL((k_fused_train_pipe<W, IN, NH, H, A, EXT>), dim3(n_blocks), dim3(512), 0, st, args);
+			TCNN_HIP_CHECK(hipGetLastError());
+			return;
+		}
+	}
+	constexpr size_t bytes = RegKernelLayout<W, IN, NH>::BYTES;
 	static bool attr = false;
 	if (!attr) {
 		TCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k_fused_train_grid<W, IN, NH, D, H, A, EXT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
@@ -179,6 +208,21 @@ __global__ void k_trim_cast(uint32_t B, uint32_t in_stride, uint32_t n_out, cons
 void launch_trim_cast(hipStream_t st, uint32_t B, uint32_t in_stride, uint32_t n_out, const void* in16, float* out) {
 	if (!B) return;
 	hipLaunchKernelGGL(k_trim_cast, dim3(div_round_up((size_t)B * n_out, 256)), dim3(256), 0, st, B, in_stride, n_out, (const _Float16*)in16, out);
+	TCNN_HIP_CHECK(hipGetLastError());
+}
+
+void launch_fused_train_profile(hipStream_t st, uint32_t B, uint32_t dims, const void* params16, const void* table16,
+                                const float* pos, const float* target, void* dLdenc, float* wgrad_partial,
+                                float* loss_partial, const LevelInfo* levels, uint32_t n_blocks, const void* wimage,
+                                unsigned long long* prof) {
+	TCNN_CHECK(dims <= 3, "phase profile: dims <= 3");
+	FusedTrainArgs a{};
+	a.wimage = (const _Float16*)wimage;
+	a.B = B; a.dims = dims; a.loss_scale = 128.0f; a.n_total = (float)(B * dims);
+	a.params = (const _Float16*)params16; a.table = (const uint32_t*)table16; a.pos = pos; a.target = target;
+	a.out = nullptr; a.dLdenc = (uint32_t*)dLdenc; a.wgrad_partial = wgrad_partial; a.loss_partial = loss_partial;
+	a.levels = levels; a.hash_grid = 1; a.interp = (uint32_t)Interp::Linear; a.dout = nullptr; a.prof = prof;
+	hipLaunchKernelGGL((k_fused_train_pipe<64, 32, 2, HashType::CoherentPrime, Act::ReLU, false, true>), dim3(n_blocks), dim3(512), 0, st, a);
 	TCNN_HIP_CHECK(hipGetLastError());
 }
 
@@ -324,7 +368,7 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_sliced(
 	__syncthreads();
 	const uint32_t i0 = blockIdx.y * pts_per_chunk;
 	const uint32_t i1 = min(B, i0 + pts_per_chunk);
-	constexpr uint32_t U = 4;  // points in flight per thread
+	constexpr uint32_t U = 8;  // points in flight per thread
 	for (uint32_t base = i0 + threadIdx.x; base < i1; base += U * blockDim.x) {
 		float xs[U][D], dy[U][F];
 #pragma unroll

@@ -43,13 +43,18 @@ __device__ __forceinline__ h4 act_fwd(f4 v) {
 	return __builtin_convertvector(v, h4);
 }
 
-// activation transfer given the post-activation value (reference common_device.h:240-297)
+// activation transfer given the post-activation value (reference common_device.h:240-297).
+// ReLU: fwd > 0 ? g : 0. act_fwd only produces +0 or positive values (never -0 or NaN), so the test
+// is "fwd bits != 0", done on packed u16 lanes: mask = 0 - min(bits, 1) keeps both halves of a
+// register packed (per-half compares would unpack the activations into one VGPR per half).
+typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
 template <Act A>
 __device__ __forceinline__ h4 act_bwd(h4 fwd, f4 g) {
 	h4 r = __builtin_convertvector(g, h4);
 	if constexpr (A == Act::ReLU) {
-#pragma unroll
-		for (int k = 0; k < 4; ++k) r[k] = fwd[k] > (_Float16)0.0f ? r[k] : (_Float16)0.0f;
+		const u16x4 one = {1, 1, 1, 1}, zero = {0, 0, 0, 0};
+		const u16x4 m = zero - __builtin_elementwise_min(__builtin_bit_cast(u16x4, fwd), one);
+		r = __builtin_bit_cast(h4, __builtin_bit_cast(u16x4, r) & m);
 	}
 	return r;
 }
@@ -73,65 +78,107 @@ __device__ __forceinline__ h8 lds_trfrag(const _Float16* S, int rs, int q, int c
 	return cat8(__builtin_bit_cast(h4, lo), __builtin_bit_cast(h4, hi));
 }
 
+// A operand of a TRANSPOSED row-major LDS matrix M[k][m] (row stride rs halves), i.e. A[m][k] = M[k][m]
+// with m = col0 + c and k permuted as k_s(8q+e) = k0 + 16(e>>2) + 4q + (e&3): two transpose reads, so no
+// W^T copy is kept in LDS.
+__device__ __forceinline__ h8 lds_wtfrag(const _Float16* M, int rs, int k0, int col0, int q, int c) {
+	typedef __attribute__((address_space(3))) s4 lds_s4;
+	const int row = k0 + 4 * q + (c >> 2);
+	const int col = col0 + 4 * (c & 3);
+	const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(M + row * rs + col));
+	const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(M + (row + 16) * rs + col));
+	return cat8(__builtin_bit_cast(h4, lo), __builtin_bit_cast(h4, hi));
+}
+
+// Same for a 16-row matrix whose k range is the 16 outputs: k = 4q + e for e < 4, zero for e >= 4.
+__device__ __forceinline__ h8 lds_wtfrag16(const _Float16* M, int rs, int col0, int q, int c) {
+	typedef __attribute__((address_space(3))) s4 lds_s4;
+	const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(M + (4 * q + (c >> 2)) * rs + col0 + 4 * (c & 3)));
+	return cat8(__builtin_bit_cast(h4, lo), zero4());
+}
+
 __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Byte address of an LDS object (for M0).
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+	return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// LDS-DMA of one dword per lane: LDS[lds_byte + 4 * lane] = *(const uint32_t*)((const char*)base + voff).
+// Issued from inline asm on purpose: the compiler then inserts no vmcnt waits for it (its alias
+// tracking of LDS-DMA is conservative and would drain the prefetch at the first staging store);
+// the kernel waits with explicit s_waitcnt vmcnt(0) before reading the destination. lds_byte must
+// be wave-uniform. M0 is restored in the same statement (compiler-reserved register).
+__device__ __forceinline__ void glds_dword(const void* base, uint32_t voff, uint32_t lds_byte) {
+	uint32_t keep;
+	const uint32_t m0v = (uint32_t)__builtin_amdgcn_readfirstlane(lds_byte);
+	asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
+	             : "=&s"(keep)
+	             : "v"(voff), "s"(base), "s"(m0v)
+	             : "memory");
+}
 
 template <int W, int IN, int NH>
 struct FusedLayout {
 	static_assert(W % 32 == 0 && IN % 32 == 0 && NH >= 1, "fused MLP: W, IN multiples of 32");
 	static constexpr int NT = W / 16, KW = W / 32, NTI = IN / 16, KI = IN / 32;
 	static constexpr int NHM = NH - 1;  // hidden WxW matrices
-	static constexpr int RSI = IN + 8, RSW = W + 8, RSO = 24;
+	static constexpr int RSI = IN + 8, RSW = W + 8;
 	static constexpr int RSS = (W > IN ? W : IN) + 8;
+	// weight image (row-major, padded rows): W0 [W][RSI] | Wh [NHM][W][RSW] | Wo [16][RSW]
 	static constexpr int oW0 = 0;
-	static constexpr int oW0T = oW0 + W * RSI;
-	static constexpr int oWh = oW0T + IN * RSW;
-	static constexpr int oWhT = oWh + NHM * W * RSW;
-	static constexpr int oWo = oWhT + NHM * W * RSW;
-	static constexpr int oWoT = oWo + 16 * RSW;
-	static constexpr int oStage = oWoT + W * RSO;
-	static constexpr int STAGE = 32 * RSS;  // one [32][RSS] buffer
-	static constexpr int WAVES = 4;
-	static constexpr int oEnd = oStage + WAVES * 2 * STAGE;
-	static constexpr int LVL_BYTES = oEnd * 2;          // LevelInfo table (byte offset)
+	static constexpr int oWh = oW0 + W * RSI;
+	static constexpr int oWo = oWh + NHM * W * RSW;
+	static constexpr int oStage = oWo + 16 * RSW;  // = weight image size in halves
+	static constexpr int STAGE = 32 * RSS;         // one [32 samples][RSS] staging buffer
 	static constexpr int N_MLP = W * IN + NHM * W * W + 16 * W;
-	static constexpr int BYTES_MAIN = LVL_BYTES + (int)MAX_LEVELS * 16;
-	static constexpr int BYTES_RED = (N_MLP + 4) * 4;
-	static constexpr int BYTES = BYTES_MAIN > BYTES_RED ? BYTES_MAIN : BYTES_RED;
-	static_assert(oW0T % 8 == 0 && oWh % 8 == 0 && oWhT % 8 == 0 && oWo % 8 == 0 && oWoT % 8 == 0 && oStage % 8 == 0, "16B alignment");
+	static_assert(oWh % 8 == 0 && oWo % 8 == 0 && oStage % 8 == 0, "16B alignment");
 };
 
-// Cooperative copy of the fp16 weights into LDS, row-major and transposed, padded rows.
+// Register-gather kernel (any D): 4 waves per workgroup, dynamic LDS.
+template <int W, int IN, int NH>
+struct RegKernelLayout {
+	using L = FusedLayout<W, IN, NH>;
+	static constexpr int WAVES = 4;
+	static constexpr int oEnd = L::oStage + WAVES * 2 * L::STAGE;
+	static constexpr int LVL_BYTES = oEnd * 2;          // LevelInfo table (byte offset)
+	static constexpr int BYTES_MAIN = LVL_BYTES + (int)MAX_LEVELS * 16;
+	static constexpr int BYTES_RED = (2 * L::N_MLP + 2 * WAVES) * 4;
+	static constexpr int BYTES = BYTES_MAIN > BYTES_RED ? BYTES_MAIN : BYTES_RED;
+};
+
+// Pipelined kernel (D = 2): 8 waves, one workgroup per CU, static LDS (see k_fused_train_pipe).
+template <int W, int IN, int NH>
+struct PipeLayout {
+	using L = FusedLayout<W, IN, NH>;
+	static constexpr int WAVES = 8;
+	static constexpr int NLV = 4 * L::KI;                // levels per lane per 16-sample tile
+	static constexpr int NG = 2 * NLV * 4;               // gather instructions per slice (2 tiles, 4 corners)
+	static constexpr int MAIN_HALVES_W = L::oStage + WAVES * 2 * L::STAGE;
+	static constexpr int MAIN_HALVES_R = 2 * (2 * L::N_MLP + 2 * WAVES);
+	static constexpr int MAIN_HALVES = MAIN_HALVES_W > MAIN_HALVES_R ? MAIN_HALVES_W : MAIN_HALVES_R;
+	static constexpr int TGT = 96;                       // targets of one slice, dims <= 3
+	static constexpr int BYTES = MAIN_HALVES * 2 + WAVES * (NG * 256 + 2 * 256 + TGT * 4) + (IN / 2) * 16;
+	static constexpr bool FITS = BYTES <= 163840;
+};
+
+// Fold the fp16 weights into the padded row-major LDS image.
 template <int W, int IN, int NH>
 __device__ __forceinline__ void load_weights_lds(_Float16* smem, const _Float16* __restrict__ params, int tid, int nthreads) {
 	using L = FusedLayout<W, IN, NH>;
 	const uint16_t* p = (const uint16_t*)params;
 	uint16_t* s = (uint16_t*)smem;
-	for (int idx = tid; idx < W * IN; idx += nthreads) {
-		const int n = idx / IN, k = idx % IN;
-		const uint16_t v = p[idx];
-		s[L::oW0 + n * L::RSI + k] = v;
-		s[L::oW0T + k * L::RSW + n] = v;
-	}
+	for (int idx = tid; idx < W * IN; idx += nthreads) s[L::oW0 + (idx / IN) * L::RSI + idx % IN] = p[idx];
 	p += W * IN;
 	for (int j = 0; j < L::NHM; ++j) {
-		for (int idx = tid; idx < W * W; idx += nthreads) {
-			const int n = idx / W, k = idx % W;
-			const uint16_t v = p[idx];
-			s[L::oWh + j * W * L::RSW + n * L::RSW + k] = v;
-			s[L::oWhT + j * W * L::RSW + k * L::RSW + n] = v;
-		}
+		for (int idx = tid; idx < W * W; idx += nthreads) s[L::oWh + j * W * L::RSW + (idx / W) * L::RSW + idx % W] = p[idx];
 		p += W * W;
 	}
-	for (int idx = tid; idx < 16 * W; idx += nthreads) {
-		const int o = idx / W, k = idx % W;
-		const uint16_t v = p[idx];
-		s[L::oWo + o * L::RSW + k] = v;
-		s[L::oWoT + k * L::RSO + o] = v;
-	}
+	for (int idx = tid; idx < 16 * W; idx += nthreads) s[L::oWo + (idx / W) * L::RSW + idx % W] = p[idx];
 }
 
-// The LDS weight image (W, W^T, padded rows) is built once per step by k_pack_weights into global
-// memory; every workgroup then copies it with 16-byte loads instead of re-transposing the weights.
+// The LDS weight image is built once per step by k_pack_weights into global memory; every
+// workgroup then copies it with 16-byte loads.
 template <int W, int IN, int NH>
 __global__ void k_pack_weights(const _Float16* __restrict__ params, _Float16* __restrict__ image) {
 	load_weights_lds<W, IN, NH>(image, params, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x);
@@ -162,13 +209,299 @@ struct FusedTrainArgs {
 	uint32_t hash_grid;
 	uint32_t interp;
 	const _Float16* dout;   // EXT_DOUT: external dL/d(output) fp16 [B][16] (loss-scaled by the caller)
+	unsigned long long* prof;  // diagnostic build only: per-wave phase cycle sums [waves][8]
 };
 
-// One workgroup = 4 waves; each wave processes 32-sample slices in a grid-stride loop.
-template <int W, int IN, int NH, uint32_t D, HashType H, Act ACT, bool EXT_DOUT>
+// Diagnostic timestamps (s_memtime, in its own statement with lgkmcnt(0); compiled in only for the
+// profiling instantiation, never in the measured kernel).
+__device__ __forceinline__ unsigned long long stamp() {
+	unsigned long long t;
+	__builtin_amdgcn_sched_barrier(0);
+	asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+	__builtin_amdgcn_sched_barrier(0);
+	return t;
+}
+
+template <int W, int IN, int NH>
+struct WgradAcc {
+	using L = FusedLayout<W, IN, NH>;
+	f4 Wo[L::NT];
+	f4 H[L::NHM > 0 ? L::NHM : 1][L::NT][L::NT];
+	f4 W0[L::NT][L::NTI];
+	float loss;
+	__device__ __forceinline__ void zero() {
+		const f4 fz = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+		for (int t = 0; t < L::NT; ++t) {
+			Wo[t] = fz;
+#pragma unroll
+			for (int u = 0; u < L::NTI; ++u) W0[t][u] = fz;
+#pragma unroll
+			for (int j = 0; j < (L::NHM > 0 ? L::NHM : 1); ++j)
+#pragma unroll
+				for (int u = 0; u < L::NT; ++u) H[j][t][u] = fz;
+		}
+		loss = 0.0f;
+	}
+};
+
+// One 32-sample slice through the network: forward, output + RelativeL2 (relative_l2.h:40-76) or
+// external dL/dy, backward, weight-gradient accumulation, dL/d(encoding) stores.
+// xt: encoded input (B fragments, 16-sample tiles tau = 0, 1); target(tau, o): the target of sample
+// base + 16 tau + c, output o (read only for o < dims); after_loss(): hook run once the targets are used.
+template <int W, int IN, int NH, Act ACT, bool EXT_DOUT, bool PROF, class TargetFn, class AfterLossFn>
+__device__ __forceinline__ void fused_slice(const FusedTrainArgs& a, uint32_t base, int c, int q, const h4 (&xt)[2][IN / 16],
+                                            TargetFn target, AfterLossFn after_loss, const h4 (&Gext)[2], const _Float16* sW0,
+                                            const _Float16* sWh, const _Float16* sWo, _Float16* bufA, _Float16* bufD,
+                                            WgradAcc<W, IN, NH>& acc, unsigned long long (&ph)[8], unsigned long long& t0) {
+	using L = FusedLayout<W, IN, NH>;
+	constexpr int NT = L::NT, KW = L::KW, NTI = L::NTI, KI = L::KI;
+	const f4 fz = {0.0f, 0.0f, 0.0f, 0.0f};
+	unsigned long long t1;
+	// ---------------- forward ----------------
+	h4 act[NH][2][NT];
+	{
+		f4 ac[2][NT];
+#pragma unroll
+		for (int t = 0; t < NT; ++t) {
+			ac[0][t] = fz; ac[1][t] = fz;
+#pragma unroll
+			for (int s = 0; s < KI; ++s) {
+				const h8 af = lds_afrag(sW0, L::RSI, 16 * t + c, 32 * s + 4 * q);
+				ac[0][t] = mfma16(af, cat8(xt[0][2 * s], xt[0][2 * s + 1]), ac[0][t]);
+				ac[1][t] = mfma16(af, cat8(xt[1][2 * s], xt[1][2 * s + 1]), ac[1][t]);
+			}
+		}
+#pragma unroll
+		for (int t = 0; t < NT; ++t) { act[0][0][t] = act_fwd<ACT>(ac[0][t]); act[0][1][t] = act_fwd<ACT>(ac[1][t]); }
+	}
+#pragma unroll
+	for (int j = 1; j < NH; ++j) {
+		const _Float16* Wm = sWh + (j - 1) * W * L::RSW;
+		f4 ac[2][NT];
+#pragma unroll
+		for (int t = 0; t < NT; ++t) {
+			ac[0][t] = fz; ac[1][t] = fz;
+#pragma unroll
+			for (int s = 0; s < KW; ++s) {
+				const h8 af = lds_afrag(Wm, L::RSW, 16 * t + c, 32 * s + 4 * q);
+				ac[0][t] = mfma16(af, cat8(act[j - 1][0][2 * s], act[j - 1][0][2 * s + 1]), ac[0][t]);
+				ac[1][t] = mfma16(af, cat8(act[j - 1][1][2 * s], act[j - 1][1][2 * s + 1]), ac[1][t]);
+			}
+		}
+#pragma unroll
+		for (int t = 0; t < NT; ++t) { act[j][0][t] = act_fwd<ACT>(ac[0][t]); act[j][1][t] = act_fwd<ACT>(ac[1][t]); }
+	}
+	if constexpr (PROF) { t1 = stamp(); ph[1] += t1 - t0; t0 = t1; }
+	h4 G[2];
+	{
+		f4 yacc[2] = {fz, fz};
+#pragma unroll
+		for (int s = 0; s < KW; ++s) {
+			const h8 af = lds_afrag(sWo, L::RSW, c, 32 * s + 4 * q);
+			yacc[0] = mfma16(af, cat8(act[NH - 1][0][2 * s], act[NH - 1][0][2 * s + 1]), yacc[0]);
+			yacc[1] = mfma16(af, cat8(act[NH - 1][1][2 * s], act[NH - 1][1][2 * s + 1]), yacc[1]);
+		}
+#pragma unroll
+		for (int tau = 0; tau < 2; ++tau) {
+			const uint32_t i = base + 16 * tau + c;
+			if constexpr (EXT_DOUT) {
+				G[tau] = Gext[tau];
+				continue;
+			}
+			const h4 y = __builtin_convertvector(yacc[tau], h4);
+			if (a.out) *(h4*)(a.out + (size_t)i * 16 + 4 * q) = y;
+			h4 g = zero4();
+#pragma unroll
+			for (int r = 0; r < 4; ++r) {
+				const uint32_t o = 4 * q + r;
+				if (o < a.dims) {
+					const float p = (float)y[r];
+					const float pse = __builtin_fmaf(p, p, 0.01f);
+					const float d = p - target(tau, o);
+					acc.loss += d * d / pse / a.n_total;
+					const float gr = 2.0f * d / pse;
+					g[r] = (_Float16)(a.loss_scale * gr / a.n_total);
+				}
+			}
+			G[tau] = g;
+		}
+	}
+	after_loss();
+	if constexpr (PROF) { t1 = stamp(); ph[2] += t1 - t0; t0 = t1; }
+	// ---------------- backward + weight gradients ----------------
+	// output layer: dWout += G * act[NH-1]^T
+#pragma unroll
+	for (int tau = 0; tau < 2; ++tau) {
+		*(h4*)(bufD + (16 * tau + c) * L::RSS + 4 * q) = G[tau];
+#pragma unroll
+		for (int t = 0; t < NT; ++t) *(h4*)(bufA + (16 * tau + c) * L::RSS + 16 * t + 4 * q) = act[NH - 1][tau][t];
+	}
+	lds_fence();
+	{
+		const h8 ga = lds_trfrag(bufD, L::RSS, q, c, 0);
+#pragma unroll
+		for (int nt = 0; nt < NT; ++nt) acc.Wo[nt] = mfma16(ga, lds_trfrag(bufA, L::RSS, q, c, nt), acc.Wo[nt]);
+	}
+	h4 dl[2][NT];
+#pragma unroll
+	for (int t = 0; t < NT; ++t) {
+		const h8 af = lds_wtfrag16(sWo, L::RSW, 16 * t, q, c);
+		dl[0][t] = act_bwd<ACT>(act[NH - 1][0][t], mfma16(af, cat8(G[0], zero4()), fz));
+		dl[1][t] = act_bwd<ACT>(act[NH - 1][1][t], mfma16(af, cat8(G[1], zero4()), fz));
+	}
+#pragma unroll
+	for (int j = NH - 1; j >= 1; --j) {
+		lds_fence();
+#pragma unroll
+		for (int tau = 0; tau < 2; ++tau) {
+#pragma unroll
+			for (int t = 0; t < NT; ++t) {
+				*(h4*)(bufD + (16 * tau + c) * L::RSS + 16 * t + 4 * q) = dl[tau][t];
+				*(h4*)(bufA + (16 * tau + c) * L::RSS + 16 * t + 4 * q) = act[j - 1][tau][t];
+			}
+		}
+		lds_fence();
+		{
+			h8 bf[NT];
+#pragma unroll
+			for (int nt = 0; nt < NT; ++nt) bf[nt] = lds_trfrag(bufA, L::RSS, q, c, nt);
+#pragma unroll
+			for (int mt = 0; mt < NT; ++mt) {
+				const h8 ad = lds_trfrag(bufD, L::RSS, q, c, mt);
+#pragma unroll
+				for (int nt = 0; nt < NT; ++nt) acc.H[j - 1][mt][nt] = mfma16(ad, bf[nt], acc.H[j - 1][mt][nt]);
+			}
+		}
+		// dL/d(act[j-1]) = W_j^T dl, the B operand re-read from bufD (dl's registers are free by now)
+		const _Float16* Wm = sWh + (j - 1) * W * L::RSW;
+#pragma unroll
+		for (int t = 0; t < NT; ++t) {
+			f4 acc0 = fz, acc1 = fz;
+#pragma unroll
+			for (int s = 0; s < KW; ++s) {
+				const h8 af = lds_wtfrag(Wm, L::RSW, 32 * s, 16 * t, q, c);
+				acc0 = mfma16(af, lds_afrag(bufD, L::RSS, c, 32 * s + 4 * q), acc0);
+				acc1 = mfma16(af, lds_afrag(bufD, L::RSS, 16 + c, 32 * s + 4 * q), acc1);
+			}
+			dl[0][t] = act_bwd<ACT>(act[j - 1][0][t], acc0);
+			dl[1][t] = act_bwd<ACT>(act[j - 1][1][t], acc1);
+		}
+	}
+	if constexpr (PROF) { t1 = stamp(); ph[3] += t1 - t0; t0 = t1; }
+	// first layer: dW0 += dl * x^T ; dL/dx = W0^T dl
+	lds_fence();
+#pragma unroll
+	for (int tau = 0; tau < 2; ++tau) {
+#pragma unroll
+		for (int t = 0; t < NT; ++t) *(h4*)(bufD + (16 * tau + c) * L::RSS + 16 * t + 4 * q) = dl[tau][t];
+#pragma unroll
+		for (int u = 0; u < NTI; ++u) *(h4*)(bufA + (16 * tau + c) * L::RSS + 16 * u + 4 * q) = xt[tau][u];
+	}
+	lds_fence();
+	{
+		h8 bf[NTI];
+#pragma unroll
+		for (int u = 0; u < NTI; ++u) bf[u] = lds_trfrag(bufA, L::RSS, q, c, u);
+#pragma unroll
+		for (int mt = 0; mt < NT; ++mt) {
+			const h8 ad = lds_trfrag(bufD, L::RSS, q, c, mt);
+#pragma unroll
+			for (int u = 0; u < NTI; ++u) acc.W0[mt][u] = mfma16(ad, bf[u], acc.W0[mt][u]);
+		}
+	}
+	if constexpr (PROF) { t1 = stamp(); ph[4] += t1 - t0; t0 = t1; }
+#pragma unroll
+	for (int u = 0; u < NTI; ++u) {
+		f4 acc0 = fz, acc1 = fz;
+#pragma unroll
+		for (int s = 0; s < KW; ++s) {
+			const h8 af = lds_wtfrag(sW0, L::RSI, 32 * s, 16 * u, q, c);
+			acc0 = mfma16(af, lds_afrag(bufD, L::RSS, c, 32 * s + 4 * q), acc0);
+			acc1 = mfma16(af, lds_afrag(bufD, L::RSS, 16 + c, 32 * s + 4 * q), acc1);
+		}
+		const h4 d0 = __builtin_convertvector(acc0, h4);
+		const h4 d1 = __builtin_convertvector(acc1, h4);
+		const uint32_t lv = 8 * u + 2 * q;  // features 16u + 4q + r -> levels lv (r=0,1), lv+1 (r=2,3)
+		const uint32_t i0 = base + c, i1 = base + 16 + c;
+		a.dLdenc[(size_t)lv * a.B + i0] = __builtin_bit_cast(uint32_t, h2{d0[0], d0[1]});
+		a.dLdenc[(size_t)(lv + 1) * a.B + i0] = __builtin_bit_cast(uint32_t, h2{d0[2], d0[3]});
+		a.dLdenc[(size_t)lv * a.B + i1] = __builtin_bit_cast(uint32_t, h2{d1[0], d1[1]});
+		a.dLdenc[(size_t)(lv + 1) * a.B + i1] = __builtin_bit_cast(uint32_t, h2{d1[2], d1[3]});
+	}
+	if constexpr (PROF) { t1 = stamp(); ph[5] += t1 - t0; t0 = t1; }
+}
+
+// Workgroup reduction of the per-wave dW / loss registers into this block's fp32 partial slab.
+// Deterministic pairwise tree over the waves through two LDS slabs (plain loads/stores: gfx950 LDS
+// float atomics are ~24x slower than integer ones and would make the order data-dependent).
+template <int W, int IN, int NH, int WAVES>
+__device__ __forceinline__ void block_reduce_wgrad(WgradAcc<W, IN, NH>& acc, float* slab, const FusedTrainArgs& a,
+                                                   int tid, int wave, int lane) {
+	using L = FusedLayout<W, IN, NH>;
+	constexpr int NT = L::NT, NTI = L::NTI, NHM = L::NHM, N = L::N_MLP;
+	constexpr int oH = W * IN, oO = W * IN + NHM * W * W;
+	const int c = lane & 15, q = lane >> 4;
+#pragma unroll
+	for (int off = 32; off > 0; off >>= 1) acc.loss += __shfl_xor(acc.loss, off);
+	float* lsum = slab + 2 * N;  // [WAVES] per-wave loss
+	if (lane == 0) lsum[wave] = acc.loss;
+	// slab element of this lane's accumulator register (mt/nt tile, r row) -- same map for write/add
+	auto visit = [&](float* S, bool add) {
+#pragma unroll
+		for (int mt = 0; mt < NT; ++mt) {
+#pragma unroll
+			for (int r = 0; r < 4; ++r) {
+				const int n = 16 * mt + 4 * q + r;
+#pragma unroll
+				for (int u = 0; u < NTI; ++u) {
+					float* p = &S[n * IN + 16 * u + c];
+					if (add) acc.W0[mt][u][r] += *p; else *p = acc.W0[mt][u][r];
+				}
+#pragma unroll
+				for (int j = 0; j < NHM; ++j)
+#pragma unroll
+					for (int nt = 0; nt < NT; ++nt) {
+						float* p = &S[oH + j * W * W + n * W + 16 * nt + c];
+						if (add) acc.H[j][mt][nt][r] += *p; else *p = acc.H[j][mt][nt][r];
+					}
+			}
+		}
+#pragma unroll
+		for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+			for (int r = 0; r < 4; ++r) {
+				float* p = &S[oO + (4 * q + r) * W + 16 * nt + c];
+				if (add) acc.Wo[nt][r] += *p; else *p = acc.Wo[nt][r];
+			}
+	};
+	for (int r = WAVES / 2; r >= 1; r >>= 1) {
+		for (int h = 0; h < r; h += 2) {
+			// writers r+h, r+h+1 -> slabs 0, 1 ; readers h, h+1 add them
+			if (wave >= r + h && wave < r + h + 2 && wave < 2 * r) visit(slab + (wave - r - h) * N, false);
+			__syncthreads();
+			if (wave >= h && wave < h + 2 && wave < r) visit(slab + (wave - h) * N, true);
+			__syncthreads();
+		}
+	}
+	if (wave == 0) visit(slab, false);
+	__syncthreads();
+	float* dst = a.wgrad_partial + (size_t)blockIdx.x * N;
+	for (int p = tid; p < N; p += WAVES * 64) dst[p] = slab[p];
+	if (tid == 0) {
+		float l = 0.0f;
+		for (int w = 0; w < WAVES; ++w) l += lsum[w];
+		a.loss_partial[blockIdx.x] = l;
+	}
+}
+
+// Register-gather variant, any D: one workgroup = 4 waves, each wave runs 32-sample slices in a
+// grid-stride loop; the grid encoding's gathers go straight to registers.
+template <int W, int IN, int NH, uint32_t D, HashType H, Act ACT, bool EXT_DOUT, bool PROF = false>
 __global__ __launch_bounds__(256, 2) void k_fused_train_grid(const FusedTrainArgs a) {
 	using L = FusedLayout<W, IN, NH>;
-	constexpr int NT = L::NT, KW = L::KW, NTI = L::NTI, KI = L::KI, NHM = L::NHM;
+	using RL = RegKernelLayout<W, IN, NH>;
+	constexpr int NTI = L::NTI, KI = L::KI;
 	constexpr int NLVL = IN / 2;
 	extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
 
@@ -176,280 +509,211 @@ __global__ __launch_bounds__(256, 2) void k_fused_train_grid(const FusedTrainArg
 	const int c = lane & 15, q = lane >> 4;
 
 	copy_image_to_lds(smem, a.wimage, L::oStage, tid, 256);
-	LevelInfo* sLvl = (LevelInfo*)((char*)smem + L::LVL_BYTES);
+	LevelInfo* sLvl = (LevelInfo*)((char*)smem + RL::LVL_BYTES);
 	for (int l = tid; l < NLVL; l += 256) sLvl[l] = a.levels[l];
 	__syncthreads();
 
-	const _Float16* sW0 = smem + L::oW0;
-	const _Float16* sW0T = smem + L::oW0T;
-	const _Float16* sWh = smem + L::oWh;
-	const _Float16* sWhT = smem + L::oWhT;
-	const _Float16* sWo = smem + L::oWo;
-	const _Float16* sWoT = smem + L::oWoT;
 	_Float16* bufA = smem + L::oStage + wave * 2 * L::STAGE;
 	_Float16* bufD = bufA + L::STAGE;
-
-	f4 accWo[NT];
-	f4 accH[NHM > 0 ? NHM : 1][NT][NT];
-	f4 accW0[NT][NTI];
-	const f4 fz = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-	for (int t = 0; t < NT; ++t) {
-		accWo[t] = fz;
-#pragma unroll
-		for (int u = 0; u < NTI; ++u) accW0[t][u] = fz;
-#pragma unroll
-		for (int j = 0; j < (NHM > 0 ? NHM : 1); ++j)
-#pragma unroll
-			for (int u = 0; u < NT; ++u) accH[j][t][u] = fz;
-	}
-	float loss_acc = 0.0f;
-
+	WgradAcc<W, IN, NH> acc;
+	acc.zero();
 	const bool hash_grid = a.hash_grid != 0;
 	const Interp interp = (Interp)a.interp;
 	const uint32_t n_chunks = a.B / 32;
 
+	unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+	unsigned long long t0 = 0, t1 = 0;
+	if constexpr (PROF) t0 = stamp();
 	for (uint32_t chunk = blockIdx.x * 4 + wave; chunk < n_chunks; chunk += gridDim.x * 4) {
 		const uint32_t base = chunk * 32;
-
-		// ---------------- grid encoding -> B fragments (tiles of 4 features) ----------------
 		h4 xt[2][NTI];
+		h4 Gext[2];
 #pragma unroll
 		for (int tau = 0; tau < 2; ++tau) {
 			const uint32_t i = base + 16 * tau + c;
 			float x[D];
 #pragma unroll
 			for (uint32_t d = 0; d < D; ++d) x[d] = a.pos[(size_t)i * D + d];
+			if constexpr (EXT_DOUT) Gext[tau] = *(const h4*)(a.dout + (size_t)i * 16 + 4 * q);
 #pragma unroll
 			for (int s = 0; s < KI; ++s) {
 #pragma unroll
 				for (int pp = 0; pp < 4; ++pp) {
 					const int level = 16 * s + 8 * (pp >> 1) + 2 * q + (pp & 1);
-					const LevelInfo li = sLvl[level];
-					const h2 e = encode_level_f2<D, H>(a.table, li, hash_grid, interp, x);
+					const h2 e = encode_level_f2<D, H>(a.table, sLvl[level], hash_grid, interp, x);
 					xt[tau][2 * s + (pp >> 1)][2 * (pp & 1) + 0] = e[0];
 					xt[tau][2 * s + (pp >> 1)][2 * (pp & 1) + 1] = e[1];
 				}
 			}
 		}
-
-		// ---------------- forward ----------------
-		h4 act[NH][2][NT];
-		{
-			f4 acc[2][NT];
-#pragma unroll
-			for (int t = 0; t < NT; ++t) {
-				acc[0][t] = fz; acc[1][t] = fz;
-#pragma unroll
-				for (int s = 0; s < KI; ++s) {
-					const h8 af = lds_afrag(sW0, L::RSI, 16 * t + c, 32 * s + 4 * q);
-					acc[0][t] = mfma16(af, cat8(xt[0][2 * s], xt[0][2 * s + 1]), acc[0][t]);
-					acc[1][t] = mfma16(af, cat8(xt[1][2 * s], xt[1][2 * s + 1]), acc[1][t]);
-				}
-			}
-#pragma unroll
-			for (int t = 0; t < NT; ++t) { act[0][0][t] = act_fwd<ACT>(acc[0][t]); act[0][1][t] = act_fwd<ACT>(acc[1][t]); }
-		}
-#pragma unroll
-		for (int j = 1; j < NH; ++j) {
-			const _Float16* Wm = sWh + (j - 1) * W * L::RSW;
-			f4 acc[2][NT];
-#pragma unroll
-			for (int t = 0; t < NT; ++t) {
-				acc[0][t] = fz; acc[1][t] = fz;
-#pragma unroll
-				for (int s = 0; s < KW; ++s) {
-					const h8 af = lds_afrag(Wm, L::RSW, 16 * t + c, 32 * s + 4 * q);
-					acc[0][t] = mfma16(af, cat8(act[j - 1][0][2 * s], act[j - 1][0][2 * s + 1]), acc[0][t]);
-					acc[1][t] = mfma16(af, cat8(act[j - 1][1][2 * s], act[j - 1][1][2 * s + 1]), acc[1][t]);
-				}
-			}
-#pragma unroll
-			for (int t = 0; t < NT; ++t) { act[j][0][t] = act_fwd<ACT>(acc[0][t]); act[j][1][t] = act_fwd<ACT>(acc[1][t]); }
-		}
-		h4 G[2];
-		{
-			f4 yacc[2] = {fz, fz};
-#pragma unroll
-			for (int s = 0; s < KW; ++s) {
-				const h8 af = lds_afrag(sWo, L::RSW, c, 32 * s + 4 * q);
-				yacc[0] = mfma16(af, cat8(act[NH - 1][0][2 * s], act[NH - 1][0][2 * s + 1]), yacc[0]);
-				yacc[1] = mfma16(af, cat8(act[NH - 1][1][2 * s], act[NH - 1][1][2 * s + 1]), yacc[1]);
-			}
-			// ---------------- RelativeL2 loss (relative_l2.h:40-76) ----------------
-#pragma unroll
-			for (int tau = 0; tau < 2; ++tau) {
-				const uint32_t i = base + 16 * tau + c;
-				if constexpr (EXT_DOUT) {
-					G[tau] = *(const h4*)(a.dout + (size_t)i * 16 + 4 * q);
-					continue;
-				}
-				const h4 y = __builtin_convertvector(yacc[tau], h4);
-				if (a.out) *(h4*)(a.out + (size_t)i * 16 + 4 * q) = y;
-				h4 g = zero4();
-#pragma unroll
-				for (int r = 0; r < 4; ++r) {
-					const uint32_t o = 4 * q + r;
-					if (o < a.dims) {
-						const float p = (float)y[r];
-						const float pse = __builtin_fmaf(p, p, 0.01f);
-						const float d = p - a.target[(size_t)i * a.dims + o];
-						loss_acc += d * d / pse / a.n_total;
-						const float gr = 2.0f * d / pse;
-						g[r] = (_Float16)(a.loss_scale * gr / a.n_total);
-					}
-				}
-				G[tau] = g;
-			}
-		}
-
-		// ---------------- backward + weight gradients ----------------
-		// output layer: dWout += G * act[NH-1]^T
-#pragma unroll
-		for (int tau = 0; tau < 2; ++tau) {
-			*(h4*)(bufD + (16 * tau + c) * L::RSS + 4 * q) = G[tau];
-#pragma unroll
-			for (int t = 0; t < NT; ++t) *(h4*)(bufA + (16 * tau + c) * L::RSS + 16 * t + 4 * q) = act[NH - 1][tau][t];
-		}
-		lds_fence();
-		{
-			const h8 ga = lds_trfrag(bufD, L::RSS, q, c, 0);
-#pragma unroll
-			for (int nt = 0; nt < NT; ++nt) accWo[nt] = mfma16(ga, lds_trfrag(bufA, L::RSS, q, c, nt), accWo[nt]);
-		}
-		h4 dl[2][NT];
-#pragma unroll
-		for (int t = 0; t < NT; ++t) {
-			const h8 af = cat8(*(const h4*)(sWoT + (16 * t + c) * L::RSO + 4 * q), zero4());
-			dl[0][t] = act_bwd<ACT>(act[NH - 1][0][t], mfma16(af, cat8(G[0], zero4()), fz));
-			dl[1][t] = act_bwd<ACT>(act[NH - 1][1][t], mfma16(af, cat8(G[1], zero4()), fz));
-		}
-#pragma unroll
-		for (int j = NH - 1; j >= 1; --j) {
-			lds_fence();
-#pragma unroll
-			for (int tau = 0; tau < 2; ++tau) {
-#pragma unroll
-				for (int t = 0; t < NT; ++t) {
-					*(h4*)(bufD + (16 * tau + c) * L::RSS + 16 * t + 4 * q) = dl[tau][t];
-					*(h4*)(bufA + (16 * tau + c) * L::RSS + 16 * t + 4 * q) = act[j - 1][tau][t];
-				}
-			}
-			lds_fence();
-			{
-				h8 bf[NT];
-#pragma unroll
-				for (int nt = 0; nt < NT; ++nt) bf[nt] = lds_trfrag(bufA, L::RSS, q, c, nt);
-#pragma unroll
-				for (int mt = 0; mt < NT; ++mt) {
-					const h8 ad = lds_trfrag(bufD, L::RSS, q, c, mt);
-#pragma unroll
-					for (int nt = 0; nt < NT; ++nt) accH[j - 1][mt][nt] = mfma16(ad, bf[nt], accH[j - 1][mt][nt]);
-				}
-			}
-			const _Float16* WT = sWhT + (j - 1) * W * L::RSW;
-			h4 ndl[2][NT];
-#pragma unroll
-			for (int t = 0; t < NT; ++t) {
-				f4 acc0 = fz, acc1 = fz;
-#pragma unroll
-				for (int s = 0; s < KW; ++s) {
-					const h8 af = lds_afrag(WT, L::RSW, 16 * t + c, 32 * s + 4 * q);
-					acc0 = mfma16(af, cat8(dl[0][2 * s], dl[0][2 * s + 1]), acc0);
-					acc1 = mfma16(af, cat8(dl[1][2 * s], dl[1][2 * s + 1]), acc1);
-				}
-				ndl[0][t] = act_bwd<ACT>(act[j - 1][0][t], acc0);
-				ndl[1][t] = act_bwd<ACT>(act[j - 1][1][t], acc1);
-			}
-#pragma unroll
-			for (int t = 0; t < NT; ++t) { dl[0][t] = ndl[0][t]; dl[1][t] = ndl[1][t]; }
-		}
-		// first layer: dW0 += dl * x^T ; dL/dx = W0^T dl
-		lds_fence();
-#pragma unroll
-		for (int tau = 0; tau < 2; ++tau) {
-#pragma unroll
-			for (int t = 0; t < NT; ++t) *(h4*)(bufD + (16 * tau + c) * L::RSS + 16 * t + 4 * q) = dl[tau][t];
-#pragma unroll
-			for (int u = 0; u < NTI; ++u) *(h4*)(bufA + (16 * tau + c) * L::RSS + 16 * u + 4 * q) = xt[tau][u];
-		}
-		lds_fence();
-		{
-			h8 bf[NTI];
-#pragma unroll
-			for (int u = 0; u < NTI; ++u) bf[u] = lds_trfrag(bufA, L::RSS, q, c, u);
-#pragma unroll
-			for (int mt = 0; mt < NT; ++mt) {
-				const h8 ad = lds_trfrag(bufD, L::RSS, q, c, mt);
-#pragma unroll
-				for (int u = 0; u < NTI; ++u) accW0[mt][u] = mfma16(ad, bf[u], accW0[mt][u]);
-			}
-		}
-#pragma unroll
-		for (int u = 0; u < NTI; ++u) {
-			f4 acc0 = fz, acc1 = fz;
-#pragma unroll
-			for (int s = 0; s < KW; ++s) {
-				const h8 af = lds_afrag(sW0T, L::RSW, 16 * u + c, 32 * s + 4 * q);
-				acc0 = mfma16(af, cat8(dl[0][2 * s], dl[0][2 * s + 1]), acc0);
-				acc1 = mfma16(af, cat8(dl[1][2 * s], dl[1][2 * s + 1]), acc1);
-			}
-			const h4 d0 = __builtin_convertvector(acc0, h4);
-			const h4 d1 = __builtin_convertvector(acc1, h4);
-			const uint32_t lv = 8 * u + 2 * q;  // features 16u + 4q + r -> levels lv (r=0,1), lv+1 (r=2,3)
-			const uint32_t i0 = base + c, i1 = base + 16 + c;
-			a.dLdenc[(size_t)lv * a.B + i0] = __builtin_bit_cast(uint32_t, h2{d0[0], d0[1]});
-			a.dLdenc[(size_t)(lv + 1) * a.B + i0] = __builtin_bit_cast(uint32_t, h2{d0[2], d0[3]});
-			a.dLdenc[(size_t)lv * a.B + i1] = __builtin_bit_cast(uint32_t, h2{d1[0], d1[1]});
-			a.dLdenc[(size_t)(lv + 1) * a.B + i1] = __builtin_bit_cast(uint32_t, h2{d1[2], d1[3]});
+		if constexpr (PROF) { t1 = stamp(); ph[0] += t1 - t0; t0 = t1; }
+		auto target = [&](int tau, uint32_t o) { return a.target[(size_t)(base + 16 * tau + c) * a.dims + o]; };
+		auto after_loss = [] {};
+		fused_slice<W, IN, NH, ACT, EXT_DOUT, PROF>(a, base, c, q, xt, target, after_loss, Gext, smem + L::oW0,
+		                                            smem + L::oWh, smem + L::oWo, bufA, bufD, acc, ph, t0);
+	}
+	if constexpr (PROF) {
+		if (lane == 0) {
+			unsigned long long* o = a.prof + (size_t)(blockIdx.x * 4 + wave) * 8;
+			for (int k = 0; k < 6; ++k) o[k] = ph[k];
 		}
 	}
-
-	// ---------------- workgroup reduction of dW and loss -> partial slabs ----------------
-	// Waves add their register accumulators into one LDS slab in fixed wave order (plain LDS
-	// loads/stores: gfx950 LDS float atomics are ~24x slower than integer ones, and a fixed order
-	// keeps the partial bit-reproducible).
 	__syncthreads();
-	float* red = (float*)smem;
-	constexpr int oH = W * IN, oO = W * IN + NHM * W * W;
-#pragma unroll
-	for (int off = 32; off > 0; off >>= 1) loss_acc += __shfl_xor(loss_acc, off);
-	for (int w = 0; w < 4; ++w) {
-		if (wave == w) {
-			const bool first = (w == 0);
-#pragma unroll
-			for (int mt = 0; mt < NT; ++mt) {
-#pragma unroll
-				for (int r = 0; r < 4; ++r) {
-					const int n = 16 * mt + 4 * q + r;
-#pragma unroll
-					for (int u = 0; u < NTI; ++u) {
-						float* p = &red[n * IN + 16 * u + c];
-						*p = first ? accW0[mt][u][r] : *p + accW0[mt][u][r];
-					}
-#pragma unroll
-					for (int j = 0; j < NHM; ++j)
-#pragma unroll
-						for (int nt = 0; nt < NT; ++nt) {
-							float* p = &red[oH + j * W * W + n * W + 16 * nt + c];
-							*p = first ? accH[j][mt][nt][r] : *p + accH[j][mt][nt][r];
-						}
-				}
-			}
-#pragma unroll
-			for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-				for (int r = 0; r < 4; ++r) {
-					float* p = &red[oO + (4 * q + r) * W + 16 * nt + c];
-					*p = first ? accWo[nt][r] : *p + accWo[nt][r];
-				}
-			if (lane == 0) red[L::N_MLP + w] = loss_acc;
+	block_reduce_wgrad<W, IN, NH, 4>(acc, (float*)smem, a, tid, wave, lane);
+}
+
+// Pipelined variant for 2D grids: one workgroup of 8 waves per CU. The table gathers are the
+// kernel's bottleneck resource (the texture-address unit handles ~one lane per cycle for these
+// divergent 4-byte reads), so they are issued ONE SLICE AHEAD as LDS-DMA loads
+// (global_load_lds_dword: 64 lanes -> 256 contiguous LDS bytes, no VGPRs held) and land while the
+// wave runs the MLP of the current slice; positions and targets of the next slices ride along
+// the same way. Each wave's slice loop:
+//   wait vmcnt(0) -> read gathered corners / next positions / targets from LDS
+//   -> fp16 FMA interpolation of the current slice (weights recomputed from its positions)
+//   -> issue next slice's corner gathers + positions(+2) + targets(+1)  -> MLP of current slice.
+template <int W, int IN, int NH, HashType H, Act ACT, bool EXT_DOUT, bool PROF = false>
+__global__ __launch_bounds__(512, 1) void k_fused_train_pipe(const FusedTrainArgs a) {
+	using L = FusedLayout<W, IN, NH>;
+	using P = PipeLayout<W, IN, NH>;
+	constexpr int NTI = L::NTI, WAVES = P::WAVES, NLV = P::NLV, NG = P::NG;
+	constexpr int NLVL = IN / 2;
+	static_assert(P::FITS, "pipelined fused kernel: LDS budget");
+	__shared__ __attribute__((aligned(16))) _Float16 s_main[P::MAIN_HALVES];
+	__shared__ __attribute__((aligned(16))) uint32_t s_gath[WAVES][NG * 64];
+	__shared__ __attribute__((aligned(16))) float s_pos[WAVES][2][64];  // two slots: slice parity
+	__shared__ __attribute__((aligned(16))) float s_tgt[WAVES][P::TGT];
+	__shared__ LevelInfo s_lvl[NLVL];
+
+	const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+	const int c = lane & 15, q = lane >> 4;
+	unsigned long long t_kernel = 0;
+	if constexpr (PROF) t_kernel = stamp();
+	copy_image_to_lds(s_main, a.wimage, L::oStage, tid, WAVES * 64);
+	for (int l = tid; l < NLVL; l += WAVES * 64) s_lvl[l] = a.levels[l];
+	__syncthreads();
+
+	_Float16* bufA = s_main + L::oStage + wave * 2 * L::STAGE;
+	_Float16* bufD = bufA + L::STAGE;
+	uint32_t* gb = s_gath[wave];
+	float* pb0 = s_pos[wave][0];
+	float* pb1 = s_pos[wave][1];
+	float* tb = s_tgt[wave];
+	WgradAcc<W, IN, NH> acc;
+	acc.zero();
+	const bool hash_grid = a.hash_grid != 0;
+	const Interp interp = (Interp)a.interp;
+	const uint32_t n_chunks = a.B / 32;
+	const uint32_t stride = gridDim.x * WAVES;
+	const uint32_t dims = a.dims;
+
+	const uint32_t gb_lds = lds_addr(gb), tb_lds = lds_addr(tb), pb_lds = lds_addr(pb0);  // pb1 = pb0 + 256 B
+	auto issue_pos = [&](uint32_t ch, uint32_t slot) { glds_dword(a.pos, (ch * 64 + lane) * 4, pb_lds + 256 * slot); };
+	auto issue_tgt = [&](uint32_t ch) {
+		if constexpr (!EXT_DOUT) {
+			const uint32_t n = 32 * dims;  // <= 96
+			if ((uint32_t)lane < n) glds_dword(a.target, (ch * n + lane) * 4, tb_lds);
+			if ((uint32_t)lane + 64 < n) glds_dword(a.target, (ch * n + 64 + lane) * 4, tb_lds + 256);
 		}
-		__syncthreads();
+	};
+	auto issue_gathers = [&](const float (&x)[2][2]) {
+#pragma unroll
+		for (int tau = 0; tau < 2; ++tau)
+#pragma unroll
+			for (int lv = 0; lv < NLV; ++lv) {
+				const int s = lv >> 2, pp = lv & 3;
+				const int level = 16 * s + 8 * (pp >> 1) + 2 * q + (pp & 1);
+				uint32_t idx[4];
+				_Float16 w16[4];
+				level_corners<2, H>(s_lvl[level], hash_grid, interp, x[tau], idx, w16);
+#pragma unroll
+				for (int cc = 0; cc < 4; ++cc) glds_dword(a.table, idx[cc] * 4, gb_lds + ((tau * NLV + lv) * 4 + cc) * 256);
+			}
+	};
+
+	unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+	unsigned long long t0 = 0, t1 = 0;
+	uint32_t chunk = blockIdx.x * WAVES + wave;
+	auto read_x = [&](const float* slot, float (&x)[2][2]) {
+#pragma unroll
+		for (int tau = 0; tau < 2; ++tau) { x[tau][0] = slot[(16 * tau + c) * 2]; x[tau][1] = slot[(16 * tau + c) * 2 + 1]; }
+	};
+	if (chunk < n_chunks) {
+		issue_pos(chunk, 0);
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		float x0[2][2];
+		read_x(pb0, x0);
+		lds_fence();
+		issue_gathers(x0);
+		if (chunk + stride < n_chunks) issue_pos(chunk + stride, 1);
+		issue_tgt(chunk);
 	}
-	float* dst = a.wgrad_partial + (size_t)blockIdx.x * L::N_MLP;
-	for (int p = tid; p < L::N_MLP; p += 256) dst[p] = red[p];
-	if (tid == 0) a.loss_partial[blockIdx.x] = red[L::N_MLP] + red[L::N_MLP + 1] + red[L::N_MLP + 2] + red[L::N_MLP + 3];
+	if constexpr (PROF) { t0 = stamp(); ph[6] = t0 - t_kernel; }
+	uint32_t par = 0;  // slot holding this slice's positions
+	for (; chunk < n_chunks; chunk += stride, par ^= 1u) {
+		const uint32_t base = chunk * 32;
+		const bool nxt = chunk + stride < n_chunks;
+		float* pcur = par ? pb1 : pb0;
+		float* pnxt = par ? pb0 : pb1;
+		h4 Gext[2];
+		if constexpr (EXT_DOUT) {
+#pragma unroll
+			for (int tau = 0; tau < 2; ++tau) Gext[tau] = *(const h4*)(a.dout + (size_t)(base + 16 * tau + c) * 16 + 4 * q);
+		}
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		if constexpr (EXT_DOUT) asm volatile("" : "+v"(Gext[0]), "+v"(Gext[1]));  // consume the loads before any DMA issue
+		// interpolation of the current slice from the DMA-delivered corners (bit-exact fp16 FMA
+		// chain, grid.h:144-163; weights recomputed from the slice's positions)
+		h4 xt[2][NTI];
+		{
+			float xc[2][2];
+			read_x(pcur, xc);
+#pragma unroll
+			for (int tau = 0; tau < 2; ++tau)
+#pragma unroll
+				for (int lv = 0; lv < NLV; ++lv) {
+					const int s = lv >> 2, pp = lv & 3;
+					const int level = 16 * s + 8 * (pp >> 1) + 2 * q + (pp & 1);
+					uint32_t idx[4];
+					_Float16 w16[4];
+					level_corners<2, H>(s_lvl[level], hash_grid, interp, xc[tau], idx, w16);
+					h2 e = {(_Float16)0.0f, (_Float16)0.0f};
+#pragma unroll
+					for (int cc = 0; cc < 4; ++cc)
+						e = pk_fma_f16(h2{w16[cc], w16[cc]}, __builtin_bit_cast(h2, gb[((tau * NLV + lv) * 4 + cc) * 64 + lane]), e);
+					xt[tau][2 * s + (pp >> 1)][2 * (pp & 1) + 0] = e[0];
+					xt[tau][2 * s + (pp >> 1)][2 * (pp & 1) + 1] = e[1];
+				}
+		}
+		// prefetch: next slice's corners, then the positions two slices ahead into this slot
+		// (targets: after the loss has read them)
+		if (nxt) {
+			float xn[2][2];
+			read_x(pnxt, xn);
+			lds_fence();
+			issue_gathers(xn);
+			if (chunk + 2 * stride < n_chunks) issue_pos(chunk + 2 * stride, par);
+		}
+		if constexpr (PROF) { t1 = stamp(); ph[0] += t1 - t0; t0 = t1; }
+		auto target = [&](int tau, uint32_t o) { return tb[(16 * tau + c) * dims + o]; };
+		auto after_loss = [&] {
+			if (nxt) {
+				lds_fence();
+				issue_tgt(chunk + stride);
+			}
+		};
+		fused_slice<W, IN, NH, ACT, EXT_DOUT, PROF>(a, base, c, q, xt, target, after_loss, Gext, s_main + L::oW0,
+		                                            s_main + L::oWh, s_main + L::oWo, bufA, bufD, acc, ph, t0);
+	}
+	if constexpr (PROF) t0 = stamp();
+	__syncthreads();
+	block_reduce_wgrad<W, IN, NH, WAVES>(acc, (float*)s_main, a, tid, wave, lane);
+	if constexpr (PROF) {
+		ph[7] = stamp() - t0;
+		if (lane == 0) {
+			unsigned long long* o = a.prof + (size_t)(blockIdx.x * WAVES + wave) * 8;
+			for (int k = 0; k < 8; ++k) o[k] = ph[k];
+		}
+	}
 }
 
 

@@ -331,7 +331,8 @@ void NetworkWithGridHost::fwd_bwd(hipStream_t st, StepWorkspace& ws, uint32_t B,
 	TCNN_CHECK(B % 32 == 0, "training: batch must be a multiple of 32");
 	const uint32_t n_mlp = mlp.n_params();
 	const uint32_t L = grid->desc.n_levels, F = grid->desc.n_features_per_level;
-	const uint32_t nb = fused_train_n_blocks(B);
+	const uint32_t nb = fused_train_n_blocks(mlp.width, mlp.n_input, mlp.n_hidden_layers, grid->desc.n_pos_dims, dims,
+	                                         dout16 != nullptr, B);
 	ws.n_fused_blocks = nb;
 	ws.dLdenc.reserve((size_t)L * F * B * 2);
 	ws.wgrad_partial.reserve((size_t)nb * n_mlp * 4);

@@ -60,6 +60,7 @@ _SIGS = {
     "tcnn_trainer_profile_begin": (c_int, [c_void_p]),
     "tcnn_trainer_profile_end": (c_int, [c_void_p, c_void_p, c_uint32, c_void_p]),
     "tcnn_debug_probe": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "tcnn_debug_fused_phase_cycles": (c_int, [c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_void_p]),
     "tcnn_debug_hfma": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint32]),
 }
 

@@ -1,0 +1,19 @@
+"""Diagnostic: wave-cycle split of the fused kernel's slice loop (s_memtime stamps build)."""
+import ctypes, os, sys
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "neuralbtf-tiny-cuda-nn_amd"), os.path.join(REPO, "tests")]
+import torch
+from helpers import CONFIG_HASH
+from tinycudann import Trainer, _lib as L
+B = 1 << 18
+t = Trainer(2, 3, CONFIG_HASH)
+pos = torch.rand(B, 2, device="cuda"); tgt = torch.rand(B, 3, device="cuda")
+out = (ctypes.c_uint64 * 8)()
+for _ in range(3):
+    L.check(L.lib().tcnn_debug_fused_phase_cycles(t.h, None, B, ctypes.c_void_p(pos.data_ptr()), ctypes.c_void_p(tgt.data_ptr()), out))
+tot = sum(out)
+nw = 256 * 8
+names = ["grid encode (gathers)", "hidden fwd", "out layer + loss", "bwd hidden + dW", "dW0 (first layer)", "dL/dx + store",
+         "prologue (per wave)", "epilogue reduce (per wave)"]
+for n, v in zip(names, out):
+    print(f"{n:28s} {v/tot*100:5.1f}%  {v/ (B/32):8.0f} cycles/slice  {v/nw:8.0f} cycles/wave")
