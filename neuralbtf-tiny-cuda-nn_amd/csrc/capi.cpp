@@ -122,8 +122,7 @@ struct ModuleGrid : ModuleBase {
 		TCNN_CHECK(!grid.stochastic, "stochastic_interpolation is not implemented by the MI355X engine yet");
 		if (!dL_dparams) return;
 		const uint32_t n_slices = (uint32_t)grid.slices.size();
-		uint32_t n_chunks = std::max(1u, 512u / n_slices);
-		n_chunks = std::min(n_chunks, std::max(1u, n / 4096));
+		const uint32_t n_chunks = grid.bwd_chunks(n);
 		partial.reserve((size_t)n_chunks * grid.n_params * 4);
 		grad32.reserve((size_t)grid.n_params * 4);
 		launch_grid_bwd(st, grid.desc.n_pos_dims, grid.desc.n_features_per_level, grid.desc.hash_type, n, in, grid.desc.n_pos_dims,
@@ -302,7 +301,7 @@ int tcnn_debug_fused_phase_cycles(tcnn_trainer* t, void* stream, uint32_t n, con
 		// run one normal step first so the workspace is sized
 		tr.training_step(st, n, input, target, false);
 		const uint32_t nb = fused_train_n_blocks(64, 32, 2, 2, tr.n_output_dims, false, n);
-		constexpr size_t WV = 8;  // waves per workgroup of the pipelined kernel
+		constexpr size_t WV = 4;  // waves per workgroup of the fused kernel
 		DevBuf prof;
 		prof.reserve((size_t)nb * WV * 8 * 8);
 		TCNN_HIP_CHECK(hipMemsetAsync(prof.p, 0, (size_t)nb * WV * 8 * 8, st));

@@ -7,11 +7,14 @@ namespace tcnn_amd {
 
 struct LevelInfo;
 
-// Workspace plan for the LDS-privatised grid backward: one work item per (level, entry slice).
+// Work plan of the LDS-privatised grid backward: one item per (level, entry range, feature range);
+// the item's int32 accumulators (end-begin) x nf fit in grid_bwd_slot_budget() LDS slots.
 struct GridSlice {
 	uint32_t level;
 	uint32_t begin;  // entry range within the level
 	uint32_t end;
+	uint32_t f0;     // feature range [f0, f0 + nf)
+	uint32_t nf;
 };
 
 struct AdamArgs {
@@ -52,7 +55,7 @@ void launch_grid_fwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_
 
 // Grid backward: dLdy layout 0 = level-major pairs ([l][i][F] halves), 1 = SoA ([(l*F+f)*B + i]),
 // 2 = AoS ([i*dy_stride + l*F + f]).
-uint32_t grid_bwd_slice_entries(uint32_t F);
+uint32_t grid_bwd_slot_budget();
 void launch_grid_bwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_t B, const float* pos,
                      uint32_t pos_stride, const void* dLdy16, int dy_layout, uint32_t dy_stride, const GridSlice* slices,
                      uint32_t n_slices, uint32_t n_chunks, float* partial, uint32_t partial_stride,

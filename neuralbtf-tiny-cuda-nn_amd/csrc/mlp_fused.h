@@ -99,24 +99,6 @@ __device__ __forceinline__ h8 lds_wtfrag16(const _Float16* M, int rs, int col0, 
 
 __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-// Byte address of an LDS object (for M0).
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-	return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-
-// LDS-DMA of one dword per lane: LDS[lds_byte + 4 * lane] = *(const uint32_t*)((const char*)base + voff).
-// Issued from inline asm on purpose: the compiler then inserts no vmcnt waits for it (its alias
-// tracking of LDS-DMA is conservative and would drain the prefetch at the first staging store);
-// the kernel waits with explicit s_waitcnt vmcnt(0) before reading the destination. lds_byte must
-// be wave-uniform. M0 is restored in the same statement (compiler-reserved register).
-__device__ __forceinline__ void glds_dword(const void* base, uint32_t voff, uint32_t lds_byte) {
-	uint32_t keep;
-	const uint32_t m0v = (uint32_t)__builtin_amdgcn_readfirstlane(lds_byte);
-	asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
-	             : "=&s"(keep)
-	             : "v"(voff), "s"(base), "s"(m0v)
-	             : "memory");
-}
 
 template <int W, int IN, int NH>
 struct FusedLayout {
@@ -145,21 +127,6 @@ struct RegKernelLayout {
 	static constexpr int BYTES_MAIN = LVL_BYTES + (int)MAX_LEVELS * 16;
 	static constexpr int BYTES_RED = (2 * L::N_MLP + 2 * WAVES) * 4;
 	static constexpr int BYTES = BYTES_MAIN > BYTES_RED ? BYTES_MAIN : BYTES_RED;
-};
-
-// Pipelined kernel (D = 2): 8 waves, one workgroup per CU, static LDS (see k_fused_train_pipe).
-template <int W, int IN, int NH>
-struct PipeLayout {
-	using L = FusedLayout<W, IN, NH>;
-	static constexpr int WAVES = 8;
-	static constexpr int NLV = 4 * L::KI;                // levels per lane per 16-sample tile
-	static constexpr int NG = 2 * NLV * 4;               // gather instructions per slice (2 tiles, 4 corners)
-	static constexpr int MAIN_HALVES_W = L::oStage + WAVES * 2 * L::STAGE;
-	static constexpr int MAIN_HALVES_R = 2 * (2 * L::N_MLP + 2 * WAVES);
-	static constexpr int MAIN_HALVES = MAIN_HALVES_W > MAIN_HALVES_R ? MAIN_HALVES_W : MAIN_HALVES_R;
-	static constexpr int TGT = 96;                       // targets of one slice, dims <= 3
-	static constexpr int BYTES = MAIN_HALVES * 2 + WAVES * (NG * 256 + 2 * 256 + TGT * 4) + (IN / 2) * 16;
-	static constexpr bool FITS = BYTES <= 163840;
 };
 
 // Fold the fp16 weights into the padded row-major LDS image.
@@ -561,161 +528,6 @@ __global__ __launch_bounds__(256, 2) void k_fused_train_grid(const FusedTrainArg
 	__syncthreads();
 	block_reduce_wgrad<W, IN, NH, 4>(acc, (float*)smem, a, tid, wave, lane);
 }
-
-// Pipelined variant for 2D grids: one workgroup of 8 waves per CU. The table gathers are the
-// kernel's bottleneck resource (the texture-address unit handles ~one lane per cycle for these
-// divergent 4-byte reads), so they are issued ONE SLICE AHEAD as LDS-DMA loads
-// (global_load_lds_dword: 64 lanes -> 256 contiguous LDS bytes, no VGPRs held) and land while the
-// wave runs the MLP of the current slice; positions and targets of the next slices ride along
-// the same way. Each wave's slice loop:
-//   wait vmcnt(0) -> read gathered corners / next positions / targets from LDS
-//   -> fp16 FMA interpolation of the current slice (weights recomputed from its positions)
-//   -> issue next slice's corner gathers + positions(+2) + targets(+1)  -> MLP of current slice.
-template <int W, int IN, int NH, HashType H, Act ACT, bool EXT_DOUT, bool PROF = false>
-__global__ __launch_bounds__(512, 1) void k_fused_train_pipe(const FusedTrainArgs a) {
-	using L = FusedLayout<W, IN, NH>;
-	using P = PipeLayout<W, IN, NH>;
-	constexpr int NTI = L::NTI, WAVES = P::WAVES, NLV = P::NLV, NG = P::NG;
-	constexpr int NLVL = IN / 2;
-	static_assert(P::FITS, "pipelined fused kernel: LDS budget");
-	__shared__ __attribute__((aligned(16))) _Float16 s_main[P::MAIN_HALVES];
-	__shared__ __attribute__((aligned(16))) uint32_t s_gath[WAVES][NG * 64];
-	__shared__ __attribute__((aligned(16))) float s_pos[WAVES][2][64];  // two slots: slice parity
-	__shared__ __attribute__((aligned(16))) float s_tgt[WAVES][P::TGT];
-	__shared__ LevelInfo s_lvl[NLVL];
-
-	const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-	const int c = lane & 15, q = lane >> 4;
-	unsigned long long t_kernel = 0;
-	if constexpr (PROF) t_kernel = stamp();
-	copy_image_to_lds(s_main, a.wimage, L::oStage, tid, WAVES * 64);
-	for (int l = tid; l < NLVL; l += WAVES * 64) s_lvl[l] = a.levels[l];
-	__syncthreads();
-
-	_Float16* bufA = s_main + L::oStage + wave * 2 * L::STAGE;
-	_Float16* bufD = bufA + L::STAGE;
-	uint32_t* gb = s_gath[wave];
-	float* pb0 = s_pos[wave][0];
-	float* pb1 = s_pos[wave][1];
-	float* tb = s_tgt[wave];
-	WgradAcc<W, IN, NH> acc;
-	acc.zero();
-	const bool hash_grid = a.hash_grid != 0;
-	const Interp interp = (Interp)a.interp;
-	const uint32_t n_chunks = a.B / 32;
-	const uint32_t stride = gridDim.x * WAVES;
-	const uint32_t dims = a.dims;
-
-	const uint32_t gb_lds = lds_addr(gb), tb_lds = lds_addr(tb), pb_lds = lds_addr(pb0);  // pb1 = pb0 + 256 B
-	auto issue_pos = [&](uint32_t ch, uint32_t slot) { glds_dword(a.pos, (ch * 64 + lane) * 4, pb_lds + 256 * slot); };
-	auto issue_tgt = [&](uint32_t ch) {
-		if constexpr (!EXT_DOUT) {
-			const uint32_t n = 32 * dims;  // <= 96
-			if ((uint32_t)lane < n) glds_dword(a.target, (ch * n + lane) * 4, tb_lds);
-			if ((uint32_t)lane + 64 < n) glds_dword(a.target, (ch * n + 64 + lane) * 4, tb_lds + 256);
-		}
-	};
-	auto issue_gathers = [&](const float (&x)[2][2]) {
-#pragma unroll
-		for (int tau = 0; tau < 2; ++tau)
-#pragma unroll
-			for (int lv = 0; lv < NLV; ++lv) {
-				const int s = lv >> 2, pp = lv & 3;
-				const int level = 16 * s + 8 * (pp >> 1) + 2 * q + (pp & 1);
-				uint32_t idx[4];
-				_Float16 w16[4];
-				level_corners<2, H>(s_lvl[level], hash_grid, interp, x[tau], idx, w16);
-#pragma unroll
-				for (int cc = 0; cc < 4; ++cc) glds_dword(a.table, idx[cc] * 4, gb_lds + ((tau * NLV + lv) * 4 + cc) * 256);
-			}
-	};
-
-	unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-	unsigned long long t0 = 0, t1 = 0;
-	uint32_t chunk = blockIdx.x * WAVES + wave;
-	auto read_x = [&](const float* slot, float (&x)[2][2]) {
-#pragma unroll
-		for (int tau = 0; tau < 2; ++tau) { x[tau][0] = slot[(16 * tau + c) * 2]; x[tau][1] = slot[(16 * tau + c) * 2 + 1]; }
-	};
-	if (chunk < n_chunks) {
-		issue_pos(chunk, 0);
-		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-		float x0[2][2];
-		read_x(pb0, x0);
-		lds_fence();
-		issue_gathers(x0);
-		if (chunk + stride < n_chunks) issue_pos(chunk + stride, 1);
-		issue_tgt(chunk);
-	}
-	if constexpr (PROF) { t0 = stamp(); ph[6] = t0 - t_kernel; }
-	uint32_t par = 0;  // slot holding this slice's positions
-	for (; chunk < n_chunks; chunk += stride, par ^= 1u) {
-		const uint32_t base = chunk * 32;
-		const bool nxt = chunk + stride < n_chunks;
-		float* pcur = par ? pb1 : pb0;
-		float* pnxt = par ? pb0 : pb1;
-		h4 Gext[2];
-		if constexpr (EXT_DOUT) {
-#pragma unroll
-			for (int tau = 0; tau < 2; ++tau) Gext[tau] = *(const h4*)(a.dout + (size_t)(base + 16 * tau + c) * 16 + 4 * q);
-		}
-		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-		if constexpr (EXT_DOUT) asm volatile("" : "+v"(Gext[0]), "+v"(Gext[1]));  // consume the loads before any DMA issue
-		// interpolation of the current slice from the DMA-delivered corners (bit-exact fp16 FMA
-		// chain, grid.h:144-163; weights recomputed from the slice's positions)
-		h4 xt[2][NTI];
-		{
-			float xc[2][2];
-			read_x(pcur, xc);
-#pragma unroll
-			for (int tau = 0; tau < 2; ++tau)
-#pragma unroll
-				for (int lv = 0; lv < NLV; ++lv) {
-					const int s = lv >> 2, pp = lv & 3;
-					const int level = 16 * s + 8 * (pp >> 1) + 2 * q + (pp & 1);
-					uint32_t idx[4];
-					_Float16 w16[4];
-					level_corners<2, H>(s_lvl[level], hash_grid, interp, xc[tau], idx, w16);
-					h2 e = {(_Float16)0.0f, (_Float16)0.0f};
-#pragma unroll
-					for (int cc = 0; cc < 4; ++cc)
-						e = pk_fma_f16(h2{w16[cc], w16[cc]}, __builtin_bit_cast(h2, gb[((tau * NLV + lv) * 4 + cc) * 64 + lane]), e);
-					xt[tau][2 * s + (pp >> 1)][2 * (pp & 1) + 0] = e[0];
-					xt[tau][2 * s + (pp >> 1)][2 * (pp & 1) + 1] = e[1];
-				}
-		}
-		// prefetch: next slice's corners, then the positions two slices ahead into this slot
-		// (targets: after the loss has read them)
-		if (nxt) {
-			float xn[2][2];
-			read_x(pnxt, xn);
-			lds_fence();
-			issue_gathers(xn);
-			if (chunk + 2 * stride < n_chunks) issue_pos(chunk + 2 * stride, par);
-		}
-		if constexpr (PROF) { t1 = stamp(); ph[0] += t1 - t0; t0 = t1; }
-		auto target = [&](int tau, uint32_t o) { return tb[(16 * tau + c) * dims + o]; };
-		auto after_loss = [&] {
-			if (nxt) {
-				lds_fence();
-				issue_tgt(chunk + stride);
-			}
-		};
-		fused_slice<W, IN, NH, ACT, EXT_DOUT, PROF>(a, base, c, q, xt, target, after_loss, Gext, s_main + L::oW0,
-		                                            s_main + L::oWh, s_main + L::oWo, bufA, bufD, acc, ph, t0);
-	}
-	if constexpr (PROF) t0 = stamp();
-	__syncthreads();
-	block_reduce_wgrad<W, IN, NH, WAVES>(acc, (float*)s_main, a, tid, wave, lane);
-	if constexpr (PROF) {
-		ph[7] = stamp() - t0;
-		if (lane == 0) {
-			unsigned long long* o = a.prof + (size_t)(blockIdx.x * WAVES + wave) * 8;
-			for (int k = 0; k < 8; ++k) o[k] = ph[k];
-		}
-	}
-}
-
 
 // Forward-only pass (inference / forward context): input fp16 from memory, SoA ([IN][B], the grid
 // encoding's layout) or AoS ([B][IN]); output fp16 [B][16] (the reference's CM [16 x B]).

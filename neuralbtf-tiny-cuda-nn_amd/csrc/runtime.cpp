@@ -177,10 +177,24 @@ GridEncodingHost::GridEncodingHost(uint32_t n_dims, const json& enc) {
 	}
 	n_params = offset * F;
 
-	// LDS-privatised backward plan: slices of at most grid_bwd_slice_entries(F) entries per level
-	const uint32_t SL = grid_bwd_slice_entries(F);
-	for (uint32_t l = 0; l < L; ++l)
-		for (uint32_t b = 0; b < levels[l].size; b += SL) slices.push_back(GridSlice{l, b, std::min(levels[l].size, b + SL)});
+	// LDS-privatised backward plan: a level whose F features fit the LDS budget is one item; else
+	// one item per feature group (as many features as fit), else entry slices of one feature.
+	// Items with all features (2 atomics per corner for F = 2) go first: they are the heaviest.
+	const uint32_t S = grid_bwd_slot_budget();
+	std::vector<GridSlice> single;
+	for (uint32_t l = 0; l < L; ++l) {
+		const uint32_t size = levels[l].size;
+		if ((uint64_t)size * F <= S) {
+			slices.push_back(GridSlice{l, 0, size, 0, F});
+			continue;
+		}
+		uint32_t nf = F;
+		while (nf > 1 && ((uint64_t)size * nf > S || F % nf)) --nf;
+		const uint32_t SL = size <= S / nf ? size : S / nf;
+		for (uint32_t f = 0; f < F; f += nf)
+			for (uint32_t b = 0; b < size; b += SL) single.push_back(GridSlice{l, b, std::min(size, b + SL), f, nf});
+	}
+	slices.insert(slices.end(), single.begin(), single.end());
 
 	d_levels.reserve(levels.size() * sizeof(LevelInfo));
 	TCNN_HIP_CHECK(hipMemcpy(d_levels.p, levels.data(), levels.size() * sizeof(LevelInfo), hipMemcpyHostToDevice));
@@ -338,8 +352,7 @@ void NetworkWithGridHost::fwd_bwd(hipStream_t st, StepWorkspace& ws, uint32_t B,
 	ws.wgrad_partial.reserve((size_t)nb * n_mlp * 4);
 	ws.loss_partial.reserve((size_t)nb * 4);
 	const uint32_t n_slices = (uint32_t)grid->slices.size();
-	uint32_t n_chunks = std::max(1u, 512u / n_slices);
-	n_chunks = std::min(n_chunks, std::max(1u, B / 4096));
+	const uint32_t n_chunks = grid->bwd_chunks(B);
 	ws.n_grid_chunks = n_chunks;
 	ws.grid_partial.reserve((size_t)n_chunks * grid->n_params * 4);
 

@@ -64,6 +64,11 @@ struct GridEncodingHost {
 	void initialize_params(Pcg32& rng, float* host_out, float scale = 1.0f) const;
 	json hyperparams() const;
 	const LevelInfo* dev_levels() const { return d_levels.as<LevelInfo>(); }
+	// point chunks of the backward: ~one 1024-thread workgroup per CU in total, >= 4096 points each
+	uint32_t bwd_chunks(uint32_t B) const {
+		uint32_t c = std::max(1u, (256u + (uint32_t)slices.size() / 2) / (uint32_t)slices.size());
+		return std::max(1u, std::min(c, B / 4096));
+	}
 };
 
 // ---- fully fused MLP shape (reference networks/fully_fused_mlp.h) ----
