@@ -64,7 +64,7 @@ void check_batch(uint32_t n) {
 }
 
 struct ModuleNWIE : ModuleBase {
-	NetworkWithGridHost model;
+	NetworkHost model;
 	StepWorkspace ws;
 	DevBuf grad32;
 	ModuleNWIE(uint32_t n_in, uint32_t n_out, const json& enc, const json& net) : model(n_in, n_out, enc, net) {}
@@ -73,19 +73,19 @@ struct ModuleNWIE : ModuleBase {
 		model.inference(st, ws, n, in, params, out);
 	}
 	void forward(hipStream_t st, uint32_t n, const float* in, void* out, const void* params, bool prep) override {
-		TCNN_CHECK(!prep, "prepare_input_gradients (dL/dinput through the grid) is not implemented by the MI355X engine yet");
+		TCNN_CHECK(!prep || !model.grid, "prepare_input_gradients (dL/dinput through the grid) is not implemented by the MI355X engine yet");
 		check_batch(n);
 		// The backward recomputes activations from the input, so the context carries nothing.
 		model.inference(st, ws, n, in, params, out);
 	}
 	void backward(hipStream_t st, uint32_t n, float* dL_din, const void* dL_dout, void* dL_dparams, const float* in,
 	              const void*, const void* params) override {
-		TCNN_CHECK(dL_din == nullptr, "dL/dinput through the grid is not implemented by the MI355X engine yet");
+		TCNN_CHECK(dL_din == nullptr || !model.grid, "dL/dinput through the grid is not implemented by the MI355X engine yet");
 		check_batch(n);
-		if (!dL_dparams) return;
+		if (!dL_dparams && !dL_din) return;
 		grad32.reserve(n_params() * 4);
-		model.fwd_bwd(st, ws, n, in, nullptr, model.n_output_dims, 1.0f, params, dL_dout, nullptr, grad32.as<float>());
-		launch_cast_f32_f16(st, grad32.as<float>(), dL_dparams, n_params());
+		model.fwd_bwd(st, ws, n, in, nullptr, model.n_output_dims, 1.0f, params, dL_dout, nullptr, grad32.as<float>(), nullptr, dL_din);
+		if (dL_dparams) launch_cast_f32_f16(st, grad32.as<float>(), dL_dparams, n_params());
 	}
 	uint32_t n_input_dims() const override { return model.n_input_dims; }
 	uint32_t n_output_dims() const override { return model.mlp.padded_output; }
@@ -98,6 +98,30 @@ struct ModuleNWIE : ModuleBase {
 	}
 	json hyperparams() const override { return model.hyperparams(); }
 	std::string name() const override { return "NetworkWithInputEncoding"; }
+};
+
+// Parameter-free encodings (OneBlob, Identity) as a module (cpp_api.cu:145-149).
+struct ModuleEncoding : ModuleBase {
+	EncodingHost enc;
+	ModuleEncoding(uint32_t n_in, const json& j) : enc(n_in, j) {}
+	void inference(hipStream_t st, uint32_t n, const float* in, void* out, const void* params) override {
+		check_batch(n);
+		enc.forward_aos(st, n, in, params, out);
+	}
+	void forward(hipStream_t st, uint32_t n, const float* in, void* out, const void* params, bool) override {
+		inference(st, n, in, out, params);
+	}
+	void backward(hipStream_t st, uint32_t n, float* dL_din, const void* dL_dout, void*, const float* in, const void*,
+	              const void*) override {
+		check_batch(n);
+		if (dL_din) enc.backward_input(st, n, in, dL_dout, dL_din);
+	}
+	uint32_t n_input_dims() const override { return enc.n_dims; }
+	uint32_t n_output_dims() const override { return enc.padded_output_width(); }
+	uint64_t n_params() const override { return 0; }
+	void initialize_params(uint64_t, float*, float) override {}
+	json hyperparams() const override { return enc.hyperparams(); }
+	std::string name() const override { return enc.kind == EncKind::OneBlob ? "OneBlobEncoding" : "IdentityEncoding"; }
 };
 
 struct ModuleGrid : ModuleBase {
@@ -181,10 +205,13 @@ tcnn_module* tcnn_create_network_with_input_encoding(uint32_t n_in, uint32_t n_o
 	});
 }
 
+// create_network = Identity encoding + network (cpp_api.cu:151-153)
 tcnn_module* tcnn_create_network(uint32_t n_in, uint32_t n_out, const char* net) {
-	(void)n_in; (void)n_out; (void)net;
-	g_last_error = "create_network (Identity encoding + MLP) is not implemented by the MI355X engine yet";
-	return nullptr;
+	return guard_ptr<tcnn_module>([&] {
+		auto* r = new tcnn_module;
+		r->m = std::make_unique<ModuleNWIE>(n_in, n_out, json{{"otype", "Identity"}}, parse_json(net));
+		return r;
+	});
 }
 
 tcnn_module* tcnn_create_encoding(uint32_t n_in, const char* enc, int precision) {
@@ -192,10 +219,10 @@ tcnn_module* tcnn_create_encoding(uint32_t n_in, const char* enc, int precision)
 		TCNN_CHECK(precision == TCNN_PRECISION_FP16, "create_encoding: only Fp16 precision is implemented by the MI355X engine");
 		json j = parse_json(enc);
 		const std::string ot = j.is_object() && j.find("otype") != j.end() ? j["otype"].get<std::string>() : "OneBlob";
-		TCNN_CHECK(ieq(ot, "HashGrid") || ieq(ot, "Grid") || ieq(ot, "TiledGrid") || ieq(ot, "DenseGrid"),
-		           "Encoding '" + ot + "' is not implemented by the MI355X engine yet");
+		TCNN_CHECK(EncodingHost::known(ot), "Encoding '" + ot + "' is not implemented by the MI355X engine yet");
 		auto* r = new tcnn_module;
-		r->m = std::make_unique<ModuleGrid>(n_in, j);
+		if (ieq(ot, "OneBlob") || ieq(ot, "Identity")) r->m = std::make_unique<ModuleEncoding>(n_in, j);
+		else r->m = std::make_unique<ModuleGrid>(n_in, j);
 		return r;
 	});
 }
@@ -278,7 +305,7 @@ int tcnn_trainer_set_params_full_precision(tcnn_trainer* t, const float* host, u
 	return guard([&] { t->t->set_params_full_precision(host, n); });
 }
 uint32_t tcnn_trainer_optimizer_step_count(const tcnn_trainer* t) { return t->t->adam_step; }
-const char* tcnn_trainer_engine(const tcnn_trainer* t) { return t->t->model->fused_ok() ? "fused" : "unsupported"; }
+const char* tcnn_trainer_engine(const tcnn_trainer* t) { return t->t->model->engine(); }
 
 int tcnn_trainer_profile_begin(tcnn_trainer* t) {
 	return guard([&] {

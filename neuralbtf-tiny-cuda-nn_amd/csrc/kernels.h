@@ -17,6 +17,12 @@ struct GridSlice {
 	uint32_t nf;
 };
 
+// Runtime activation codes of the layer-wise engine (reference Activation, common.h:126-136).
+enum : int {
+	ACT_NONE = 0, ACT_RELU = 1, ACT_LEAKY_RELU = 2, ACT_EXPONENTIAL = 3, ACT_SINE = 4, ACT_SIGMOID = 5,
+	ACT_SQUAREPLUS = 6, ACT_SOFTPLUS = 7, ACT_TANH = 8,
+};
+
 struct AdamArgs {
 	uint32_t n, n_matrix;
 	float loss_scale, grad_scale;  // grad_scale multiplies the fp32 gradient before fp16 rounding (1/N for N-rank sums)
@@ -76,6 +82,34 @@ void launch_relative_l2(hipStream_t st, uint32_t B, uint32_t stride, uint32_t di
                         const void* pred16, const float* target, float* values, void* grads16);
 
 void launch_sum(hipStream_t st, const float* in, uint32_t n, float* out);
+
+// ---- layer-wise MFMA MLP (mlp_layers.hip); activations sample-major fp16 [B][width] ----
+bool layered_width_supported(uint32_t w);
+// y[B][N] = act(x[B][K] w^T), w row-major [N][K]
+void launch_layer_fwd(hipStream_t st, uint32_t B, uint32_t N, uint32_t K, const void* w16, const void* x16, void* y16, int act);
+// dx[B][K] = act'(h) * (dy[B][N] w); h == nullptr: no transfer
+void launch_layer_bwd(hipStream_t st, uint32_t B, uint32_t N, uint32_t K, const void* w16, const void* dy16, const void* h16,
+                      void* dx16, int act);
+// in-place output-activation transfer: g[i] = act'(y[i]) g[i] over n elements
+void launch_act_bwd_inplace(hipStream_t st, uint32_t n, int act, const void* y16, void* g16);
+// partial[chunk][N][K] = sum over the chunk's samples of dy[i][n] x[i][k]
+uint32_t wgrad_n_chunks(uint32_t B);
+void launch_wgrad(hipStream_t st, uint32_t B, uint32_t N, uint32_t K, const void* dy16, const void* x16, float* partial,
+                  uint32_t n_chunks);
+uint32_t relative_l2_n_blocks(uint32_t B, uint32_t stride);
+void launch_relative_l2_partial(hipStream_t st, uint32_t B, uint32_t stride, uint32_t dims, float loss_scale, const void* pred16,
+                                const float* target, void* grads16, float* loss_partial);
+
+// ---- OneBlob / Identity encodings (encodings.hip); output AoS fp16 [B][out_stride], padding = 1 ----
+void launch_oneblob_fwd(hipStream_t st, uint32_t B, uint32_t D, uint32_t n_bins, const float* x, uint32_t x_stride, void* out16,
+                        uint32_t out_stride, uint32_t n_pad);
+// dL/dx fp32 [B][x_stride] from dL/dy fp16 AoS (kernel_one_blob_backward, oneblob.h:116-147)
+void launch_oneblob_bwd(hipStream_t st, uint32_t B, uint32_t D, uint32_t n_bins, const float* x, uint32_t x_stride,
+                        const void* dy16, uint32_t dy_stride, float* dx, uint32_t dx_stride);
+void launch_identity_fwd(hipStream_t st, uint32_t B, uint32_t D, float scale, float offset, const float* x, uint32_t x_stride,
+                         void* out16, uint32_t out_stride, uint32_t n_pad);
+void launch_identity_bwd(hipStream_t st, uint32_t B, uint32_t D, float scale, const void* dy16, uint32_t dy_stride, float* dx,
+                         uint32_t dx_stride);
 
 void launch_probe_hfma(hipStream_t st, const void* a, const void* b, const void* c, void* out, uint32_t n_pairs);
 // Diagnostic: the config_hash fused (pipelined) kernel with s_memtime phase stamps (prof: [blocks*8][8] u64).

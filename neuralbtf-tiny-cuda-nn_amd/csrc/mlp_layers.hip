@@ -1,0 +1,349 @@
+// mlp_layers.hip -- layer-wise MFMA MLP engine for gfx950: widths 16, 32, 64, 128, any
+// depth, any input width multiple of 16 up to 128, every activation of the reference.
+//
+// Used for the shapes the register-resident fused kernel (mlp_fused.h) does not cover: W = 128 (the
+// LDS-pressure configs: OneBlob W128/H5 = 168 KB of fp16 weights does not fit 160 KB of LDS at all),
+// non-grid encodings (OneBlob, Identity), CutlassMLP / "MLP" otypes, output activations.
+// Reference: FullyFusedMLP forward/backward (fully_fused_mlp.cu:47-557, 735-836) and CutlassMLP
+// (cutlass_mlp.cu:38-371) -- same dataflow as the reference (per-layer fp16 activations in HBM,
+// split-K weight-gradient GEMMs), with fp32 MFMA accumulation instead of fp16 accumulators.
+//
+// Layouts: activations are sample-major AoS [B][width] fp16 (the reference's CM matrices);
+// weights row-major [n_out][n_in] fp16 inside the parameter buffer.
+//
+//   k_layer_fwd<NT, KS>  Y = act(X W^T)               out tiles NT x 16, contraction K <= 32 KS
+//   k_layer_bwd<NT, KS>  dX = act'(H) . (dY W)        out tiles NT x 16 over K, contraction N <= 32 KS
+//   k_wgrad<MT, KT>      dW partial = dY^T X over a sample chunk (samples on the MFMA K axis,
+//                        staged through LDS and read back with ds_read_b64_tr_b16)
+//   k_relative_l2_partial RelativeL2 with per-workgroup loss partial sums
+#include "kernels.h"
+
+#include "mlp_fused.h"
+
+namespace tcnn_amd {
+
+// ---- activations (reference common_device.h:102-297), fp32 math on fp16-stored values ----
+__device__ __forceinline__ float logistic_f(float x) { return 1.0f / (1.0f + expf(-x)); }
+constexpr float K_ACT = 10.0f;
+
+__device__ __forceinline__ float act_fwd_rt(int a, float x) {
+	switch (a) {
+		case ACT_RELU: return x > 0.0f ? x : 0.0f;
+		case ACT_LEAKY_RELU: return x * (x > 0.0f ? 1.0f : 0.01f);
+		case ACT_EXPONENTIAL: return expf(x);
+		case ACT_SINE: return sinf(x);
+		case ACT_SIGMOID: return logistic_f(x);
+		case ACT_SQUAREPLUS: {
+			const float y = x * K_ACT;
+			return 0.5f * (y + sqrtf(y * y + 4.0f)) / K_ACT;
+		}
+		case ACT_SOFTPLUS: return logf(expf(x * K_ACT) + 1.0f) / K_ACT;
+		case ACT_TANH: return tanhf(x);
+		default: return x;
+	}
+}
+
+// Transfer given the post-activation value y (warp_activation_backward, common_device.h:240-297):
+// the factor is rounded to fp16 like the reference's (T)(...) before the fp16 product.
+__device__ __forceinline__ float act_bwd_rt(int a, float g, float y) {
+	float f;
+	switch (a) {
+		case ACT_RELU: return y > 0.0f ? g : 0.0f;
+		case ACT_LEAKY_RELU: f = y > 0.0f ? 1.0f : 0.01f; break;
+		case ACT_EXPONENTIAL: f = y; break;
+		case ACT_SIGMOID: f = y * (float)(_Float16)(1.0f - y); break;
+		case ACT_SQUAREPLUS: {
+			const float t = y * K_ACT;
+			f = t * t / (t * t + 1.0f);
+			break;
+		}
+		case ACT_SOFTPLUS: f = 1.0f - expf(-y * K_ACT); break;
+		case ACT_TANH: f = 1.0f - y * y; break;
+		default: return g;
+	}
+	return (float)(_Float16)g * (float)(_Float16)f;
+}
+
+// Stage a row-major [rows][cols] fp16 matrix into LDS with row stride rs, zero-filling columns
+// [cols, zc) (transpose = false), or its transpose [cols][rows] with columns [rows, zc) zeroed.
+template <bool TRANSPOSE>
+__device__ __forceinline__ void stage_matrix(_Float16* s, const _Float16* __restrict__ m, uint32_t rows, uint32_t cols,
+                                             uint32_t rs, uint32_t zc, int tid, int nthr) {
+	if (!TRANSPOSE) {
+		for (uint32_t idx = tid; idx < rows * zc; idx += nthr) {
+			const uint32_t r = idx / zc, cc = idx % zc;
+			s[r * rs + cc] = cc < cols ? m[r * cols + cc] : (_Float16)0.0f;
+		}
+	} else {
+		for (uint32_t idx = tid; idx < cols * zc; idx += nthr) {
+			const uint32_t r = idx / zc, cc = idx % zc;  // s[r][cc] = m[cc][r]
+			s[r * rs + cc] = cc < rows ? m[cc * cols + r] : (_Float16)0.0f;
+		}
+	}
+}
+
+// One 32-sample slice of  Out[i][16t + 4q + r] = epi( sum_k Amat[16t + c'][k] In[i][k] )  in the
+// transposed MFMA form: A = LDS matrix rows (output features), B = In rows loaded from HBM with
+// 16-byte loads (lane (c, q) of tile tau: sample base + 16 tau + c, k = 32 s + 8 q .. +7).
+template <int NT, int KS, class Epi>
+__device__ __forceinline__ void layer_slice(const _Float16* sA, int rs, const _Float16* __restrict__ in, uint32_t in_stride,
+                                            uint32_t K, uint32_t base, int c, int q, Epi epi) {
+	const f4 fz = {0.0f, 0.0f, 0.0f, 0.0f};
+	h8 xb[2][KS];
+#pragma unroll
+	for (int tau = 0; tau < 2; ++tau) {
+		const _Float16* row = in + (size_t)(base + 16 * tau + c) * in_stride;
+#pragma unroll
+		for (int s = 0; s < KS; ++s) {
+			const uint32_t k0 = 32 * s + 8 * q;
+			if (k0 < K) xb[tau][s] = *(const h8*)(row + k0);
+			else xb[tau][s] = h8{0, 0, 0, 0, 0, 0, 0, 0};
+		}
+	}
+#pragma unroll
+	for (int t = 0; t < NT; ++t) {
+		f4 a0 = fz, a1 = fz;
+#pragma unroll
+		for (int s = 0; s < KS; ++s) {
+			const h8 af = *(const h8*)(sA + (16 * t + c) * rs + 32 * s + 8 * q);
+			a0 = mfma16(af, xb[0][s], a0);
+			a1 = mfma16(af, xb[1][s], a1);
+		}
+		epi(0, t, a0);
+		epi(1, t, a1);
+	}
+}
+
+template <int NT, int KS>
+__global__ __launch_bounds__(256) void k_layer_fwd(uint32_t B, uint32_t K, const _Float16* __restrict__ w,
+                                                    const _Float16* __restrict__ x, _Float16* __restrict__ y, int act) {
+	constexpr int N = 16 * NT, RS = 32 * KS + 8;
+	__shared__ __attribute__((aligned(16))) _Float16 sW[N * RS];
+	const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+	const int c = lane & 15, q = lane >> 4;
+	stage_matrix<false>(sW, w, N, K, RS, 32 * KS, tid, 256);
+	__syncthreads();
+	const uint32_t n_slices = B / 32;
+	for (uint32_t sl = blockIdx.x * 4 + wave; sl < n_slices; sl += gridDim.x * 4) {
+		const uint32_t base = sl * 32;
+		layer_slice<NT, KS>(sW, RS, x, K, K, base, c, q, [&](int tau, int t, f4 v) {
+			h4 o;
+#pragma unroll
+			for (int r = 0; r < 4; ++r) o[r] = (_Float16)act_fwd_rt(act, v[r]);
+			*(h4*)(y + (size_t)(base + 16 * tau + c) * N + 16 * t + 4 * q) = o;
+		});
+	}
+}
+
+// dX[i][k] = act'(H[i][k]) * sum_n dY[i][n] W[n][k]; H == nullptr -> no transfer. K = 16 NT.
+template <int NT, int KS>
+__global__ __launch_bounds__(256) void k_layer_bwd(uint32_t B, uint32_t N, const _Float16* __restrict__ w,
+                                                    const _Float16* __restrict__ dy, const _Float16* __restrict__ h,
+                                                    _Float16* __restrict__ dx, int act) {
+	constexpr int K = 16 * NT, RS = 32 * KS + 8;
+	__shared__ __attribute__((aligned(16))) _Float16 sWT[K * RS];
+	const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+	const int c = lane & 15, q = lane >> 4;
+	stage_matrix<true>(sWT, w, N, K, RS, 32 * KS, tid, 256);
+	__syncthreads();
+	const uint32_t n_slices = B / 32;
+	for (uint32_t sl = blockIdx.x * 4 + wave; sl < n_slices; sl += gridDim.x * 4) {
+		const uint32_t base = sl * 32;
+		layer_slice<NT, KS>(sWT, RS, dy, N, N, base, c, q, [&](int tau, int t, f4 v) {
+			const size_t o = (size_t)(base + 16 * tau + c) * K + 16 * t + 4 * q;
+			h4 r4;
+			if (h) {
+				const h4 hv = *(const h4*)(h + o);
+#pragma unroll
+				for (int r = 0; r < 4; ++r) r4[r] = (_Float16)act_bwd_rt(act, v[r], (float)hv[r]);
+			} else {
+#pragma unroll
+				for (int r = 0; r < 4; ++r) r4[r] = (_Float16)v[r];
+			}
+			*(h4*)(dx + o) = r4;
+		});
+	}
+}
+
+// Weight-gradient partial of one sample chunk: P[n][k] = sum_{i in chunk} dY[i][n] X[i][k].
+// The workgroup stages 32 samples of dY and X in LDS; wave w owns output tiles w, w+4, ...
+// (MT x KT tiles of 16x16), fp32 accumulators in registers for the whole chunk.
+template <int MT, int KT>
+__global__ __launch_bounds__(256) void k_wgrad(uint32_t B, uint32_t pts_per_chunk, const _Float16* __restrict__ dy,
+                                                const _Float16* __restrict__ x, float* __restrict__ partial) {
+	constexpr int N = 16 * MT, K = 16 * KT, RSD = N + 8, RSX = K + 8;
+	constexpr int TILES = MT * KT, TPW = (TILES + 3) / 4;
+	__shared__ __attribute__((aligned(16))) _Float16 sD[2][32 * RSD];
+	__shared__ __attribute__((aligned(16))) _Float16 sX[2][32 * RSX];
+	const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+	const int c = lane & 15, q = lane >> 4;
+	const f4 fz = {0.0f, 0.0f, 0.0f, 0.0f};
+	f4 acc[TPW];
+#pragma unroll
+	for (int m = 0; m < TPW; ++m) acc[m] = fz;
+	const uint32_t i0 = blockIdx.x * pts_per_chunk;
+	const uint32_t i1 = min(B, i0 + pts_per_chunk);
+	auto stage = [&](int buf, uint32_t b0) {
+		for (int idx = tid; idx < 32 * N / 8; idx += 256) {
+			const int r = idx / (N / 8), c8 = idx % (N / 8);
+			*(uint4*)(&sD[buf][r * RSD + 8 * c8]) = *(const uint4*)(dy + (size_t)(b0 + r) * N + 8 * c8);
+		}
+		for (int idx = tid; idx < 32 * K / 8; idx += 256) {
+			const int r = idx / (K / 8), c8 = idx % (K / 8);
+			*(uint4*)(&sX[buf][r * RSX + 8 * c8]) = *(const uint4*)(x + (size_t)(b0 + r) * K + 8 * c8);
+		}
+	};
+	int buf = 0;
+	if (i0 < i1) stage(0, i0);
+	__syncthreads();
+	for (uint32_t b0 = i0; b0 < i1; b0 += 32) {
+		if (b0 + 32 < i1) stage(buf ^ 1, b0 + 32);  // next slice lands while this one is consumed
+#pragma unroll
+		for (int m = 0; m < TPW; ++m) {
+			const int j = wave + 4 * m;
+			if (j < TILES) {
+				const int mt = j / KT, kt = j % KT;
+				acc[m] = mfma16(lds_trfrag(sD[buf], RSD, q, c, mt), lds_trfrag(sX[buf], RSX, q, c, kt), acc[m]);
+			}
+		}
+		__syncthreads();
+		buf ^= 1;
+	}
+	float* dst = partial + (size_t)blockIdx.x * N * K;
+#pragma unroll
+	for (int m = 0; m < TPW; ++m) {
+		const int j = wave + 4 * m;
+		if (j < TILES) {
+			const int mt = j / KT, kt = j % KT;
+#pragma unroll
+			for (int r = 0; r < 4; ++r) dst[(16 * mt + 4 * q + r) * K + 16 * kt + c] = acc[m][r];
+		}
+	}
+}
+
+// ---- launchers ----
+static uint32_t pow2_ceil_steps(uint32_t k) {  // 32-wide K steps, rounded up to 1, 2, 4 (K <= 128)
+	const uint32_t s = div_round_up(k, 32);
+	return s <= 1 ? 1 : s <= 2 ? 2 : s <= 4 ? 4 : 0;
+}
+
+static uint32_t layer_blocks(uint32_t B) { return std::max(1u, std::min(div_round_up(B / 32, 4), 1024u)); }
+
+bool layered_width_supported(uint32_t w) { return w == 16 || w == 32 || w == 64 || w == 128; }
+
+#define TCNN_LAYER_DISPATCH(NTV, KSV, CALL)                                                              \
+	switch (NTV) {                                                                                       \
+		case 1: switch (KSV) { case 1: CALL(1, 1); break; case 2: CALL(1, 2); break; case 4: CALL(1, 4); break; default: ok = false; } break; \
+		case 2: switch (KSV) { case 1: CALL(2, 1); break; case 2: CALL(2, 2); break; case 4: CALL(2, 4); break; default: ok = false; } break; \
+		case 4: switch (KSV) { case 1: CALL(4, 1); break; case 2: CALL(4, 2); break; case 4: CALL(4, 4); break; default: ok = false; } break; \
+		case 8: switch (KSV) { case 1: CALL(8, 1); break; case 2: CALL(8, 2); break; case 4: CALL(8, 4); break; default: ok = false; } break; \
+		default: ok = false;                                                                             \
+	}
+
+void launch_layer_fwd(hipStream_t st, uint32_t B, uint32_t N, uint32_t K, const void* w16, const void* x16, void* y16, int act) {
+	TCNN_CHECK(B % 32 == 0 && N % 16 == 0 && K % 16 == 0, "layer_fwd: B % 32, N % 16, K % 16 must be 0");
+	if (B == 0) return;
+	bool ok = true;
+	const dim3 g(layer_blocks(B));
+#define CALL(nt, ks) hipLaunchKernelGGL((k_layer_fwd<nt, ks>), g, dim3(256), 0, st, B, K, (const _Float16*)w16, (const _Float16*)x16, (_Float16*)y16, act)
+	TCNN_LAYER_DISPATCH(N / 16, pow2_ceil_steps(K), CALL)
+#undef CALL
+	TCNN_CHECK(ok, "layer_fwd: unsupported shape N=" + std::to_string(N) + " K=" + std::to_string(K));
+	TCNN_HIP_CHECK(hipGetLastError());
+}
+
+void launch_layer_bwd(hipStream_t st, uint32_t B, uint32_t N, uint32_t K, const void* w16, const void* dy16, const void* h16,
+                      void* dx16, int act) {
+	TCNN_CHECK(B % 32 == 0 && N % 16 == 0 && K % 16 == 0, "layer_bwd: B % 32, N % 16, K % 16 must be 0");
+	if (B == 0) return;
+	bool ok = true;
+	const dim3 g(layer_blocks(B));
+#define CALL(nt, ks) hipLaunchKernelGGL((k_layer_bwd<nt, ks>), g, dim3(256), 0, st, B, N, (const _Float16*)w16, (const _Float16*)dy16, (const _Float16*)h16, (_Float16*)dx16, act)
+	TCNN_LAYER_DISPATCH(K / 16, pow2_ceil_steps(N), CALL)
+#undef CALL
+	TCNN_CHECK(ok, "layer_bwd: unsupported shape N=" + std::to_string(N) + " K=" + std::to_string(K));
+	TCNN_HIP_CHECK(hipGetLastError());
+}
+
+uint32_t wgrad_n_chunks(uint32_t B) { return std::max(1u, std::min(B / 1024u, 256u)); }
+
+void launch_wgrad(hipStream_t st, uint32_t B, uint32_t N, uint32_t K, const void* dy16, const void* x16, float* partial,
+                  uint32_t n_chunks) {
+	TCNN_CHECK(B % 32 == 0 && N % 16 == 0 && K % 16 == 0, "wgrad: B % 32, N % 16, K % 16 must be 0");
+	if (B == 0) return;
+	const uint32_t ppc = div_round_up(div_round_up(B, n_chunks), 32) * 32;
+	const uint32_t nc = div_round_up(B, ppc);
+	TCNN_CHECK(nc <= n_chunks, "wgrad: chunk plan");
+	if (nc < n_chunks) TCNN_HIP_CHECK(hipMemsetAsync(partial + (size_t)nc * N * K, 0, (size_t)(n_chunks - nc) * N * K * 4, st));
+	bool ok = true;
+	const dim3 g(nc);
+	// MT = N / 16 (output tiles), KT = K / 16 (input tiles): both from {1, 2, 4, 8, 16}
+#define WG(mt, kt) hipLaunchKernelGGL((k_wgrad<mt, kt>), g, dim3(256), 0, st, B, ppc, (const _Float16*)dy16, (const _Float16*)x16, partial)
+#define WGK(mt)                                                                          \
+	switch (K / 16) {                                                                    \
+		case 1: WG(mt, 1); break; case 2: WG(mt, 2); break; case 4: WG(mt, 4); break;    \
+		case 8: WG(mt, 8); break; default: ok = false;       \
+	}
+	switch (N / 16) {
+		case 1: WGK(1); break;
+		case 2: WGK(2); break;
+		case 4: WGK(4); break;
+		case 8: WGK(8); break;
+		default: ok = false;
+	}
+#undef WGK
+#undef WG
+	TCNN_CHECK(ok, "wgrad: unsupported shape N=" + std::to_string(N) + " K=" + std::to_string(K));
+	TCNN_HIP_CHECK(hipGetLastError());
+}
+
+// RelativeL2 (losses/relative_l2.h:40-76) over pred fp16 [B][stride]; per-workgroup loss sums.
+__global__ __launch_bounds__(256) void k_relative_l2_partial(uint32_t n_elements, uint32_t stride, uint32_t dims, float loss_scale,
+                                                              float n_total, const _Float16* __restrict__ pred,
+                                                              const float* __restrict__ target, _Float16* __restrict__ grads,
+                                                              float* __restrict__ loss_partial) {
+	__shared__ float part[4];
+	float s = 0.0f;
+	for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n_elements; i += gridDim.x * 256) {
+		const uint32_t intra = i % stride, inter = i / stride;
+		if (intra >= dims) {
+			grads[i] = (_Float16)0.0f;
+			continue;
+		}
+		const float p = (float)pred[i];
+		const float pse = __builtin_fmaf(p, p, 0.01f);
+		const float d = p - target[inter * dims + intra];
+		s += d * d / pse / n_total;
+		const float gr = 2.0f * d / pse;
+		grads[i] = (_Float16)(loss_scale * gr / n_total);
+	}
+#pragma unroll
+	for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+	if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+	__syncthreads();
+	if (threadIdx.x == 0) loss_partial[blockIdx.x] = (part[0] + part[1]) + (part[2] + part[3]);
+}
+
+uint32_t relative_l2_n_blocks(uint32_t B, uint32_t stride) { return std::max(1u, std::min(div_round_up((uint64_t)B * stride, 256), 1024u)); }
+
+void launch_relative_l2_partial(hipStream_t st, uint32_t B, uint32_t stride, uint32_t dims, float loss_scale, const void* pred16,
+                                const float* target, void* grads16, float* loss_partial) {
+	const uint32_t n = B * stride;
+	if (!n) return;
+	hipLaunchKernelGGL(k_relative_l2_partial, dim3(relative_l2_n_blocks(B, stride)), dim3(256), 0, st, n, stride, dims, loss_scale,
+	                   (float)((uint64_t)B * dims), (const _Float16*)pred16, target, (_Float16*)grads16, loss_partial);
+	TCNN_HIP_CHECK(hipGetLastError());
+}
+
+__global__ __launch_bounds__(256) void k_act_bwd_inplace(uint32_t n, int act, const _Float16* __restrict__ y, _Float16* __restrict__ g) {
+	const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+	if (i < n) g[i] = (_Float16)act_bwd_rt(act, (float)g[i], (float)y[i]);
+}
+
+void launch_act_bwd_inplace(hipStream_t st, uint32_t n, int act, const void* y16, void* g16) {
+	if (!n || act == ACT_NONE) return;
+	hipLaunchKernelGGL(k_act_bwd_inplace, dim3(div_round_up(n, 256)), dim3(256), 0, st, n, act, (const _Float16*)y16, (_Float16*)g16);
+	TCNN_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace tcnn_amd

@@ -223,10 +223,12 @@ json GridEncodingHost::hyperparams() const {  // grid.h:1096-1114
 // ------------------------------------------------------------------------------------------
 // MLP (reference src/network.cu:48-138, fully_fused_mlp.cu:635-678, 865-891)
 // ------------------------------------------------------------------------------------------
-static int parse_activation(const std::string& s) {
-	if (ieq(s, "None")) return 0;
-	if (ieq(s, "ReLU")) return 1;
-	throw std::runtime_error("activation '" + s + "' is not supported by the MI355X engine (None, ReLU)");
+static const char* const ACT_NAMES[] = {"None", "ReLU", "LeakyReLU", "Exponential", "Sine", "Sigmoid", "Squareplus", "Softplus", "Tanh"};
+
+static int parse_activation(const std::string& s) {  // string_to_activation (common.cu)
+	for (int a = 0; a <= ACT_TANH; ++a)
+		if (ieq(s, ACT_NAMES[a])) return a;
+	throw std::runtime_error("Invalid activation name: " + s);
 }
 
 MlpHost::MlpHost(uint32_t n_input_dims, uint32_t n_output_dims, const json& net) {
@@ -266,7 +268,7 @@ void MlpHost::initialize_params(Pcg32& rng, float* out, float scale) const {
 	xavier(rng, padded_output, width, out, scale);
 }
 
-static const char* act_str(int a) { return a == 1 ? "ReLU" : "None"; }
+static const char* act_str(int a) { return a >= 0 && a <= ACT_TANH ? ACT_NAMES[a] : "None"; }
 
 json MlpHost::hyperparams() const {
 	return {{"otype", ieq(otype, "CutlassMLP") || ieq(otype, "MLP") ? "CutlassMLP" : "FullyFusedMLP"},
@@ -297,57 +299,168 @@ json AdamHost::hyperparams() const {
 }
 
 // ------------------------------------------------------------------------------------------
-// NetworkWithInputEncoding (grid + fused MLP)
+// Encodings (reference src/encoding.cu:77-150)
 // ------------------------------------------------------------------------------------------
-NetworkWithGridHost::NetworkWithGridHost(uint32_t n_in, uint32_t n_out, const json& enc, const json& net)
-	: n_input_dims(n_in), n_output_dims(n_out) {
-	const std::string eo = jval<std::string>(enc, "otype", "OneBlob");
-	TCNN_CHECK(ieq(eo, "HashGrid") || ieq(eo, "Grid") || ieq(eo, "TiledGrid") || ieq(eo, "DenseGrid"),
-	           "Encoding '" + eo + "' is not implemented by the MI355X engine yet (grid encodings only)");
-	grid = std::make_unique<GridEncodingHost>(n_in, enc);
-	grid->set_alignment(16);  // minimum_alignment(network) for FullyFusedMLP (network.cu:76-95)
-	mlp = MlpHost(grid->padded_output_width(), n_out, net);
+bool EncodingHost::known(const std::string& eo) {
+	return ieq(eo, "HashGrid") || ieq(eo, "Grid") || ieq(eo, "TiledGrid") || ieq(eo, "DenseGrid") || ieq(eo, "OneBlob") ||
+	       ieq(eo, "Identity");
 }
 
-bool NetworkWithGridHost::fused_ok() const {
-	return grid->n_to_pad == 0 && !grid->stochastic && mlp.output_activation == 0 &&
+EncodingHost::EncodingHost(uint32_t n_dims_to_encode, const json& enc) : n_dims(n_dims_to_encode) {
+	const std::string eo = jval<std::string>(enc, "otype", "OneBlob");  // encoding.cu:133
+	TCNN_CHECK(known(eo), "Encoding '" + eo + "' is not implemented by the MI355X engine yet");
+	if (ieq(eo, "OneBlob")) {
+		kind = EncKind::OneBlob;
+		n_bins = jval<uint32_t>(enc, "n_bins", 16u);  // encoding.cu:81-83
+		TCNN_CHECK(n_bins > 0 && (n_bins & (n_bins - 1)) == 0, "Number of bins must be a power of 2");
+	} else if (ieq(eo, "Identity")) {
+		kind = EncKind::Identity;
+		scale = jval<float>(enc, "scale", 1.0f);  // encoding.cu:77-79
+		offset = jval<float>(enc, "offset", 0.0f);
+	} else {
+		kind = EncKind::Grid;
+		grid = std::make_unique<GridEncodingHost>(n_dims_to_encode, enc);
+	}
+}
+
+uint32_t EncodingHost::n_output_unpadded() const {
+	switch (kind) {
+		case EncKind::OneBlob: return n_dims * n_bins;
+		case EncKind::Identity: return n_dims;
+		default: return grid->n_features;
+	}
+}
+
+void EncodingHost::set_alignment(uint32_t a) {  // Encoding::set_alignment (encoding.h)
+	if (kind == EncKind::Grid) {
+		grid->set_alignment(a);
+		return;
+	}
+	const uint32_t n = n_output_unpadded();
+	n_to_pad = (n + a - 1) / a * a - n;
+}
+
+void EncodingHost::initialize_params(Pcg32& rng, float* out, float s) const {
+	if (kind == EncKind::Grid) grid->initialize_params(rng, out, s);
+}
+
+json EncodingHost::hyperparams() const {
+	switch (kind) {
+		case EncKind::OneBlob: return {{"otype", "OneBlob"}, {"n_bins", n_bins}};
+		case EncKind::Identity: return {{"otype", "Identity"}, {"scale", scale}, {"offset", offset}};
+		default: return grid->hyperparams();
+	}
+}
+
+void EncodingHost::forward_aos(hipStream_t st, uint32_t B, const float* x, const void* params16, void* out16) const {
+	const uint32_t W = padded_output_width();
+	switch (kind) {
+		case EncKind::OneBlob: launch_oneblob_fwd(st, B, n_dims, n_bins, x, n_dims, out16, W, n_to_pad); break;
+		case EncKind::Identity: launch_identity_fwd(st, B, n_dims, scale, offset, x, n_dims, out16, W, n_to_pad); break;
+		default:
+			TCNN_CHECK(!grid->stochastic, "stochastic_interpolation is not implemented by the MI355X engine yet");
+			if (grid->n_to_pad) TCNN_HIP_CHECK(hipMemsetAsync(out16, 0, (size_t)B * W * 2, st));
+			launch_grid_fwd(st, grid->desc.n_pos_dims, grid->desc.n_features_per_level, grid->desc.hash_type, B, grid->desc.n_levels, x,
+			                grid->desc.n_pos_dims, params16, out16, false, W, grid->dev_levels(), grid->hash_grid(), grid->desc.interp);
+	}
+}
+
+void EncodingHost::backward_input(hipStream_t st, uint32_t B, const float* x, const void* dy16, float* dx) const {
+	const uint32_t W = padded_output_width();
+	switch (kind) {
+		case EncKind::OneBlob: launch_oneblob_bwd(st, B, n_dims, n_bins, x, n_dims, dy16, W, dx, n_dims); break;
+		case EncKind::Identity: launch_identity_bwd(st, B, n_dims, scale, dy16, W, dx, n_dims); break;
+		default: throw std::runtime_error("dL/dinput through the grid is not implemented by the MI355X engine yet");
+	}
+}
+
+// ------------------------------------------------------------------------------------------
+// NetworkWithInputEncoding
+// ------------------------------------------------------------------------------------------
+NetworkHost::NetworkHost(uint32_t n_in, uint32_t n_out, const json& e, const json& net) : n_input_dims(n_in), n_output_dims(n_out) {
+	enc = std::make_unique<EncodingHost>(n_in, e);
+	grid = enc->grid.get();
+	enc->set_alignment(16);  // minimum_alignment(network): 16 for FullyFusedMLP and CutlassMLP (network.cu:76-95)
+	mlp = MlpHost(enc->padded_output_width(), n_out, net);
+	TCNN_CHECK(fused_ok() || layered_ok(), "network shape (n_neurons = " + std::to_string(mlp.width) + ", input width " +
+	                                           std::to_string(mlp.n_input) + ") is not supported by the MI355X engine");
+}
+
+bool NetworkHost::fused_ok() const {
+	// CutlassMLP / "MLP" run on the layer-wise engine (the reference's separate GEMM-per-layer network)
+	const bool ff = ieq(mlp.otype, "FullyFusedMLP") || ieq(mlp.otype, "MegakernelMLP");
+	return ff && grid && grid->n_to_pad == 0 && !grid->stochastic && mlp.output_activation == 0 &&
+	       (mlp.activation == ACT_NONE || mlp.activation == ACT_RELU) &&
 	       fused_train_supported(mlp.width, mlp.n_input, mlp.n_hidden_layers, grid->desc.n_pos_dims,
 	                             grid->desc.n_features_per_level, mlp.padded_output, mlp.activation, grid->desc.hash_type);
 }
 
-void NetworkWithGridHost::initialize_params(Pcg32& rng, float* out, float scale) const {
+bool NetworkHost::layered_ok() const {
+	return layered_width_supported(mlp.width) && mlp.n_input % 16 == 0 && mlp.n_input <= 128 && mlp.padded_output <= 128 &&
+	       mlp.activation != ACT_SINE && mlp.output_activation != ACT_SINE;  // Sine has no post-activation backward
+}
+
+void NetworkHost::initialize_params(Pcg32& rng, float* out, float scale) const {
 	mlp.initialize_params(rng, out, scale);
-	grid->initialize_params(rng, out + mlp.n_params(), scale);
+	enc->initialize_params(rng, out + mlp.n_params(), scale);
 }
 
-json NetworkWithGridHost::hyperparams() const {
-	return {{"otype", "NetworkWithInputEncoding"}, {"encoding", grid->hyperparams()}, {"network", mlp.hyperparams()}};
+json NetworkHost::hyperparams() const {
+	return {{"otype", "NetworkWithInputEncoding"}, {"encoding", enc->hyperparams()}, {"network", mlp.hyperparams()}};
 }
 
-void NetworkWithGridHost::inference(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const void* params16, void* out16) {
-	TCNN_CHECK(B % 16 == 0, "inference: batch must be a multiple of 16");
-	TCNN_CHECK(mlp_infer_supported(mlp.width, mlp.n_input, mlp.n_hidden_layers, mlp.padded_output, mlp.activation) && grid->n_to_pad == 0 &&
-	           mlp.output_activation == 0, "inference: network shape not supported by the MI355X engine yet");
+void NetworkHost::forward_layers(hipStream_t st, StepWorkspace& ws, uint32_t B, const void* params16, void* out16, bool keep) {
+	const uint32_t W = mlp.width, IN = mlp.n_input, NH = mlp.n_hidden_layers, OUTP = mlp.padded_output;
+	const _Float16* p = (const _Float16*)params16;
+	ws.acts.reserve((size_t)(keep ? NH : 2) * B * W * 2);
+	auto act_buf = [&](uint32_t j) { return ws.acts.as<_Float16>() + (size_t)(keep ? j : (j & 1)) * B * W; };
+	const void* x = ws.enc16.p;
+	uint32_t K = IN;
+	for (uint32_t j = 0; j < NH; ++j) {
+		launch_layer_fwd(st, B, W, K, p, x, act_buf(j), mlp.activation);
+		p += (size_t)W * K;
+		x = act_buf(j);
+		K = W;
+	}
+	launch_layer_fwd(st, B, OUTP, W, p, x, out16, mlp.output_activation);
+}
+
+void NetworkHost::inference(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const void* params16, void* out16) {
+	TCNN_CHECK(B % 32 == 0, "inference: batch must be a multiple of 32");
 	const uint32_t IN = mlp.n_input;
+	const uint8_t* eparams = (const uint8_t*)params16 + (size_t)mlp.n_params() * 2;
+	if (fused_ok() && mlp_infer_supported(mlp.width, IN, mlp.n_hidden_layers, mlp.padded_output, mlp.activation)) {
+		ws.enc16.reserve((size_t)IN * B * 2);
+		launch_grid_fwd(st, grid->desc.n_pos_dims, grid->desc.n_features_per_level, grid->desc.hash_type, B, grid->desc.n_levels,
+		                pos, grid->desc.n_pos_dims, eparams, ws.enc16.p, true, 0, grid->dev_levels(), grid->hash_grid(), grid->desc.interp);
+		ws.wimage.reserve(fused_weight_image_bytes(mlp.width, IN, mlp.n_hidden_layers));
+		launch_pack_weights(st, mlp.width, IN, mlp.n_hidden_layers, params16, ws.wimage.p);
+		launch_mlp_infer(st, mlp.width, IN, mlp.n_hidden_layers, mlp.activation, true, B, ws.wimage.p, ws.enc16.p, out16);
+		return;
+	}
+	TCNN_CHECK(layered_ok(), "inference: network shape not supported by the MI355X engine");
 	ws.enc16.reserve((size_t)IN * B * 2);
-	const uint8_t* table = (const uint8_t*)params16 + (size_t)mlp.n_params() * 2;
-	launch_grid_fwd(st, grid->desc.n_pos_dims, grid->desc.n_features_per_level, grid->desc.hash_type, B, grid->desc.n_levels,
-	                pos, grid->desc.n_pos_dims, table, ws.enc16.p, true, 0, grid->dev_levels(), grid->hash_grid(), grid->desc.interp);
-	ws.wimage.reserve(fused_weight_image_bytes(mlp.width, IN, mlp.n_hidden_layers));
-	launch_pack_weights(st, mlp.width, IN, mlp.n_hidden_layers, params16, ws.wimage.p);
-	launch_mlp_infer(st, mlp.width, IN, mlp.n_hidden_layers, mlp.activation, true, B, ws.wimage.p, ws.enc16.p, out16);
+	enc->forward_aos(st, B, pos, eparams, ws.enc16.p);
+	forward_layers(st, ws, B, params16, out16, false);
 }
 
-void NetworkWithGridHost::fwd_bwd(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target,
-                                  uint32_t dims, float loss_scale, const void* params16, const void* dout16, void* out16, float* grad32,
-                                  const std::function<void(int)>& mark) {
-	TCNN_CHECK(fused_ok(), "training: network/encoding configuration not supported by the MI355X fused engine yet");
+void NetworkHost::fwd_bwd(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target, uint32_t dims,
+                          float loss_scale, const void* params16, const void* dout16, void* out16, float* grad32,
+                          const std::function<void(int)>& mark, float* dL_dinput) {
+	if (fused_ok() && !dL_dinput) fwd_bwd_fused(st, ws, B, pos, target, dims, loss_scale, params16, dout16, out16, grad32, mark);
+	else fwd_bwd_layered(st, ws, B, pos, target, dims, loss_scale, params16, dout16, out16, grad32, mark, dL_dinput);
+}
+
+void NetworkHost::fwd_bwd_fused(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target,
+                                uint32_t dims, float loss_scale, const void* params16, const void* dout16, void* out16, float* grad32,
+                                const std::function<void(int)>& mark) {
 	TCNN_CHECK(B % 32 == 0, "training: batch must be a multiple of 32");
 	const uint32_t n_mlp = mlp.n_params();
 	const uint32_t L = grid->desc.n_levels, F = grid->desc.n_features_per_level;
 	const uint32_t nb = fused_train_n_blocks(mlp.width, mlp.n_input, mlp.n_hidden_layers, grid->desc.n_pos_dims, dims,
 	                                         dout16 != nullptr, B);
 	ws.n_fused_blocks = nb;
+	ws.n_loss_partials = nb;
 	ws.dLdenc.reserve((size_t)L * F * B * 2);
 	ws.wgrad_partial.reserve((size_t)nb * n_mlp * 4);
 	ws.loss_partial.reserve((size_t)nb * 4);
@@ -374,6 +487,82 @@ void NetworkWithGridHost::fwd_bwd(hipStream_t st, StepWorkspace& ws, uint32_t B,
 	if (mark) mark(4);
 }
 
+// Layer-wise training pass (reference FullyFusedMLP::forward_impl/backward_impl dataflow,
+// fully_fused_mlp.cu:680-836; CutlassMLP cutlass_mlp.cu:120-315).
+void NetworkHost::fwd_bwd_layered(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target,
+                                  uint32_t dims, float loss_scale, const void* params16, const void* dout16, void* out16,
+                                  float* grad32, const std::function<void(int)>& mark, float* dL_dinput) {
+	TCNN_CHECK(layered_ok(), "training: network/encoding configuration not supported by the MI355X engine");
+	TCNN_CHECK(B % 32 == 0, "training: batch must be a multiple of 32");
+	const uint32_t W = mlp.width, IN = mlp.n_input, NH = mlp.n_hidden_layers, OUTP = mlp.padded_output;
+	const uint32_t n_mlp = mlp.n_params();
+	const _Float16* p16 = (const _Float16*)params16;
+	const uint8_t* eparams = (const uint8_t*)params16 + (size_t)n_mlp * 2;
+	const uint32_t nck = wgrad_n_chunks(B);
+	const uint32_t maxK = std::max(W, IN);
+	ws.enc16.reserve((size_t)B * IN * 2);
+	ws.out16.reserve((size_t)B * OUTP * 2);
+	ws.dout16.reserve((size_t)B * OUTP * 2);
+	ws.delta0.reserve((size_t)B * std::max(W, IN) * 2);
+	ws.delta1.reserve((size_t)B * std::max(W, IN) * 2);
+	ws.wgrad_partial.reserve((size_t)nck * std::max(W, OUTP) * maxK * 4);
+
+	// forward
+	enc->forward_aos(st, B, pos, eparams, ws.enc16.p);
+	void* out = out16 ? out16 : ws.out16.p;
+	forward_layers(st, ws, B, params16, out, true);
+	auto act = [&](uint32_t j) { return ws.acts.as<_Float16>() + (size_t)j * B * W; };
+
+	// loss / external dL/dout (loss-scaled by the caller) -> G fp16 [B][OUTP]
+	if (dout16) {
+		TCNN_HIP_CHECK(hipMemcpyAsync(ws.dout16.p, dout16, (size_t)B * OUTP * 2, hipMemcpyDeviceToDevice, st));
+		ws.n_loss_partials = 0;
+	} else {
+		const uint32_t nl = relative_l2_n_blocks(B, OUTP);
+		ws.loss_partial.reserve((size_t)nl * 4);
+		launch_relative_l2_partial(st, B, OUTP, dims, loss_scale, out, target, ws.dout16.p, ws.loss_partial.as<float>());
+		ws.n_loss_partials = nl;
+	}
+	launch_act_bwd_inplace(st, B * OUTP, mlp.output_activation, out, ws.dout16.p);
+	if (mark) mark(1);
+
+	// backward: weight offsets [W0 | W1..W_{NH-1} | Wout]
+	auto w_off = [&](uint32_t j) -> size_t { return j == 0 ? 0 : (size_t)W * IN + (size_t)(j - 1) * W * W; };
+	auto wgrad = [&](uint32_t N, uint32_t K, const void* dy, const void* x, size_t off) {
+		launch_wgrad(st, B, N, K, dy, x, ws.wgrad_partial.as<float>(), nck);
+		launch_reduce_partials(st, ws.wgrad_partial.as<float>(), nck, N * K, N * K, grad32 + off);
+	};
+	_Float16* dcur = ws.delta0.as<_Float16>();
+	_Float16* dnext = ws.delta1.as<_Float16>();
+	// output layer
+	wgrad(OUTP, W, ws.dout16.p, act(NH - 1), w_off(NH));
+	launch_layer_bwd(st, B, OUTP, W, p16 + w_off(NH), ws.dout16.p, act(NH - 1), dcur, mlp.activation);
+	for (uint32_t j = NH - 1; j >= 1; --j) {
+		wgrad(W, W, dcur, act(j - 1), w_off(j));
+		launch_layer_bwd(st, B, W, W, p16 + w_off(j), dcur, act(j - 1), dnext, mlp.activation);
+		std::swap(dcur, dnext);
+	}
+	wgrad(W, IN, dcur, ws.enc16.p, 0);
+	if (mark) mark(2);
+	const bool enc_grad = enc->n_params() > 0 || dL_dinput;
+	if (enc_grad) {
+		// dL/d(encoding) = W0^T delta_0 (no transfer), AoS [B][IN]
+		launch_layer_bwd(st, B, W, IN, p16, dcur, nullptr, dnext, ACT_NONE);
+		if (dL_dinput) enc->backward_input(st, B, pos, dnext, dL_dinput);
+	}
+	if (mark) mark(3);
+	if (grid) {
+		const uint32_t n_chunks = grid->bwd_chunks(B);
+		ws.n_grid_chunks = n_chunks;
+		ws.grid_partial.reserve((size_t)n_chunks * grid->n_params * 4);
+		launch_grid_bwd(st, grid->desc.n_pos_dims, grid->desc.n_features_per_level, grid->desc.hash_type, B, pos,
+		                grid->desc.n_pos_dims, dnext, 2, IN, grid->d_slices.as<GridSlice>(), (uint32_t)grid->slices.size(), n_chunks,
+		                ws.grid_partial.as<float>(), grid->n_params, grid->dev_levels(), grid->hash_grid(), grid->desc.interp);
+		launch_reduce_partials(st, ws.grid_partial.as<float>(), n_chunks, grid->n_params, grid->n_params, grad32 + n_mlp);
+	}
+	if (mark) mark(4);
+}
+
 // ------------------------------------------------------------------------------------------
 // Trainer (reference trainer.h:47-361, config.h:46-63)
 // ------------------------------------------------------------------------------------------
@@ -388,7 +577,7 @@ TrainerHost::TrainerHost(uint32_t n_in, uint32_t n_out, const json& cfg, uint32_
 	const std::string oo = jval<std::string>(opt, "otype", "Adam");
 	TCNN_CHECK(ieq(oo, "Adam"), "Optimizer '" + oo + "' is not implemented by the MI355X engine yet");
 	adam.update(opt);
-	model = std::make_unique<NetworkWithGridHost>(n_in, n_out, enc, net);
+	model = std::make_unique<NetworkHost>(n_in, n_out, enc, net);
 	n_params = model->n_params();
 	n_mlp = model->mlp.n_params();
 	initialize_params(seed);
@@ -435,7 +624,7 @@ void TrainerHost::training_step(hipStream_t st, uint32_t B, const float* input, 
 	mark(st, 0);
 	model->fwd_bwd(st, ws, B, input, target, n_output_dims, loss_scale, w16.p, nullptr, nullptr, g32.as<float>(),
 	               [&](int ph) { mark(st, ph); });
-	launch_sum(st, ws.loss_partial.as<float>(), ws.n_fused_blocks, d_loss.as<float>());
+	launch_sum(st, ws.loss_partial.as<float>(), ws.n_loss_partials, d_loss.as<float>());
 	mark(st, 5);
 	last_B = B;
 	if (run_optimizer) optimizer_step(st);

@@ -91,31 +91,75 @@ struct AdamHost {
 	json hyperparams() const;
 };
 
-// Workspace for one fused fwd/bwd over a batch of B (sizes grow only).
-struct StepWorkspace {
-	DevBuf dLdenc, wgrad_partial, loss_partial, grid_partial, grad32_tmp, out16, enc16, wimage;
-	uint32_t n_fused_blocks = 0, n_grid_chunks = 0;
+// Encodings of the network input (reference encodings/*.h): the multiresolution grid (parametric,
+// fused path), OneBlob (oneblob.h) and Identity (identity.h).
+enum class EncKind { Grid, OneBlob, Identity };
+
+struct EncodingHost {
+	EncKind kind = EncKind::Grid;
+	std::unique_ptr<GridEncodingHost> grid;
+	uint32_t n_dims = 0;        // input dims encoded
+	uint32_t n_bins = 16;       // OneBlob
+	float scale = 1.0f, offset = 0.0f;  // Identity
+	uint32_t n_to_pad = 0;      // OneBlob / Identity padding (grid: grid->n_to_pad)
+
+	EncodingHost(uint32_t n_dims_to_encode, const json& enc);
+	static bool known(const std::string& otype);
+	uint32_t n_output_unpadded() const;
+	uint32_t padded_output_width() const { return kind == EncKind::Grid ? grid->padded_output_width() : n_output_unpadded() + n_to_pad; }
+	void set_alignment(uint32_t a);
+	uint32_t n_params() const { return kind == EncKind::Grid ? grid->n_params : 0u; }
+	void initialize_params(Pcg32& rng, float* host_out, float scale = 1.0f) const;
+	json hyperparams() const;
+	// encoded output AoS fp16 [B][padded_output_width()] (padding: grid 0, OneBlob / Identity 1)
+	void forward_aos(hipStream_t st, uint32_t B, const float* x, const void* params16, void* out16) const;
+	// dL/dx fp32 [B][n_dims] from dL/d(encoding) fp16 AoS (OneBlob / Identity; the grid's is not built)
+	void backward_input(hipStream_t st, uint32_t B, const float* x, const void* dy16, float* dx) const;
 };
 
-// NetworkWithInputEncoding<__half> with a grid encoding and the fused MLP
-// (reference network_with_input_encoding.h:41-190).
-struct NetworkWithGridHost {
-	std::unique_ptr<GridEncodingHost> grid;
+// Workspace for one fwd/bwd over a batch of B (sizes grow only).
+struct StepWorkspace {
+	DevBuf dLdenc, wgrad_partial, loss_partial, grid_partial, grad32_tmp, out16, enc16, wimage;
+	DevBuf acts, delta0, delta1, dout16;  // layer-wise engine
+	uint32_t n_fused_blocks = 0, n_grid_chunks = 0, n_loss_partials = 0;
+};
+
+// NetworkWithInputEncoding<__half> (reference network_with_input_encoding.h:41-190) over two engines:
+//   "fused"   grid encoding + W in {32, 64} FullyFusedMLP: one register-resident kernel
+//             (mlp_fused.h) + the LDS-privatised grid backward;
+//   "layered" everything else (W = 128, OneBlob / Identity, CutlassMLP, output activations):
+//             per-layer MFMA kernels (mlp_layers.hip) with fp16 activations in HBM.
+struct NetworkHost {
+	std::unique_ptr<EncodingHost> enc;
+	GridEncodingHost* grid = nullptr;  // enc->grid when the encoding is a grid
 	MlpHost mlp;
 	uint32_t n_input_dims = 0, n_output_dims = 0;
-	NetworkWithGridHost(uint32_t n_in, uint32_t n_out, const json& enc, const json& net);
-	uint64_t n_params() const { return (uint64_t)mlp.n_params() + grid->n_params; }
+	NetworkHost(uint32_t n_in, uint32_t n_out, const json& enc, const json& net);
+	uint64_t n_params() const { return (uint64_t)mlp.n_params() + enc->n_params(); }
 	bool fused_ok() const;
+	bool layered_ok() const;
+	const char* engine() const { return fused_ok() ? "fused" : layered_ok() ? "layered" : "unsupported"; }
 	void initialize_params(Pcg32& rng, float* host_out, float scale = 1.0f) const;  // network first (nwie.h:124-130)
 
-	// params16: [mlp | grid] fp16. out16: fp16 [B][padded_output].
+	// params16: [mlp | encoding] fp16. out16: fp16 [B][padded_output].
 	void inference(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const void* params16, void* out16);
-	// fused forward+backward; dout16 == nullptr -> RelativeL2 on target, else external dL/dout.
-	// Writes fp32 gradient sums into grad32 ([mlp | grid]) and the per-block loss partials.
+	// forward+backward; dout16 == nullptr -> RelativeL2 on target, else external dL/dout.
+	// Writes fp32 gradient sums into grad32 ([mlp | encoding]) and the loss partials
+	// (ws.loss_partial[0 .. ws.n_loss_partials)). dL_dinput (optional): fp32 [B][n_input_dims].
 	void fwd_bwd(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target, uint32_t dims,
 	             float loss_scale, const void* params16, const void* dout16, void* out16, float* grad32,
-	             const std::function<void(int)>& mark = nullptr);
+	             const std::function<void(int)>& mark = nullptr, float* dL_dinput = nullptr);
 	json hyperparams() const;
+
+private:
+	void fwd_bwd_fused(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target, uint32_t dims,
+	                   float loss_scale, const void* params16, const void* dout16, void* out16, float* grad32,
+	                   const std::function<void(int)>& mark);
+	void fwd_bwd_layered(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target, uint32_t dims,
+	                     float loss_scale, const void* params16, const void* dout16, void* out16, float* grad32,
+	                     const std::function<void(int)>& mark, float* dL_dinput);
+	// forward through the layers from ws.enc16; hidden activations kept in ws.acts when `keep`
+	void forward_layers(hipStream_t st, StepWorkspace& ws, uint32_t B, const void* params16, void* out16, bool keep);
 };
 
 // Per-phase hipEvent timing of the training step (bench.py's live per-kernel roofline source).
@@ -134,7 +178,7 @@ struct TrainerHost {
 	uint32_t n_input_dims, n_output_dims;
 	PhaseTimer timer;
 	json config;
-	std::unique_ptr<NetworkWithGridHost> model;
+	std::unique_ptr<NetworkHost> model;
 	AdamHost adam;
 	std::string loss_otype;
 	uint64_t n_params = 0, n_mlp = 0;

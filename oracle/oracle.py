@@ -48,6 +48,8 @@ class Model(ctypes.Structure):
         ("grad16", ctypes.POINTER(ctypes.c_uint16)), ("grad32", ctypes.POINTER(ctypes.c_float)),
         ("m1", ctypes.POINTER(ctypes.c_float)), ("m2", ctypes.POINTER(ctypes.c_float)),
         ("steps", ctypes.POINTER(ctypes.c_uint32)),
+        ("enc_type", ctypes.c_uint32), ("n_dims", ctypes.c_uint32), ("n_bins", ctypes.c_uint32), ("IN", ctypes.c_uint32),
+        ("enc_scale", ctypes.c_float), ("enc_offset", ctypes.c_float),
     ]
 
 
@@ -91,6 +93,10 @@ def lib():
         _lib.orc_train_step.argtypes = [ctypes.POINTER(Model), ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
         _lib.orc_model_inference.argtypes = [ctypes.POINTER(Model), ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         _lib.orc_seed_seq.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
+        _lib.orc_oneblob_fwd.argtypes = [ctypes.c_uint32] * 3 + [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]
+        _lib.orc_oneblob_bwd.argtypes = [ctypes.c_uint32] * 3 + [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+        _lib.orc_identity_fwd.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_float, ctypes.c_float, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]
         _lib.orc_hfma.restype = ctypes.c_uint16
         _lib.orc_hfma.argtypes = [ctypes.c_uint16] * 3
     return _lib
@@ -230,6 +236,33 @@ def mlp_bwd(W, IN, NH, OUTP, params16, x16, hidden16, dout16, input_soa=True, ac
     return wgrad, din
 
 
+def oneblob_fwd(x, n_bins, n_pad=0):
+    """x float32 [B, D] -> uint16 AoS [B, D*n_bins + n_pad] (reference kernel_one_blob semantics)"""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    B, D = x.shape
+    out = np.empty((B, D * n_bins + n_pad), dtype=np.uint16)
+    lib().orc_oneblob_fwd(B, D, n_bins, _p(x), _p(out), D * n_bins + n_pad, n_pad)
+    return out
+
+
+def oneblob_bwd(x, n_bins, dy16):
+    """dL/dx float32 [B, D] from dL/dy uint16 AoS [B, stride]"""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    dy16 = np.ascontiguousarray(dy16, dtype=np.uint16)
+    B, D = x.shape
+    dx = np.empty((B, D), dtype=np.float32)
+    lib().orc_oneblob_bwd(B, D, n_bins, _p(x), _p(dy16), dy16.shape[1], _p(dx))
+    return dx
+
+
+def identity_fwd(x, scale=1.0, offset=0.0, n_pad=0):
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    B, D = x.shape
+    out = np.empty((B, D + n_pad), dtype=np.uint16)
+    lib().orc_identity_fwd(B, D, scale, offset, _p(x), _p(out), D + n_pad, n_pad)
+    return out
+
+
 def relative_l2(pred16, target, loss_scale=128.0, want_values=False):
     """pred16 uint16 [B, stride] CM; target float32 [B, dims]"""
     pred16 = np.ascontiguousarray(pred16, dtype=np.uint16)
@@ -249,12 +282,26 @@ def adam_step(cfg, n_matrix, loss_scale, current_step, w32, w16, grad16, m1, m2,
 
 
 class OracleModel:
-    """Trainer<float,__half,__half> over NetworkWithInputEncoding<Grid, FullyFusedMLP> on the CPU."""
+    """Trainer<float,__half,__half> over NetworkWithInputEncoding<Grid | OneBlob | Identity,
+    FullyFusedMLP> on the CPU (encoding padded to 16 columns, network.cu:76-95)."""
 
     def __init__(self, config, n_input_dims, n_output_dims, seed=1337):
         self.m = Model()
         enc, net, opt = config["encoding"], config["network"], config.get("optimizer", {})
-        self.m.grid = grid_cfg(enc, n_input_dims)
+        eo = enc.get("otype", "OneBlob").lower()
+        self.m.n_dims = n_input_dims
+        if eo == "oneblob":
+            self.m.enc_type = 1
+            self.m.n_bins = int(enc.get("n_bins", 16))
+            self.m.IN = (n_input_dims * self.m.n_bins + 15) // 16 * 16
+        elif eo == "identity":
+            self.m.enc_type = 2
+            self.m.enc_scale = float(enc.get("scale", 1.0))
+            self.m.enc_offset = float(enc.get("offset", 0.0))
+            self.m.IN = (n_input_dims + 15) // 16 * 16
+        else:
+            self.m.enc_type = 0
+            self.m.grid = grid_cfg(enc, n_input_dims)
         self.m.W = int(net.get("n_neurons", 128))
         self.m.NH = int(net.get("n_hidden_layers", 5))
         self.m.n_output_dims = n_output_dims

@@ -558,6 +558,80 @@ void orc_mlp_bwd(uint32_t W, uint32_t IN, uint32_t NH, uint32_t OUTP, uint32_t a
 }
 
 /* ------------------------------------------------------------------------------------------ */
+/* OneBlob -- encodings/oneblob.h:46-164, quartic_cdf common_device.h:905-920                  */
+/* ------------------------------------------------------------------------------------------ */
+/* nvcc compiles the reference with FMA contraction on; the contracted forms are written out. */
+static uint32_t orc_log2u(uint32_t v) { /* (uint32_t)std::log2(n_bins) for powers of two */
+	uint32_t r = 0;
+	while ((1u << r) < v) ++r;
+	return r;
+}
+static float quartic_cdf(float x, float inv_radius) {
+	const float u = x * inv_radius;
+	const float u2 = u * u;
+	const float u4 = u2 * u2;
+	float p = fmaf(-(2.0f / 3.0f), u2, 1.0f);
+	p = fmaf(1.0f / 5.0f, u4, p);
+	return fmaxf(0.0f, fminf(1.0f, fmaf((15.0f / 16.0f) * u, p, 0.5f)));
+}
+static float quartic_cdf_deriv(float x, float inv_radius) {
+	const float u = x * inv_radius;
+	const float tmp = fmaxf(fmaf(-u, u, 1.0f), 0.0f);
+	return (15.0f / 16.0f) * tmp * tmp * inv_radius;
+}
+/* left-boundary CDF with wrap-around (one_blob_subwarp_aligned, oneblob.h:48-51) */
+static float oneblob_left_cdf(uint32_t bin, uint32_t n_bins, float x) {
+	const float d = ldexpf((float)bin, -(int)orc_log2u(n_bins)) - x;
+	return quartic_cdf(d, (float)n_bins) + quartic_cdf(d - 1.0f, (float)n_bins) + quartic_cdf(d + 1.0f, (float)n_bins);
+}
+
+void orc_oneblob_fwd(uint32_t B, uint32_t D, uint32_t n_bins, const float* x, uint16_t* out, uint32_t stride, uint32_t n_pad) {
+	/* Reference lane j (= encoded index) holds bin b = j & (n_bins-1); the right CDF comes from
+	 * __shfl_sync(mask, left, b + 1, n_bins) (oneblob.h:57). The shuffle width is clamped by the 32-lane
+	 * warp: the source is lane ((b + 1) mod S) of the lane's S-wide segment, S = min(n_bins, 32), so
+	 * for n_bins = 64 bin 31 reads bin 0's left CDF and bin 63 reads bin 32's (+1 at the last bin). */
+	const uint32_t S = n_bins < 32 ? n_bins : 32;
+	for (uint32_t i = 0; i < B; ++i) {
+		uint16_t* row = out + (size_t)i * stride;
+		for (uint32_t d = 0; d < D; ++d) {
+			const float xv = x[(size_t)i * D + d];
+			for (uint32_t b = 0; b < n_bins; ++b) {
+				const uint32_t src = (b & ~(S - 1)) + ((b + 1) & (S - 1));
+				float right = oneblob_left_cdf(src, n_bins, xv);
+				if (b == n_bins - 1) right += 1.0f;
+				row[d * n_bins + b] = orc_f2h(right - oneblob_left_cdf(b, n_bins, xv));
+			}
+		}
+		for (uint32_t j = 0; j < n_pad; ++j) row[D * n_bins + j] = orc_f2h(1.0f);
+	}
+}
+
+void orc_oneblob_bwd(uint32_t B, uint32_t D, uint32_t n_bins, const float* x, const uint16_t* dy, uint32_t stride, float* dx) {
+	const float nb = (float)n_bins;
+	for (uint32_t i = 0; i < B; ++i)
+		for (uint32_t d = 0; d < D; ++d) {
+			const float xv = x[(size_t)i * D + d];
+			float left = quartic_cdf_deriv(-xv, nb) + quartic_cdf_deriv(-xv - 1.0f, nb) + quartic_cdf_deriv(-xv + 1.0f, nb);
+			float result = 0.0f;
+			for (uint32_t k = 0; k < n_bins; ++k) {
+				const float rb = ldexpf((float)(k + 1), -(int)orc_log2u(n_bins));
+				const float right = quartic_cdf_deriv(rb - xv, nb) + quartic_cdf_deriv(rb - xv - 1.0f, nb) + quartic_cdf_deriv(rb - xv + 1.0f, nb);
+				const float deriv = left - right;
+				left = right;
+				result = fmaf(orc_h2f(dy[(size_t)i * stride + d * n_bins + k]), deriv, result);
+			}
+			dx[(size_t)i * D + d] = result;
+		}
+}
+
+void orc_identity_fwd(uint32_t B, uint32_t D, float scale, float offset, const float* x, uint16_t* out, uint32_t stride,
+                      uint32_t n_pad) {
+	for (uint32_t i = 0; i < B; ++i)
+		for (uint32_t j = 0; j < D + n_pad; ++j)
+			out[(size_t)i * stride + j] = orc_f2h(j < D ? fmaf(x[(size_t)i * D + j], scale, offset) : 1.0f);
+}
+
+/* ------------------------------------------------------------------------------------------ */
 /* RelativeL2 -- losses/relative_l2.h:40-76                                                     */
 /* ------------------------------------------------------------------------------------------ */
 double orc_relative_l2(uint32_t B, uint32_t stride, uint32_t dims, float loss_scale,
@@ -635,11 +709,30 @@ void orc_adam_step(const orc_adam_cfg* c, uint32_t n, uint32_t n_matrix, float l
 /* Trainer (trainer.h:50-190) for NetworkWithInputEncoding<Grid, FullyFusedMLP>                  */
 /* ------------------------------------------------------------------------------------------ */
 
+static uint32_t model_enc_params(const orc_model* m) { return m->enc_type == 0 ? m->grid.n_params : 0u; }
+
+/* encoding forward: grid -> SoA [IN][B] (returns 1), OneBlob / Identity -> AoS [B][IN] (returns 0) */
+static int model_encode(const orc_model* m, uint32_t B, const float* pos, uint16_t* enc) {
+	if (m->enc_type == 1) {
+		orc_oneblob_fwd(B, m->n_dims, m->n_bins, pos, enc, m->IN, m->IN - m->n_dims * m->n_bins);
+		return 0;
+	}
+	if (m->enc_type == 2) {
+		orc_identity_fwd(B, m->n_dims, m->enc_scale, m->enc_offset, pos, enc, m->IN, m->IN - m->n_dims);
+		return 0;
+	}
+	orc_grid_fwd(&m->grid, B, pos, m->w16 + m->n_mlp_params, enc);
+	return 1;
+}
+
 int orc_model_init(orc_model* m, uint32_t seed) {
-	if (orc_grid_init(&m->grid) != 0) return -1;
-	const uint32_t IN = m->grid.n_levels * m->grid.n_features_per_level;
+	if (m->enc_type == 0) {
+		if (orc_grid_init(&m->grid) != 0) return -1;
+		m->IN = m->grid.n_levels * m->grid.n_features_per_level;
+	}
+	const uint32_t IN = m->IN;
 	m->n_mlp_params = orc_mlp_n_params(m->W, IN, m->NH, m->OUTP);
-	m->n_params = m->n_mlp_params + m->grid.n_params;
+	m->n_params = m->n_mlp_params + model_enc_params(m);
 	m->adam_step = 0;
 	size_t n = m->n_params;
 	m->w32 = (float*)calloc(n, 4); m->w16 = (uint16_t*)calloc(n, 2);
@@ -656,7 +749,7 @@ int orc_model_init(orc_model* m, uint32_t seed) {
 	for (uint32_t k = 1; k < m->NH; ++k) { orc_xavier_uniform(&rng, m->W, m->W, p, 1.0f); p += (size_t)m->W * m->W; }
 	orc_xavier_uniform(&rng, m->OUTP, m->W, p, 1.0f); p += (size_t)m->OUTP * m->W;
 	/* GridEncodingTemplated::initialize_params (grid.h:1059-1062) */
-	orc_generate_uniform(&rng, m->grid.n_params, p, -1e-4f, 1e-4f);
+	if (m->enc_type == 0) orc_generate_uniform(&rng, m->grid.n_params, p, -1e-4f, 1e-4f);
 	orc_f2h_array(m->w32, m->w16, n); /* trainer.h:83-85 */
 	return 0;
 }
@@ -667,27 +760,30 @@ void orc_model_free(orc_model* m) {
 }
 
 void orc_model_inference(orc_model* m, uint32_t B, const float* pos, uint16_t* out, int n_threads) {
-	const uint32_t IN = m->grid.n_levels * m->grid.n_features_per_level;
+	const uint32_t IN = m->IN;
 	uint16_t* enc = (uint16_t*)malloc((size_t)IN * B * 2);
-	orc_grid_fwd(&m->grid, B, pos, m->w16 + m->n_mlp_params, enc);
-	orc_mlp_fwd(m->W, IN, m->NH, m->OUTP, m->activation, m->w16, B, enc, 1, out, NULL, n_threads);
+	const int soa = model_encode(m, B, pos, enc);
+	orc_mlp_fwd(m->W, IN, m->NH, m->OUTP, m->activation, m->w16, B, enc, soa, out, NULL, n_threads);
 	free(enc);
 }
 
 double orc_train_step(orc_model* m, uint32_t B, const float* pos, const float* target, int run_optimizer, int n_threads) {
-	const uint32_t IN = m->grid.n_levels * m->grid.n_features_per_level;
+	const uint32_t IN = m->IN;
 	const float loss_scale = 128.0f; /* default_loss_scale<__half> (common.h:232) */
 	uint16_t* enc = (uint16_t*)malloc((size_t)IN * B * 2);
 	uint16_t* out = (uint16_t*)malloc((size_t)m->OUTP * B * 2);
 	uint16_t* hidden = (uint16_t*)malloc((size_t)m->NH * m->W * B * 2);
 	uint16_t* dout = (uint16_t*)malloc((size_t)m->OUTP * B * 2);
 	uint16_t* denc = (uint16_t*)malloc((size_t)IN * B * 2);
-	orc_grid_fwd(&m->grid, B, pos, m->w16 + m->n_mlp_params, enc);
-	orc_mlp_fwd(m->W, IN, m->NH, m->OUTP, m->activation, m->w16, B, enc, 1, out, hidden, n_threads);
+	const int soa = model_encode(m, B, pos, enc);
+	orc_mlp_fwd(m->W, IN, m->NH, m->OUTP, m->activation, m->w16, B, enc, soa, out, hidden, n_threads);
 	double loss = orc_relative_l2(B, m->OUTP, m->n_output_dims, loss_scale, out, target, NULL, dout);
-	orc_mlp_bwd(m->W, IN, m->NH, m->OUTP, m->activation, m->w16, B, enc, 1, hidden, dout, m->grad32, denc, n_threads);
-	memset(m->grad32 + m->n_mlp_params, 0, (size_t)m->grid.n_params * 4);
-	orc_grid_bwd(&m->grid, B, pos, denc, m->grad32 + m->n_mlp_params);
+	orc_mlp_bwd(m->W, IN, m->NH, m->OUTP, m->activation, m->w16, B, enc, soa, hidden, dout, m->grad32,
+	            m->enc_type == 0 ? denc : NULL, n_threads);
+	if (m->enc_type == 0) {
+		memset(m->grad32 + m->n_mlp_params, 0, (size_t)m->grid.n_params * 4);
+		orc_grid_bwd(&m->grid, B, pos, denc, m->grad32 + m->n_mlp_params);
+	}
 	orc_f2h_array(m->grad32, m->grad16, m->n_params);
 	if (run_optimizer) {
 		m->adam_step++;

@@ -89,6 +89,16 @@ void orc_mlp_bwd(uint32_t W, uint32_t IN, uint32_t NH, uint32_t OUTP, uint32_t a
                  const uint16_t* hidden, const uint16_t* dL_dout, float* wgrad,
                  uint16_t* dL_dinput, int n_threads);
 
+/* ---- OneBlob (encodings/oneblob.h:46-164) and Identity (encodings/identity.h:45-85) ----
+ * x fp32 CM [D][B] (x[i*D+d]); out fp16 AoS [B][stride]: out[i*stride + d*n_bins + b], padding
+ * columns [D*n_bins, D*n_bins + n_pad) = 1. Forward reproduces the reference's subwarp shuffle,
+ * including its 32-lane wrap for n_bins > 32 (see tcnn_oracle.c). */
+void orc_oneblob_fwd(uint32_t B, uint32_t D, uint32_t n_bins, const float* x, uint16_t* out, uint32_t stride, uint32_t n_pad);
+/* kernel_one_blob_backward: dL/dx fp32 [B][D] from dL/dy fp16 AoS [B][stride] */
+void orc_oneblob_bwd(uint32_t B, uint32_t D, uint32_t n_bins, const float* x, const uint16_t* dy, uint32_t stride, float* dx);
+void orc_identity_fwd(uint32_t B, uint32_t D, float scale, float offset, const float* x, uint16_t* out, uint32_t stride,
+                      uint32_t n_pad);
+
 /* ---- RelativeL2 loss (losses/relative_l2.h:40-76) ----
  * pred fp16 CM [stride][B]; target fp32 CM [dims][B]; values fp32 CM [stride][B] (may be NULL);
  * grads fp16 CM [stride][B]. Returns sum of values (in double). */
@@ -107,7 +117,7 @@ void orc_adam_step(const orc_adam_cfg* c, uint32_t n, uint32_t n_matrix, float l
                    uint32_t current_step, float* w32, uint16_t* w16, const uint16_t* grad16,
                    float* m1, float* m2, uint32_t* steps);
 
-/* ---- Trainer::training_step for NetworkWithInputEncoding<HashGrid, FullyFusedMLP> ----
+/* ---- Trainer::training_step for NetworkWithInputEncoding<Grid | OneBlob | Identity, FullyFusedMLP> ----
  * (trainer.h:97-190, network_with_input_encoding.h:70-113). Param layout [MLP | grid].
  * Returns the loss sum (trainer.h:205-207). Gradients are rounded to fp16 (the reference's
  * m_param_gradients is __half) before Adam. run_optimizer=0 leaves params untouched. */
@@ -117,6 +127,10 @@ typedef struct {
 	orc_adam_cfg adam;
 	uint32_t n_params, n_mlp_params, adam_step;
 	float* w32; uint16_t* w16; uint16_t* grad16; float* grad32; float* m1; float* m2; uint32_t* steps;
+	/* encoding: 0 = grid (above), 1 = OneBlob, 2 = Identity; IN = padded encoding width (set by the
+	 * caller for OneBlob / Identity: n_dims * n_bins or n_dims, rounded up to 16) */
+	uint32_t enc_type, n_dims, n_bins, IN;
+	float enc_scale, enc_offset;
 } orc_model;
 int orc_model_init(orc_model* m, uint32_t seed); /* allocate + Trainer::initialize_params */
 void orc_model_free(orc_model* m);

@@ -10,6 +10,7 @@ from oracle import oracle as O
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 CONFIG_HASH = json.load(open(os.path.join(GOLD, "config_hash.json")))
+CONFIG_ONEBLOB = json.load(open(os.path.join(GOLD, "config_oneblob.json")))
 
 
 def rgb_field(pos):

@@ -1,0 +1,196 @@
+"""GPU parity of the layer-wise MFMA engine (mlp_layers.hip) and the OneBlob / Identity encodings
+(encodings.hip) against the CPU oracle, on the BASELINE configs the register-resident fused kernel
+does not take: config_oneblob.json as-is (OneBlob 64 bins + FullyFusedMLP W128/H5), its W64/H2
+variant, HashGrid + W128/H4 (the LDS-pressure config), CutlassMLP, Identity.
+
+Tolerances (north_star: 1e-3 relative, fp16):
+  * OneBlob / Identity encodings: bit-exact (same fp32 op sequence, explicit FMAs)
+  * loss sum: relative 1e-3; gradients: relative L2 <= 1e-3 (2e-3 for the 6-layer W128 network,
+    whose fp16 hidden activations round at every layer in both implementations)
+  * network output: rtol 2e-3, atol 2e-4 (2 fp16 ulp)
+"""
+import copy
+import ctypes
+import json
+
+import numpy as np
+import pytest
+
+from helpers import CONFIG_HASH, CONFIG_ONEBLOB, make_batch, rel_err, trainer_arrays
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_mod():
+    import torch
+    assert torch.cuda.is_available()
+    return torch
+
+
+def _cfg(enc, net):
+    c = copy.deepcopy(CONFIG_HASH)
+    c["encoding"] = enc
+    c["network"] = net
+    return c
+
+
+def _net(w, nh, otype="FullyFusedMLP"):
+    return {"otype": otype, "activation": "ReLU", "output_activation": "None", "n_neurons": w, "n_hidden_layers": nh}
+
+
+CONFIGS = {
+    "oneblob_as_file_w128_h5": (CONFIG_ONEBLOB, 2e-3),
+    "oneblob_w64_h2": (_cfg({"otype": "OneBlob", "n_bins": 64}, _net(64, 2)), 1e-3),
+    "oneblob16_w64_h2": (_cfg({"otype": "OneBlob", "n_bins": 16}, _net(64, 2)), 1e-3),
+    "hashgrid_w128_h4": (_cfg(CONFIG_HASH["encoding"], _net(128, 4)), 2e-3),
+    "hashgrid_cutlass_w64_h2": (_cfg(CONFIG_HASH["encoding"], _net(64, 2, "CutlassMLP")), 1e-3),
+    "identity_w32_h3": (_cfg({"otype": "Identity"}, _net(32, 3)), 1e-3),
+}
+
+
+@pytest.mark.parametrize("n_bins,n_in", [(64, 2), (16, 2), (16, 3), (32, 1)])
+def test_oneblob_encoding_bit_exact(torch_mod, n_bins, n_in):
+    torch = torch_mod
+    from tinycudann import _lib as L
+    lib = L.lib()
+    m = L.check_ptr(lib.tcnn_create_encoding(n_in, json.dumps({"otype": "OneBlob", "n_bins": n_bins}).encode(), 1))
+    B = 1024
+    rng = np.random.default_rng(5)
+    x = rng.random((B, n_in), dtype=np.float32)
+    x[:4] = [[0.0] * n_in, [0.4999] * n_in, [0.999999] * n_in, [1.0 / n_bins] * n_in]  # boundary cases
+    xd = torch.from_numpy(x).cuda()
+    W = lib.tcnn_module_n_output_dims(m)
+    out = torch.empty(B, W, dtype=torch.float16, device="cuda")
+    L.check(lib.tcnn_module_inference(m, None, B, ctypes.c_void_p(xd.data_ptr()), ctypes.c_void_p(out.data_ptr()), None))
+    torch.cuda.synchronize()
+    ref = O.oneblob_fwd(x, n_bins, W - n_in * n_bins)
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint16), ref)
+    # backward: dL/dx
+    dy = torch.from_numpy(rng.standard_normal((B, W)).astype(np.float32)).half().cuda()
+    dx = torch.empty(B, n_in, dtype=torch.float32, device="cuda")
+    ctx = L.check_ptr(lib.tcnn_module_forward(m, None, B, ctypes.c_void_p(xd.data_ptr()), ctypes.c_void_p(out.data_ptr()), None, 1))
+    L.check(lib.tcnn_module_backward(m, None, ctx, B, ctypes.c_void_p(dx.data_ptr()), ctypes.c_void_p(dy.data_ptr()), None,
+                                     ctypes.c_void_p(xd.data_ptr()), ctypes.c_void_p(out.data_ptr()), None))
+    torch.cuda.synchronize()
+    refdx = O.oneblob_bwd(x, n_bins, dy.cpu().numpy().view(np.uint16))
+    np.testing.assert_allclose(dx.cpu().numpy(), refdx, rtol=1e-5, atol=1e-5)
+    lib.tcnn_context_destroy(ctx)
+    lib.tcnn_module_destroy(m)
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_layered_step_gradients_and_loss(torch_mod, name):
+    torch = torch_mod
+    from tinycudann import Trainer
+    cfg, tol = CONFIGS[name]
+    t = Trainer(2, 3, cfg, seed=1337)
+    assert t.engine == "layered", t.engine
+    om = O.OracleModel(cfg, 2, 3, seed=1337)
+    assert t.n_params == om.n_params
+    a0 = trainer_arrays(t)
+    np.testing.assert_array_equal(a0["w16"], om.w16)
+    B = 512
+    pos, tgt = make_batch(B)
+    t.training_step(torch.from_numpy(pos).cuda(), torch.from_numpy(tgt).cuda(), run_optimizer=False)
+    loss_gpu = t.loss()
+    loss_ref = om.train_step(pos, tgt, run_optimizer=False, n_threads=4)
+    assert abs(loss_gpu - loss_ref) <= 1e-3 * abs(loss_ref), (loss_gpu, loss_ref)
+    a = trainer_arrays(t)
+    nm = om.n_mlp_params
+    e_mlp = rel_err(a["g32"][:nm], om.grad32[:nm])
+    assert e_mlp <= tol, e_mlp
+    if om.n_params > nm:
+        e_enc = rel_err(a["g32"][nm:], om.grad32[nm:])
+        assert e_enc <= tol, e_enc
+
+
+@pytest.mark.parametrize("name", ["oneblob_as_file_w128_h5", "hashgrid_w128_h4", "identity_w32_h3"])
+def test_layered_inference_matches_oracle(torch_mod, name):
+    torch = torch_mod
+    from tinycudann import Trainer
+    cfg, _ = CONFIGS[name]
+    t = Trainer(2, 3, cfg, seed=1337)
+    om = O.OracleModel(cfg, 2, 3, seed=1337)
+    pos, _ = make_batch(1024, seed=3)
+    out = t.inference(torch.from_numpy(pos).cuda()).cpu().numpy()
+    ref = O.h2f(om.inference(pos, n_threads=4))[:, :3]
+    np.testing.assert_allclose(out, ref, rtol=2e-3, atol=2e-4)
+
+
+@pytest.mark.parametrize("name", ["oneblob_as_file_w128_h5", "hashgrid_w128_h4"])
+def test_layered_training_trajectory_tracks_oracle(torch_mod, name):
+    torch = torch_mod
+    from tinycudann import Trainer
+    cfg, _ = CONFIGS[name]
+    t = Trainer(2, 3, cfg, seed=1337)
+    om = O.OracleModel(cfg, 2, 3, seed=1337)
+    B = 1024
+    lg, lr = [], []
+    for s in range(8):
+        pos, tgt = make_batch(B, step=s)
+        t.training_step(torch.from_numpy(pos).cuda(), torch.from_numpy(tgt).cuda())
+        lg.append(t.loss())
+        lr.append(om.train_step(pos, tgt, n_threads=8))
+    lg, lr = np.array(lg), np.array(lr)
+    assert lg[-1] < lg[0]
+    np.testing.assert_allclose(lg, lr, rtol=5e-2)
+
+
+def test_lds_pressure_config_full_batch(torch_mod):
+    """BASELINE configs[3]: HashGrid + W128/H4 at B = 2^20 on one GPU -- finite, decreasing loss
+    (size-independent property; the oracle covers the same code at B = 512 above)."""
+    torch = torch_mod
+    from tinycudann import Trainer
+    cfg, _ = CONFIGS["hashgrid_w128_h4"]
+    t = Trainer(2, 3, cfg, seed=1337)
+    B = 1 << 20
+    losses = []
+    for s in range(6):
+        pos, tgt = make_batch(B, step=s)
+        t.training_step(torch.from_numpy(pos).cuda(), torch.from_numpy(tgt).cuda())
+        losses.append(t.loss())
+    assert np.all(np.isfinite(losses))
+    assert losses[-1] < losses[0], losses
+
+
+def test_create_network_identity_module(torch_mod):
+    """cpp_api create_network (Identity encoding + network, cpp_api.cu:151-153): forward and
+    backward (params + dL/dinput) against the oracle."""
+    torch = torch_mod
+    from tinycudann import _lib as L
+    lib = L.lib()
+    net = _net(64, 2)
+    m = L.check_ptr(lib.tcnn_create_network(3, 3, json.dumps(net).encode()))
+    n = lib.tcnn_module_n_params(m)
+    assert n == O.mlp_n_params(64, 16, 2, 16)
+    p32 = torch.zeros(n, dtype=torch.float32, device="cuda")
+    L.check(lib.tcnn_module_initialize_params(m, 42, ctypes.c_void_p(p32.data_ptr()), 1.0))
+    p16 = p32.half().contiguous()
+    B = 512
+    x = np.random.default_rng(1).random((B, 3), dtype=np.float32)
+    xd = torch.from_numpy(x).cuda()
+    out = torch.empty(B, 16, dtype=torch.float16, device="cuda")
+    ctx = L.check_ptr(lib.tcnn_module_forward(m, None, B, ctypes.c_void_p(xd.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                              ctypes.c_void_p(p16.data_ptr()), 1))
+    dout = np.zeros((B, 16), np.float32)
+    dout[:, :3] = np.random.default_rng(2).standard_normal((B, 3)) * 0.05
+    dout16 = torch.from_numpy(dout).half().cuda()
+    grad = torch.empty(n, dtype=torch.float16, device="cuda")
+    dx = torch.empty(B, 3, dtype=torch.float32, device="cuda")
+    L.check(lib.tcnn_module_backward(m, None, ctx, B, ctypes.c_void_p(dx.data_ptr()), ctypes.c_void_p(dout16.data_ptr()),
+                                     ctypes.c_void_p(grad.data_ptr()), ctypes.c_void_p(xd.data_ptr()),
+                                     ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(p16.data_ptr())))
+    torch.cuda.synchronize()
+    params16 = p16.cpu().numpy().view(np.uint16)
+    enc = O.identity_fwd(x, n_pad=13)
+    outr, hidden = O.mlp_fwd(64, 16, 2, 16, params16, enc, input_soa=False)
+    np.testing.assert_allclose(O.h2f(out.cpu().numpy().view(np.uint16)), O.h2f(outr), rtol=2e-3, atol=2e-4)
+    wg, denc = O.mlp_bwd(64, 16, 2, 16, params16, enc, hidden, dout16.cpu().numpy().view(np.uint16), input_soa=False)
+    assert rel_err(grad.float().cpu().numpy(), wg) <= 1e-3
+    # identity_backward: dL/dx = (half)(dL/denc * scale)
+    refdx = O.h2f(denc)[:, :3]
+    assert rel_err(dx.cpu().numpy(), refdx) <= 2e-3
+    lib.tcnn_context_destroy(ctx)
+    lib.tcnn_module_destroy(m)

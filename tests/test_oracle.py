@@ -106,3 +106,63 @@ def test_hfma_single_rounding():
         got = L.orc_hfma(int(a[i].view(np.uint16)), int(b[i].view(np.uint16)), int(c[i].view(np.uint16)))
         exact = np.float64(a[i]) * np.float64(b[i]) + np.float64(c[i])
         assert got == np.float16(exact).view(np.uint16), i
+
+
+# ---- OneBlob restatement (oneblob.h:46-164, common_device.h:905-920) ----
+def test_oneblob_partition_of_unity_small_bins():
+    """For n_bins <= 32 the reference's shuffle wraps inside the n_bins segment, so the bins of one
+    dimension telescope to exactly right(last) - left(0) = 1 (quartic CDF, wrap-around)."""
+    rng = np.random.default_rng(0)
+    x = rng.random((2000, 2), dtype=np.float32)
+    for nb in (4, 16, 32):
+        e = O.h2f(O.oneblob_fwd(x, nb)).reshape(2000, 2, nb).astype(np.float64)
+        np.testing.assert_allclose(e.sum(axis=2), 1.0, atol=nb * 5e-4)
+        assert e.min() >= -1e-3
+        # the blob sits on the bin containing x
+        peak = e.argmax(axis=2)
+        ok = np.abs(((peak + 0.5) / nb - x + 0.5) % 1.0 - 0.5) <= 1.5 / nb
+        assert ok.mean() > 0.999
+
+
+def test_oneblob_64_bins_reproduces_32_lane_shuffle_wrap():
+    """n_bins = 64 > warp size: bin 31 reads bin 0's left CDF and bin 63 reads bin 32's
+    (+1 wrap), the reference's __shfl_sync(.., bin + 1, 64) semantics on 32-lane warps."""
+    x = np.array([[0.3], [0.7], [0.49], [0.99]], np.float32)
+    e = O.h2f(O.oneblob_fwd(x, 64))
+    assert e[0, 31] == -1.0 and e[0, 63] == 1.0   # x < 0.48: bin 31 = L(0) - L(31) = -1
+    assert e[1, 31] == 0.0 and e[1, 63] == 0.0    # 0.5 < x < 0.98
+    # bins away from 31/63 are the ordinary quartic blob
+    assert abs(e[0, 19] - 0.0) < 1.0 and e[0, 15:24].sum() > 0.99
+
+
+def test_oneblob_backward_matches_finite_differences():
+    rng = np.random.default_rng(1)
+    nb = 16
+    x = rng.uniform(0.05, 0.95, (64, 2)).astype(np.float32)
+    dy = rng.standard_normal((64, 2 * nb)).astype(np.float32)
+    dy16 = O.f2h(dy)
+    dx = O.oneblob_bwd(x, nb, dy16)
+    # reference derivative in float64 from the smooth CDF (no fp16 rounding)
+    def L(b, xv):
+        def q(t):
+            u = t * nb
+            return np.clip(15 / 16 * u * (1 - 2 / 3 * u * u + u ** 4 / 5) + 0.5, 0, 1)
+        d = b / nb - xv
+        return q(d) + q(d - 1) + q(d + 1)
+    eps = 1e-4
+    dyf = O.h2f(dy16).astype(np.float64).reshape(64, 2, nb)
+    fd = np.zeros((64, 2))
+    for i in range(64):
+        for d in range(2):
+            xv = float(x[i, d])
+            b = np.arange(nb)
+            def enc(v):
+                return L(b + 1, v) - L(b, v)
+            fd[i, d] = (dyf[i, d] * (enc(xv + eps) - enc(xv - eps)) / (2 * eps)).sum()
+    np.testing.assert_allclose(dx, fd, rtol=2e-3, atol=2e-3)
+
+
+def test_identity_encoding():
+    x = np.array([[0.25, -3.0]], np.float32)
+    e = O.h2f(O.identity_fwd(x, scale=2.0, offset=0.5, n_pad=2))
+    np.testing.assert_array_equal(e, [[1.0, -5.5, 1.0, 1.0]])
