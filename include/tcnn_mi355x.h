@@ -110,15 +110,17 @@ int tcnn_trainer_set_gradient_scale(tcnn_trainer* t, float scale);
 int tcnn_trainer_set_params_full_precision(tcnn_trainer* t, const float* host_params, uint64_t n);
 /* Adam step counter (AdamOptimizer::step(), adam.h:200-202). */
 uint32_t tcnn_trainer_optimizer_step_count(const tcnn_trainer* t);
-/* Engine diagnostics: name of the path the trainer runs ("fused" / "unfused"). */
+/* Engine diagnostics: name of the path the trainer runs ("fused" / "layered" / "unsupported"). */
 const char* tcnn_trainer_engine(const tcnn_trainer* t);
 
 /* ---- per-phase hipEvent timing of training steps (measurement hook, not in the reference) ----
- * Between begin and end every training_step records events around its phases on its stream:
- * 0 fused grid-encode + MLP fwd/loss/bwd kernel, 1 weight-gradient reduction, 2 grid backward,
- * 3 grid-gradient reduction, 4 loss sum, 5 Adam (only when the optimizer ran in that step).
+ * Between begin and end training_step records events around its phases on its stream:
+ * 0 fused grid-encode + MLP fwd/loss/bwd kernel (layered engine: the whole fwd/bwd), 1 grid backward,
+ * 2 reductions + Adam on the critical path, 3 join with the side stream (overlapped step) / loss sum.
  * end() synchronises the device and writes the mean ms per phase over the complete steps. */
 int tcnn_trainer_profile_begin(tcnn_trainer* t);
+/* same, recording phase events only on every `every`-th step (each event record idles the GPU briefly) */
+int tcnn_trainer_profile_begin_sampled(tcnn_trainer* t, uint32_t every);
 int tcnn_trainer_profile_end(tcnn_trainer* t, double* ms_per_phase, uint32_t n_phases, uint32_t* n_steps);
 
 /* ---- self test (layout probe for the MFMA / transpose-read operand maps) ---- */

@@ -307,9 +307,12 @@ int tcnn_trainer_set_params_full_precision(tcnn_trainer* t, const float* host, u
 uint32_t tcnn_trainer_optimizer_step_count(const tcnn_trainer* t) { return t->t->adam_step; }
 const char* tcnn_trainer_engine(const tcnn_trainer* t) { return t->t->model->engine(); }
 
-int tcnn_trainer_profile_begin(tcnn_trainer* t) {
+int tcnn_trainer_profile_begin(tcnn_trainer* t) { return tcnn_trainer_profile_begin_sampled(t, 1); }
+int tcnn_trainer_profile_begin_sampled(tcnn_trainer* t, uint32_t every) {
 	return guard([&] {
 		t->t->timer.reset();
+		t->t->timer.every = every ? every : 1;
+		t->t->timer.counter = 0;
 		t->t->timer.enabled = true;
 	});
 }

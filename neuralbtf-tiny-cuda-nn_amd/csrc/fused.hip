@@ -45,6 +45,18 @@ void launch_pack_weights(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, c
 	throw std::runtime_error("pack weights: unsupported shape");
 }
 
+void fused_image_layout(uint32_t W, uint32_t IN, uint32_t NH, uint32_t* RSI, uint32_t* RSW, uint32_t* oWh, uint32_t* oWo) {
+#define X(w, in, nh)                                                                      \
+	if (W == w && IN == in && NH == nh) {                                                 \
+		using L = FusedLayout<w, in, nh>;                                                 \
+		*RSI = L::RSI; *RSW = L::RSW; *oWh = L::oWh; *oWo = L::oWo;                       \
+		return;                                                                           \
+	}
+	TCNN_FUSED_SHAPES(X)
+#undef X
+	throw std::runtime_error("fused image layout: unsupported shape");
+}
+
 static uint32_t device_cu_count() {
 	int dev = 0, n = 0;
 	TCNN_HIP_CHECK(hipGetDevice(&dev));

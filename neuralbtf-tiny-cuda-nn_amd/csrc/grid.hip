@@ -4,6 +4,7 @@
 //                   (reference grid.h:214-320; int32 fixed-point sums instead of fp16 atomics)
 #include "kernels.h"
 
+#include "adam_device.h"
 #include "grid_device.h"
 
 namespace tcnn_amd {
@@ -267,20 +268,67 @@ __device__ __forceinline__ void grid_bwd_mode(int mode, int layout, uint32_t B, 
 	grid_bwd_points<D, F, H, KIND, 1>(layout, B, pos, pstride, dLdy, dy_stride, level, li, hash_grid, interp, begin, len, f0, i0, i1, scale, acc);
 }
 
+// Network-gradient tail of the epilogue (extra workgroups g = 0 .. n_mlp_groups-1): group sums of
+// the fused kernel's slabs (same grouping and order as launch_reduce_partials), then the last
+// group finishes the sum, runs Adam on the network parameters and writes the fused weight image.
+__device__ void grid_bwd_mlp_tail(const GridBwdEpilogue& ep, uint32_t g, volatile uint32_t* flag) {
+	const uint32_t G = ep.n_mlp_groups, N = ep.n_mlp, P = ep.n_wparts;
+	const uint32_t per = (P + G - 1) / G;
+	const uint32_t j0 = g * per, j1 = min(P, j0 + per);
+	float* dst = ep.group_slab + (size_t)g * (N + 4);
+	for (uint32_t c = threadIdx.x * 4; c < N; c += blockDim.x * 4)
+		*(f4*)(dst + c) = slab_sum((const f4*)(ep.wpart + (size_t)j0 * N + c), N / 4, j1 - j0);
+	if (threadIdx.x == 0) {
+		float l = 0.0f;
+		for (uint32_t j = j0; j < j1; ++j) l += ep.lpart[j];
+		dst[N] = l;
+	}
+	if (!arrive_last(ep.tail_counter, G, flag)) return;
+	const uint32_t nW0 = ep.W * ep.IN, nWh = (ep.NH - 1) * ep.W * ep.W;
+	for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) {
+		const float s = slab_sum(ep.group_slab + i, N + 4, G);
+		ep.buf.g32[i] = s;
+		const _Float16 h = adam_update(ep.adam_mlp, ep.buf, i, s);
+		uint32_t o;
+		if (i < nW0) {
+			o = (i / ep.IN) * ep.RSI + i % ep.IN;
+		} else if (i < nW0 + nWh) {
+			const uint32_t k = i - nW0;
+			o = ep.oWh + (k / ep.W) * ep.RSW + k % ep.W;  // rows of all hidden matrices are consecutive
+		} else {
+			const uint32_t k = i - nW0 - nWh;
+			o = ep.oWo + (k / ep.W) * ep.RSW + k % ep.W;
+		}
+		ep.wimage[o] = h;
+	}
+	if (threadIdx.x == 0) {
+		float l = 0.0f;
+		for (uint32_t k = 0; k < G; ++k) l += ep.group_slab[(size_t)k * (N + 4) + N];
+		*ep.d_loss = l;
+	}
+}
+
 template <uint32_t D, uint32_t F, HashType H>
 __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 	int layout, uint32_t B, const float* __restrict__ pos, uint32_t pstride, const _Float16* __restrict__ dLdy, uint32_t dy_stride,
 	const GridSlice* __restrict__ items, float* __restrict__ partial, uint32_t partial_stride,
-	const LevelInfo* __restrict__ levels, uint32_t hash_grid, uint32_t interp_u, uint32_t pts_per_chunk) {
+	const LevelInfo* __restrict__ levels, uint32_t hash_grid, uint32_t interp_u, uint32_t pts_per_chunk, uint32_t n_items,
+	uint32_t n_chunks, const GridBwdEpilogue ep) {
 	extern __shared__ __attribute__((aligned(16))) int acc[];
 	__shared__ float red[GRID_BWD_THREADS / 64];
-	const GridSlice it = items[blockIdx.x];
+	volatile uint32_t* flag = (volatile uint32_t*)&red[0];
+	if (blockIdx.x >= n_items * n_chunks) {
+		grid_bwd_mlp_tail(ep, blockIdx.x - n_items * n_chunks, flag);
+		return;
+	}
+	const uint32_t item = blockIdx.x % n_items, chunk = blockIdx.x / n_items;
+	const GridSlice it = items[item];
 	const LevelInfo li = levels[it.level];
 	const uint32_t len = it.end - it.begin;
 	const uint32_t nf = it.nf, f0 = it.f0;
 	const Interp interp = (Interp)interp_u;
 	for (uint32_t j = threadIdx.x; j < len * nf; j += blockDim.x) acc[j] = 0;
-	const uint32_t i0 = blockIdx.y * pts_per_chunk;
+	const uint32_t i0 = chunk * pts_per_chunk;
 	const uint32_t i1 = min(B, i0 + pts_per_chunk);
 
 	// pre-pass: max |dL/dy| of this item's features over the chunk -> fixed-point scale
@@ -324,7 +372,7 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 		grid_bwd_mode<D, F, H, IDX_GENERIC>(mode, layout, B, pos, pstride, dLdy, dy_stride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, i0, i1, scale, acc);
 	__syncthreads();
 	const float inv = ldexpf(1.0f, -e);
-	float* dst = partial + (size_t)blockIdx.y * partial_stride + (size_t)(li.offset + it.begin) * F + f0;
+	float* dst = partial + (size_t)chunk * partial_stride + (size_t)(li.offset + it.begin) * F + f0;
 	if (mode == 0) {  // decode the packed int32 pairs
 		const long long* a64 = (const long long*)acc;
 		for (uint32_t j = threadIdx.x; j < len; j += blockDim.x) {
@@ -340,38 +388,44 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 	}
 }
 
+struct GridBwdLaunch {
+	uint32_t n_items, n_chunks;
+	GridBwdEpilogue ep;
+};
+
 template <uint32_t D, uint32_t F, HashType H>
 static void grid_bwd_t(hipStream_t st, int layout, uint32_t dys, dim3 g, size_t lds, uint32_t B, const float* pos, uint32_t ps,
                        const _Float16* dy, const GridSlice* sl, float* part, uint32_t pstr, const LevelInfo* lv,
-                       uint32_t hg, uint32_t in, uint32_t ppc) {
+                       uint32_t hg, uint32_t in, uint32_t ppc, const GridBwdLaunch& gl) {
 	static bool attr = false;
 	if (!attr) {
 		TCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k_grid_bwd_lds<D, F, H>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GRID_BWD_LDS_BYTES));
 		attr = true;
 	}
-	hipLaunchKernelGGL((k_grid_bwd_lds<D, F, H>), g, dim3(GRID_BWD_THREADS), lds, st, layout, B, pos, ps, dy, dys, sl, part, pstr, lv, hg, in, ppc);
+	hipLaunchKernelGGL((k_grid_bwd_lds<D, F, H>), g, dim3(GRID_BWD_THREADS), lds, st, layout, B, pos, ps, dy, dys, sl, part, pstr, lv, hg, in, ppc,
+	                   gl.n_items, gl.n_chunks, gl.ep);
 }
 
 template <uint32_t D, uint32_t F>
 static void grid_bwd_h(hipStream_t st, HashType h, int pairs, uint32_t dys, dim3 g, size_t lds, uint32_t B, const float* pos, uint32_t ps,
                        const _Float16* dy, const GridSlice* sl, float* part, uint32_t pstr, const LevelInfo* lv,
-                       uint32_t hg, uint32_t in, uint32_t ppc) {
+                       uint32_t hg, uint32_t in, uint32_t ppc, const GridBwdLaunch& gl) {
 	switch (h) {
-		case HashType::Prime: grid_bwd_t<D, F, HashType::Prime>(st, pairs, dys, g, lds, B, pos, ps, dy, sl, part, pstr, lv, hg, in, ppc); break;
-		case HashType::ReversedPrime: grid_bwd_t<D, F, HashType::ReversedPrime>(st, pairs, dys, g, lds, B, pos, ps, dy, sl, part, pstr, lv, hg, in, ppc); break;
-		default: grid_bwd_t<D, F, HashType::CoherentPrime>(st, pairs, dys, g, lds, B, pos, ps, dy, sl, part, pstr, lv, hg, in, ppc); break;
+		case HashType::Prime: grid_bwd_t<D, F, HashType::Prime>(st, pairs, dys, g, lds, B, pos, ps, dy, sl, part, pstr, lv, hg, in, ppc, gl); break;
+		case HashType::ReversedPrime: grid_bwd_t<D, F, HashType::ReversedPrime>(st, pairs, dys, g, lds, B, pos, ps, dy, sl, part, pstr, lv, hg, in, ppc, gl); break;
+		default: grid_bwd_t<D, F, HashType::CoherentPrime>(st, pairs, dys, g, lds, B, pos, ps, dy, sl, part, pstr, lv, hg, in, ppc, gl); break;
 	}
 }
 
 template <uint32_t D>
 static void grid_bwd_f(hipStream_t st, uint32_t F, HashType h, int pairs, uint32_t dys, dim3 g, size_t lds, uint32_t B, const float* pos,
                        uint32_t ps, const _Float16* dy, const GridSlice* sl, float* part, uint32_t pstr, const LevelInfo* lv,
-                       uint32_t hg, uint32_t in, uint32_t ppc) {
+                       uint32_t hg, uint32_t in, uint32_t ppc, const GridBwdLaunch& gl) {
 	switch (F) {
-		case 1: grid_bwd_h<D, 1>(st, h, pairs, dys, g, lds, B, pos, ps, dy, sl, part, pstr, lv, hg, in, ppc); break;
-		case 2: grid_bwd_h<D, 2>(st, h, pairs, dys, g, lds, B, pos, ps, dy, sl, part, pstr, lv, hg, in, ppc); break;
-		case 4: grid_bwd_h<D, 4>(st, h, pairs, dys, g, lds, B, pos, ps, dy, sl, part, pstr, lv, hg, in, ppc); break;
-		case 8: grid_bwd_h<D, 8>(st, h, pairs, dys, g, lds, B, pos, ps, dy, sl, part, pstr, lv, hg, in, ppc); break;
+		case 1: grid_bwd_h<D, 1>(st, h, pairs, dys, g, lds, B, pos, ps, dy, sl, part, pstr, lv, hg, in, ppc, gl); break;
+		case 2: grid_bwd_h<D, 2>(st, h, pairs, dys, g, lds, B, pos, ps, dy, sl, part, pstr, lv, hg, in, ppc, gl); break;
+		case 4: grid_bwd_h<D, 4>(st, h, pairs, dys, g, lds, B, pos, ps, dy, sl, part, pstr, lv, hg, in, ppc, gl); break;
+		case 8: grid_bwd_h<D, 8>(st, h, pairs, dys, g, lds, B, pos, ps, dy, sl, part, pstr, lv, hg, in, ppc, gl); break;
 		default: throw std::runtime_error("GridEncoding: n_features_per_level must be 1, 2, 4 or 8");
 	}
 }
@@ -379,16 +433,22 @@ static void grid_bwd_f(hipStream_t st, uint32_t F, HashType h, int pairs, uint32
 void launch_grid_bwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_t B, const float* pos,
                      uint32_t pos_stride, const void* dLdy16, int dy_layout, uint32_t dy_stride, const GridSlice* slices,
                      uint32_t n_slices, uint32_t n_chunks, float* partial, uint32_t partial_stride,
-                     const LevelInfo* levels, bool hash_grid, Interp interp) {
+                     const LevelInfo* levels, bool hash_grid, Interp interp, const GridBwdEpilogue* ep) {
 	if (B == 0 || n_slices == 0) return;
 	const uint32_t ppc = div_round_up(B, n_chunks);
-	dim3 g(n_slices, n_chunks);
+	GridBwdLaunch gl{};
+	gl.n_items = n_slices;
+	gl.n_chunks = n_chunks;
+	if (ep) gl.ep = *ep;
+	else gl.ep.enabled = 0;
+	const uint32_t n_tail = (ep && ep->enabled) ? ep->n_mlp_groups : 0u;
+	dim3 g(n_slices * n_chunks + n_tail);
 	const size_t lds = GRID_BWD_LDS_BYTES;
 	const _Float16* dy = (const _Float16*)dLdy16;
 	switch (D) {
-		case 2: grid_bwd_f<2>(st, F, h, dy_layout, dy_stride, g, lds, B, pos, pos_stride, dy, slices, partial, partial_stride, levels, hash_grid, (uint32_t)interp, ppc); break;
-		case 3: grid_bwd_f<3>(st, F, h, dy_layout, dy_stride, g, lds, B, pos, pos_stride, dy, slices, partial, partial_stride, levels, hash_grid, (uint32_t)interp, ppc); break;
-		case 4: grid_bwd_f<4>(st, F, h, dy_layout, dy_stride, g, lds, B, pos, pos_stride, dy, slices, partial, partial_stride, levels, hash_grid, (uint32_t)interp, ppc); break;
+		case 2: grid_bwd_f<2>(st, F, h, dy_layout, dy_stride, g, lds, B, pos, pos_stride, dy, slices, partial, partial_stride, levels, hash_grid, (uint32_t)interp, ppc, gl); break;
+		case 3: grid_bwd_f<3>(st, F, h, dy_layout, dy_stride, g, lds, B, pos, pos_stride, dy, slices, partial, partial_stride, levels, hash_grid, (uint32_t)interp, ppc, gl); break;
+		case 4: grid_bwd_f<4>(st, F, h, dy_layout, dy_stride, g, lds, B, pos, pos_stride, dy, slices, partial, partial_stride, levels, hash_grid, (uint32_t)interp, ppc, gl); break;
 		default: throw std::runtime_error("GridEncoding: number of input dims must be 2, 3 or 4");
 	}
 	TCNN_HIP_CHECK(hipGetLastError());

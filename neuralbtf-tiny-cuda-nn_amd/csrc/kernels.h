@@ -29,6 +29,45 @@ struct AdamArgs {
 	float lr, beta1, beta2, eps, l2_reg, rel_decay, abs_decay, clip, nonmat_lr_factor;
 	float lower_lr_bound, upper_lr_bound;
 	int opt_matrix, opt_nonmatrix;
+	// parameter range [begin, n) of this launch; when part != nullptr the gradient of parameter i is
+	// the fixed-order sum of n_parts partial slabs part[j * part_stride + (i - begin)] (written back
+	// to grad32[i]) instead of grad32[i] (reduction fused into the optimizer)
+	uint32_t begin;
+	const float* part;
+	uint32_t n_parts, part_stride;
+};
+
+// Optimizer state buffers (full parameter vector [network | encoding]).
+struct AdamBuffers {
+	float* w32;
+	_Float16* w16;
+	float* g32;      // fp32 gradient sums (written by fused-reduction epilogues)
+	_Float16* g16;   // fp16 gradients (reference m_param_gradients)
+	float* m1;
+	float* m2;
+	uint32_t* steps;
+};
+
+// Work carried by the grid backward launch (single-GPU trainer step): n_mlp_groups extra
+// workgroups, on CUs the grid items leave free, reduce the fused kernel's network-gradient slabs and
+// loss partials; the last of them runs Adam on the network parameters and writes the next step's
+// fused weight image. The counter must be zero before the first launch.
+struct GridBwdEpilogue {
+	int enabled;
+	AdamArgs adam_mlp;       // range [0, n_mlp)
+	AdamBuffers buf;
+	// network-gradient tail
+	uint32_t n_mlp_groups;   // extra workgroups (0 = none)
+	const float* wpart;      // fused kernel slabs [n_wparts][n_mlp]
+	uint32_t n_wparts, n_mlp;
+	const float* lpart;      // loss partials [n_wparts]
+	float* group_slab;       // scratch [n_mlp_groups][n_mlp + 4]
+	uint32_t* tail_counter;
+	float* d_loss;
+	// fused weight image (mlp_fused.h FusedLayout): W0 rows of RSI halves at 0, hidden rows of RSW
+	// at oWh, output rows of RSW at oWo
+	_Float16* wimage;
+	uint32_t W, IN, NH, RSI, RSW, oWh, oWo;
 };
 
 // Fused train step (grid encoding -> MLP fwd -> RelativeL2 -> MLP bwd -> dW partials, dL/denc).
@@ -65,7 +104,9 @@ uint32_t grid_bwd_slot_budget();
 void launch_grid_bwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_t B, const float* pos,
                      uint32_t pos_stride, const void* dLdy16, int dy_layout, uint32_t dy_stride, const GridSlice* slices,
                      uint32_t n_slices, uint32_t n_chunks, float* partial, uint32_t partial_stride,
-                     const LevelInfo* levels, bool hash_grid, Interp interp);
+                     const LevelInfo* levels, bool hash_grid, Interp interp, const GridBwdEpilogue* ep = nullptr);
+// fused weight-image geometry (FusedLayout) for the epilogue
+void fused_image_layout(uint32_t W, uint32_t IN, uint32_t NH, uint32_t* RSI, uint32_t* RSW, uint32_t* oWh, uint32_t* oWo);
 
 // out[p] = sum_j in[j*stride + p] (p < n), optional fp16 copy
 void launch_reduce_partials(hipStream_t st, const float* in, uint32_t n_parts, uint32_t stride, uint32_t n,

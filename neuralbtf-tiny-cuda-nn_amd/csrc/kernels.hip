@@ -6,6 +6,7 @@
 //   k_relative_l2       standalone RelativeL2 (reference losses/relative_l2.h:40-76)
 #include "kernels.h"
 
+#include "adam_device.h"
 #include "grid_device.h"
 #include "mlp_fused.h"
 
@@ -25,12 +26,12 @@ __global__ __launch_bounds__(256) void k_reduce_groups(const float* __restrict__
 	float* dst = out + (size_t)blockIdx.y * out_stride;
 	if (p4 + 4 <= n && (stride % 4) == 0 && (out_stride % 4) == 0) {
 		f4 s = {0.0f, 0.0f, 0.0f, 0.0f};
-		for (uint32_t j = j0; j < j1; ++j) s += *(const f4*)(in + (size_t)j * stride + p4);
+		s = slab_sum((const f4*)(in + (size_t)j0 * stride + p4), stride / 4, j1 - j0);
 		*(f4*)(dst + p4) = s;
 	} else {
 		for (uint32_t p = p4; p < n && p < p4 + 4; ++p) {
 			float s = 0.0f;
-			for (uint32_t j = j0; j < j1; ++j) s += in[(size_t)j * stride + p];
+			s = slab_sum(in + (size_t)j0 * stride + p, stride, j1 - j0);
 			dst[p] = s;
 		}
 	}
@@ -56,44 +57,29 @@ void launch_reduce_partials(hipStream_t st, const float* in, uint32_t n_parts, u
 	TCNN_HIP_CHECK(hipGetLastError());
 }
 
-// reference optimizers/adam.h:47-119; the fp32 gradient sum is rounded to fp16 first because the
-// reference's gradient buffer is __half (trainer.h:327).
+// reference optimizers/adam.h:47-119 (per-parameter update in adam_device.h)
 __global__ __launch_bounds__(256) void k_adam(const AdamArgs a, float* __restrict__ w32, _Float16* __restrict__ w16,
                                                const float* __restrict__ grad32, _Float16* __restrict__ grad16,
                                                float* __restrict__ m1, float* __restrict__ m2, uint32_t* __restrict__ steps) {
-	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	const uint32_t i = a.begin + blockIdx.x * blockDim.x + threadIdx.x;
 	if (i >= a.n) return;
-	const _Float16 g16 = (_Float16)(grad32[i] * a.grad_scale);
-	if (grad16) grad16[i] = g16;
-	float gradient = (float)g16 / a.loss_scale;
-	if (i >= a.n_matrix) {
-		if (!a.opt_nonmatrix || gradient == 0.0f) return;
+	float gsum;
+	if (a.part) {
+		gsum = slab_sum(a.part + (i - a.begin), a.part_stride, a.n_parts);
+		((float*)grad32)[i] = gsum;
 	} else {
-		if (!a.opt_matrix) return;
+		gsum = grad32[i];
 	}
-	const float wfp = w32[i];
-	if (i < a.n_matrix) gradient = __builtin_fmaf(a.l2_reg, wfp, gradient);
-	const float gsq = gradient * gradient;
-	const float mm1 = __builtin_fmaf(a.beta1, m1[i], (1.0f - a.beta1) * gradient);
-	const float mm2 = __builtin_fmaf(a.beta2, m2[i], (1.0f - a.beta2) * gsq);
-	m1[i] = mm1;
-	m2[i] = mm2;
-	float lr = a.lr;
-	if (i >= a.n_matrix) lr *= a.nonmat_lr_factor;
-	const uint32_t st = ++steps[i];
-	lr *= sqrtf(1.0f - powf(a.beta2, (float)st)) / (1.0f - powf(a.beta1, (float)st));
-	const float eff = fminf(fmaxf(lr / (sqrtf(mm2) + a.eps), a.lower_lr_bound), a.upper_lr_bound);
-	const float decayed = __builtin_fmaf(1.0f - a.rel_decay * lr, wfp, -copysignf(a.abs_decay * lr, wfp));
-	float nw = __builtin_fmaf(-eff, mm1, decayed);
-	if (a.clip != 0.0f) nw = fminf(fmaxf(nw, -a.clip), a.clip);
-	w32[i] = nw;
-	w16[i] = (_Float16)nw;
+	const AdamBuffers s{w32, w16, (float*)grad32, grad16, m1, m2, steps};
+	adam_update(a, s, i, gsum);
 }
 
 void launch_adam(hipStream_t st, const AdamArgs& a, float* w32, void* w16, const float* grad32, void* grad16,
                  float* m1, float* m2, uint32_t* steps) {
-	if (a.n == 0) return;
-	hipLaunchKernelGGL(k_adam, dim3(div_round_up(a.n, 256)), dim3(256), 0, st, a, w32, (_Float16*)w16, grad32, (_Float16*)grad16, m1, m2, steps);
+	if (a.n <= a.begin) return;
+	// one parameter per thread: measured faster than 4-wide vector access (16.7 vs 19.5 us for the
+	// config_hash grid range with 8 slabs) -- 4x the waves in flight for the slab loads
+	hipLaunchKernelGGL(k_adam, dim3(div_round_up(a.n - a.begin, 256)), dim3(256), 0, st, a, w32, (_Float16*)w16, grad32, (_Float16*)grad16, m1, m2, steps);
 	TCNN_HIP_CHECK(hipGetLastError());
 }
 

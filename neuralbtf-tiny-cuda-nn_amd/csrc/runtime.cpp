@@ -451,9 +451,14 @@ void NetworkHost::fwd_bwd(hipStream_t st, StepWorkspace& ws, uint32_t B, const f
 	else fwd_bwd_layered(st, ws, B, pos, target, dims, loss_scale, params16, dout16, out16, grad32, mark, dL_dinput);
 }
 
-void NetworkHost::fwd_bwd_fused(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target,
-                                uint32_t dims, float loss_scale, const void* params16, const void* dout16, void* out16, float* grad32,
-                                const std::function<void(int)>& mark) {
+void NetworkHost::pack_weights(hipStream_t st, StepWorkspace& ws, const void* params16) {
+	ws.wimage.reserve(fused_weight_image_bytes(mlp.width, mlp.n_input, mlp.n_hidden_layers));
+	launch_pack_weights(st, mlp.width, mlp.n_input, mlp.n_hidden_layers, params16, ws.wimage.p);
+	ws.wimage_valid = true;
+}
+
+void NetworkHost::fused_kernel(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target, uint32_t dims,
+                               float loss_scale, const void* params16, bool pack, const void* dout16, void* out16) {
 	TCNN_CHECK(B % 32 == 0, "training: batch must be a multiple of 32");
 	const uint32_t n_mlp = mlp.n_params();
 	const uint32_t L = grid->desc.n_levels, F = grid->desc.n_features_per_level;
@@ -464,27 +469,53 @@ void NetworkHost::fwd_bwd_fused(hipStream_t st, StepWorkspace& ws, uint32_t B, c
 	ws.dLdenc.reserve((size_t)L * F * B * 2);
 	ws.wgrad_partial.reserve((size_t)nb * n_mlp * 4);
 	ws.loss_partial.reserve((size_t)nb * 4);
-	const uint32_t n_slices = (uint32_t)grid->slices.size();
-	const uint32_t n_chunks = grid->bwd_chunks(B);
-	ws.n_grid_chunks = n_chunks;
-	ws.grid_partial.reserve((size_t)n_chunks * grid->n_params * 4);
-
+	if (pack || !ws.wimage_valid) pack_weights(st, ws, params16);
 	const uint8_t* table = (const uint8_t*)params16 + (size_t)n_mlp * 2;
-	ws.wimage.reserve(fused_weight_image_bytes(mlp.width, mlp.n_input, mlp.n_hidden_layers));
-	launch_pack_weights(st, mlp.width, mlp.n_input, mlp.n_hidden_layers, params16, ws.wimage.p);
 	launch_fused_train(st, mlp.width, mlp.n_input, mlp.n_hidden_layers, grid->desc.n_pos_dims, grid->desc.hash_type,
 	                   mlp.activation, B, dims, loss_scale, params16, table, pos, target, out16, ws.dLdenc.p,
 	                   ws.wgrad_partial.as<float>(), ws.loss_partial.as<float>(), grid->dev_levels(), grid->hash_grid(),
 	                   grid->desc.interp, nb, dout16, ws.wimage.p);
+}
+
+void NetworkHost::grid_backward(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, GridBwdEpilogue* ep) {
+	const uint32_t n_slices = (uint32_t)grid->slices.size();
+	const uint32_t n_chunks = grid->bwd_chunks(B, ep ? ep->n_mlp_groups : 0u);
+	ws.n_grid_chunks = n_chunks;
+	ws.grid_partial.reserve((size_t)n_chunks * grid->n_params * 4);
+	if (ep) {
+		if (ws.counters.bytes < 64) {
+			ws.counters.reserve(64);
+			TCNN_HIP_CHECK(hipMemset(ws.counters.p, 0, ws.counters.bytes));
+		}
+		ep->tail_counter = ws.counters.as<uint32_t>();
+		ws.group_slab.reserve((size_t)ep->n_mlp_groups * (ep->n_mlp + 4) * 4);
+		ep->group_slab = ws.group_slab.as<float>();
+		ep->wimage = ws.wimage.as<_Float16>();
+		ep->W = mlp.width;
+		ep->IN = mlp.n_input;
+		ep->NH = mlp.n_hidden_layers;
+		fused_image_layout(mlp.width, mlp.n_input, mlp.n_hidden_layers, &ep->RSI, &ep->RSW, &ep->oWh, &ep->oWo);
+		ep->wpart = ws.wgrad_partial.as<float>();
+		ep->n_wparts = ws.n_fused_blocks;
+		ep->lpart = ws.loss_partial.as<float>();
+	}
+	launch_grid_bwd(st, grid->desc.n_pos_dims, grid->desc.n_features_per_level, grid->desc.hash_type, B, pos, grid->desc.n_pos_dims,
+	                ws.dLdenc.p, 0, 0, grid->d_slices.as<GridSlice>(), n_slices, n_chunks, ws.grid_partial.as<float>(),
+	                grid->n_params, grid->dev_levels(), grid->hash_grid(), grid->desc.interp, ep);
+	if (ep) ws.wimage_valid = true;  // the epilogue wrote the image of the updated weights
+}
+
+void NetworkHost::fwd_bwd_fused(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target,
+                                uint32_t dims, float loss_scale, const void* params16, const void* dout16, void* out16, float* grad32,
+                                const std::function<void(int)>& mark) {
+	const uint32_t n_mlp = mlp.n_params();
+	fused_kernel(st, ws, B, pos, target, dims, loss_scale, params16, true, dout16, out16);
 	if (mark) mark(1);
-	launch_reduce_partials(st, ws.wgrad_partial.as<float>(), nb, n_mlp, n_mlp, grad32);
+	grid_backward(st, ws, B, pos);
 	if (mark) mark(2);
-	launch_grid_bwd(st, grid->desc.n_pos_dims, F, grid->desc.hash_type, B, pos, grid->desc.n_pos_dims, ws.dLdenc.p, 0, 0,
-	                grid->d_slices.as<GridSlice>(), n_slices, n_chunks, ws.grid_partial.as<float>(), grid->n_params,
-	                grid->dev_levels(), grid->hash_grid(), grid->desc.interp);
+	launch_reduce_partials(st, ws.wgrad_partial.as<float>(), ws.n_fused_blocks, n_mlp, n_mlp, grad32);
+	launch_reduce_partials(st, ws.grid_partial.as<float>(), ws.n_grid_chunks, grid->n_params, grid->n_params, grad32 + n_mlp);
 	if (mark) mark(3);
-	launch_reduce_partials(st, ws.grid_partial.as<float>(), n_chunks, grid->n_params, grid->n_params, grad32 + n_mlp);
-	if (mark) mark(4);
 }
 
 // Layer-wise training pass (reference FullyFusedMLP::forward_impl/backward_impl dataflow,
@@ -524,7 +555,6 @@ void NetworkHost::fwd_bwd_layered(hipStream_t st, StepWorkspace& ws, uint32_t B,
 		ws.n_loss_partials = nl;
 	}
 	launch_act_bwd_inplace(st, B * OUTP, mlp.output_activation, out, ws.dout16.p);
-	if (mark) mark(1);
 
 	// backward: weight offsets [W0 | W1..W_{NH-1} | Wout]
 	auto w_off = [&](uint32_t j) -> size_t { return j == 0 ? 0 : (size_t)W * IN + (size_t)(j - 1) * W * W; };
@@ -543,14 +573,13 @@ void NetworkHost::fwd_bwd_layered(hipStream_t st, StepWorkspace& ws, uint32_t B,
 		std::swap(dcur, dnext);
 	}
 	wgrad(W, IN, dcur, ws.enc16.p, 0);
-	if (mark) mark(2);
+	if (mark) mark(1);
 	const bool enc_grad = enc->n_params() > 0 || dL_dinput;
 	if (enc_grad) {
 		// dL/d(encoding) = W0^T delta_0 (no transfer), AoS [B][IN]
 		launch_layer_bwd(st, B, W, IN, p16, dcur, nullptr, dnext, ACT_NONE);
 		if (dL_dinput) enc->backward_input(st, B, pos, dnext, dL_dinput);
 	}
-	if (mark) mark(3);
 	if (grid) {
 		const uint32_t n_chunks = grid->bwd_chunks(B);
 		ws.n_grid_chunks = n_chunks;
@@ -560,7 +589,8 @@ void NetworkHost::fwd_bwd_layered(hipStream_t st, StepWorkspace& ws, uint32_t B,
 		                ws.grid_partial.as<float>(), grid->n_params, grid->dev_levels(), grid->hash_grid(), grid->desc.interp);
 		launch_reduce_partials(st, ws.grid_partial.as<float>(), n_chunks, grid->n_params, grid->n_params, grad32 + n_mlp);
 	}
-	if (mark) mark(4);
+	if (mark) mark(2);
+	if (mark) mark(3);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -609,25 +639,69 @@ void TrainerHost::initialize_params(uint32_t seed) {
 	launch_cast_f32_f16(nullptr, w32.as<float>(), w16.p, n_params);
 	TCNN_HIP_CHECK(hipDeviceSynchronize());
 	adam_step = 0;
+	ws.wimage_valid = false;
 }
 
 void TrainerHost::set_params_full_precision(const float* host, uint64_t n) {
 	TCNN_CHECK(n == n_params, "Can't set fp params because buffer has the wrong size.");
 	TCNN_HIP_CHECK(hipMemcpy(w32.p, host, n * 4, hipMemcpyHostToDevice));
 	launch_cast_f32_f16(nullptr, w32.as<float>(), w16.p, n_params);
+	ws.wimage_valid = false;
 	TCNN_HIP_CHECK(hipDeviceSynchronize());
 }
 
 void TrainerHost::training_step(hipStream_t st, uint32_t B, const float* input, const float* target, bool run_optimizer) {
 	TCNN_CHECK(B % BATCH_GRANULARITY == 0, "training_step: batch size must be a multiple of 256");
-	if (timer.enabled) timer.marks.push_back({-1, -1, -1, -1, -1, -1, -1});
+	if (timer.enabled) {
+		timer.sampling = (timer.counter++ % timer.every) == 0;
+		if (timer.sampling) timer.marks.push_back({-1, -1, -1, -1, -1});
+	}
+	if (run_optimizer && overlapped_ok()) {
+		training_step_overlapped(st, B, input, target);
+		return;
+	}
 	mark(st, 0);
 	model->fwd_bwd(st, ws, B, input, target, n_output_dims, loss_scale, w16.p, nullptr, nullptr, g32.as<float>(),
 	               [&](int ph) { mark(st, ph); });
 	launch_sum(st, ws.loss_partial.as<float>(), ws.n_loss_partials, d_loss.as<float>());
-	mark(st, 5);
+	mark(st, 4);
 	last_B = B;
 	if (run_optimizer) optimizer_step(st);
+}
+
+
+// Single-GPU training step in three launches on one stream (the reference's step is ~10 kernels plus
+// side streams, trainer.h:163-190): the fused grid+MLP kernel; the grid backward, whose 16 extra
+// workgroups (on CUs the grid items leave free) reduce the fused kernel's network-gradient slabs
+// and the loss, run Adam on the network and write the next step's weight image; Adam over the grid
+// parameters summing the grid backward's chunk slabs on the fly. Summation orders equal the
+// sequential path's (bit-identical parameters).
+void TrainerHost::training_step_overlapped(hipStream_t st, uint32_t B, const float* input, const float* target) {
+	NetworkHost& m = *model;
+	mark(st, 0);
+	m.fused_kernel(st, ws, B, input, target, n_output_dims, loss_scale, w16.p, false);
+	mark(st, 1);
+	++adam_step;
+	GridBwdEpilogue ep{};
+	ep.enabled = 1;
+	ep.adam_mlp = adam_args();
+	ep.adam_mlp.n = (uint32_t)n_mlp;
+	ep.buf = AdamBuffers{w32.as<float>(), w16.as<_Float16>(), g32.as<float>(), g16.as<_Float16>(), m1.as<float>(), m2.as<float>(),
+	                     steps.as<uint32_t>()};
+	ep.n_mlp_groups = 16;
+	ep.n_mlp = (uint32_t)n_mlp;
+	ep.d_loss = d_loss.as<float>();
+	TCNN_CHECK(n_mlp % 4 == 0, "network parameter count must be a multiple of 4");
+	m.grid_backward(st, ws, B, input, &ep);
+	mark(st, 2);
+	AdamArgs ag = adam_args();
+	ag.begin = (uint32_t)n_mlp;
+	ag.part = ws.grid_partial.as<float>();
+	ag.n_parts = ws.n_grid_chunks;
+	ag.part_stride = m.grid->n_params;
+	launch_adam(st, ag, w32.as<float>(), w16.p, g32.as<float>(), g16.p, m1.as<float>(), m2.as<float>(), steps.as<uint32_t>());
+	mark(st, 3);
+	last_B = B;
 }
 
 hipEvent_t PhaseTimer::get() {
@@ -644,7 +718,7 @@ PhaseTimer::~PhaseTimer() {
 }
 
 void TrainerHost::mark(hipStream_t st, int phase) {
-	if (!timer.enabled || timer.marks.empty()) return;
+	if (!timer.enabled || !timer.sampling || timer.marks.empty()) return;
 	const int idx = (int)timer.next;
 	TCNN_HIP_CHECK(hipEventRecord(timer.get(), st));
 	timer.marks.back()[phase] = idx;
@@ -654,29 +728,24 @@ void TrainerHost::profile_end(double* ms, uint32_t n_phases, uint32_t* n_steps) 
 	TCNN_HIP_CHECK(hipDeviceSynchronize());
 	const uint32_t P = std::min<uint32_t>(n_phases, PhaseTimer::N_PHASES);
 	for (uint32_t p = 0; p < n_phases; ++p) ms[p] = 0.0;
-	uint32_t counted = 0;
+	std::vector<uint32_t> cnt(P, 0);
 	for (auto& m : timer.marks) {
-		bool ok = true;
 		for (uint32_t p = 0; p < P; ++p) {
-			if (m[p] < 0 || m[p + 1] < 0) { ok = false; break; }
-		}
-		if (!ok) continue;
-		for (uint32_t p = 0; p < P; ++p) {
+			if (m[p] < 0 || m[p + 1] < 0) continue;
 			float t = 0.0f;
 			TCNN_HIP_CHECK(hipEventElapsedTime(&t, timer.pool[m[p]], timer.pool[m[p + 1]]));
 			ms[p] += t;
+			++cnt[p];
 		}
-		++counted;
 	}
-	if (counted)
-		for (uint32_t p = 0; p < P; ++p) ms[p] /= counted;
-	if (n_steps) *n_steps = counted;
+	for (uint32_t p = 0; p < P; ++p)
+		if (cnt[p]) ms[p] /= cnt[p];
+	if (n_steps) *n_steps = P ? cnt[0] : 0;
 	timer.enabled = false;
 	timer.reset();
 }
 
-void TrainerHost::optimizer_step(hipStream_t st) {  // AdamOptimizer::step, adam.h:150-188
-	++adam_step;
+AdamArgs TrainerHost::adam_args() const {
 	AdamArgs a{};
 	a.n = (uint32_t)n_params;
 	a.n_matrix = (uint32_t)n_mlp;  // layer_sizes() of the network only (grid.h:1084-1088)
@@ -699,8 +768,14 @@ void TrainerHost::optimizer_step(hipStream_t st) {  // AdamOptimizer::step, adam
 	}
 	a.opt_matrix = adam.optimize_matrix_params;
 	a.opt_nonmatrix = adam.optimize_non_matrix_params;
+	return a;
+}
+
+void TrainerHost::optimizer_step(hipStream_t st) {  // AdamOptimizer::step, adam.h:150-188
+	++adam_step;
+	const AdamArgs a = adam_args();
 	launch_adam(st, a, w32.as<float>(), w16.p, g32.as<float>(), g16.p, m1.as<float>(), m2.as<float>(), steps.as<uint32_t>());
-	mark(st, 6);
+	ws.wimage_valid = false;
 }
 
 float TrainerHost::loss(hipStream_t st) {

@@ -6,6 +6,7 @@
 #include <json.hpp>
 
 #include <array>
+#include <cstdlib>
 #include <functional>
 #include <memory>
 #include <string>
@@ -64,9 +65,16 @@ struct GridEncodingHost {
 	void initialize_params(Pcg32& rng, float* host_out, float scale = 1.0f) const;
 	json hyperparams() const;
 	const LevelInfo* dev_levels() const { return d_levels.as<LevelInfo>(); }
-	// point chunks of the backward: ~one 1024-thread workgroup per CU in total, >= 4096 points each
-	uint32_t bwd_chunks(uint32_t B) const {
-		uint32_t c = std::max(1u, (256u + (uint32_t)slices.size() / 2) / (uint32_t)slices.size());
+	// point chunks of the backward: items x chunks workgroups of 1024 threads (one per CU: 128 KiB
+	// of LDS each) fit the CUs left after `reserved` other workgroups in ONE round, with one chunk of
+	// slack (config_hash, 26 items + 16 tail workgroups: 7 / 8 / 9 / 10 chunks -> 68.8 / 65.8 /
+	// 67.5 / 109 us, the last spilling into a second round); >= 4096 points each
+	uint32_t bwd_chunks(uint32_t B, uint32_t reserved = 0) const {
+		const uint32_t n_cu = 256;
+		const uint32_t fit = (n_cu > reserved ? n_cu - reserved : 1u) / (uint32_t)slices.size();
+		uint32_t c = std::max(1u, fit > 2 ? fit - 1 : fit);
+		if (const char* e = std::getenv("TCNN_GRID_BWD_CHUNKS"))  // tuning override
+			if (std::atoi(e) > 0) c = (uint32_t)std::atoi(e);
 		return std::max(1u, std::min(c, B / 4096));
 	}
 };
@@ -122,6 +130,8 @@ struct StepWorkspace {
 	DevBuf dLdenc, wgrad_partial, loss_partial, grid_partial, grad32_tmp, out16, enc16, wimage;
 	DevBuf acts, delta0, delta1, dout16;  // layer-wise engine
 	uint32_t n_fused_blocks = 0, n_grid_chunks = 0, n_loss_partials = 0;
+	bool wimage_valid = false;  // fused weight image matches the current fp16 params (trainer fast path)
+	DevBuf counters, group_slab;  // grid-backward epilogue: hand-off counters (zeroed once), network-gradient group sums
 };
 
 // NetworkWithInputEncoding<__half> (reference network_with_input_encoding.h:41-190) over two engines:
@@ -151,6 +161,12 @@ struct NetworkHost {
 	             const std::function<void(int)>& mark = nullptr, float* dL_dinput = nullptr);
 	json hyperparams() const;
 
+	// pieces of the fused engine for the trainer's overlapped step
+	void fused_kernel(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target, uint32_t dims,
+	                  float loss_scale, const void* params16, bool pack, const void* dout16 = nullptr, void* out16 = nullptr);
+	void grid_backward(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, GridBwdEpilogue* ep = nullptr);
+	void pack_weights(hipStream_t st, StepWorkspace& ws, const void* params16);
+
 private:
 	void fwd_bwd_fused(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target, uint32_t dims,
 	                   float loss_scale, const void* params16, const void* dout16, void* out16, float* grad32,
@@ -163,9 +179,15 @@ private:
 };
 
 // Per-phase hipEvent timing of the training step (bench.py's live per-kernel roofline source).
+// Phases on the trainer's stream: [0] fused grid+MLP kernel (fwd, loss, bwd, dW), [1] grid backward
+// (two-launch step: with the reduction + Adam epilogue), [2] reductions, [3] loss sum / optimizer
+// (sequential path only; phases a step does not have are skipped). Events are recorded
+// only on every `every`-th step (each record is a barrier packet that idles the GPU for a few us).
 struct PhaseTimer {
-	static constexpr int N_PHASES = 6;  // fused fwd/bwd, wgrad reduce, grid bwd, grid reduce, loss sum, adam
+	static constexpr int N_PHASES = 4;
 	bool enabled = false;
+	uint32_t every = 1, counter = 0;
+	bool sampling = false;  // this step records events
 	std::vector<hipEvent_t> pool;
 	std::vector<std::array<int, N_PHASES + 1>> marks;  // event indices per step (-1 = not recorded)
 	size_t next = 0;
@@ -188,6 +210,10 @@ struct TrainerHost {
 	float grad_scale = 1.0f;
 	float loss_scale = 128.0f;  // default_loss_scale<__half> (common.h:232)
 	uint32_t last_B = 0;
+	// two-launch single-GPU step: reductions + Adam fused into the grid backward's epilogue
+	bool overlapped_ok() const { return model->fused_ok(); }
+	void training_step_overlapped(hipStream_t st, uint32_t B, const float* input, const float* target);
+	AdamArgs adam_args() const;
 
 	TrainerHost(uint32_t n_in, uint32_t n_out, const json& cfg, uint32_t seed);
 	void initialize_params(uint32_t seed);

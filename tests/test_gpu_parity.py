@@ -180,3 +180,24 @@ def test_trainer_buffer_views_alias_device_memory(torch_mod):
     g.mul_(2.0)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(trainer_arrays(t)["g32"], a["g32"] * 2.0)
+
+
+def test_overlapped_step_bit_identical_to_sequential(torch_mod):
+    """The single-GPU two-launch step (reductions + Adam in the grid backward's epilogue) gives
+    bit-identical parameters to training_step(run_optimizer=False) + optimizer_step(); the loss
+    sum differs only in summation order."""
+    torch = torch_mod
+    from tinycudann import Trainer
+    ta = Trainer(2, 3, CONFIG_HASH, seed=1337)
+    tb = Trainer(2, 3, CONFIG_HASH, seed=1337)
+    for s in range(4):
+        pos, tgt = make_batch(4096, step=s)
+        p, t = torch.from_numpy(pos).cuda(), torch.from_numpy(tgt).cuda()
+        ta.training_step(p, t, run_optimizer=True)
+        tb.training_step(p, t, run_optimizer=False)
+        tb.optimizer_step()
+        assert abs(ta.loss() - tb.loss()) <= 1e-6 * abs(tb.loss())
+    a, b = trainer_arrays(ta), trainer_arrays(tb)
+    np.testing.assert_array_equal(a["w32"], b["w32"])
+    np.testing.assert_array_equal(a["w16"], b["w16"])
+    np.testing.assert_array_equal(a["g16"], b["g16"])
