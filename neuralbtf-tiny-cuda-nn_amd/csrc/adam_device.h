@@ -8,12 +8,17 @@
 
 namespace tcnn_amd {
 
+__device__ __forceinline__ float adam_bias_factor(const AdamArgs& a, uint32_t st) {
+	return sqrtf(1.0f - powf(a.beta2, (float)st)) / (1.0f - powf(a.beta1, (float)st));
+}
+
 // Adam on register values of parameter i (fp32 gradient sum gsum); returns false when the
 // parameter is skipped (reference adam.h:75-82: frozen class, or a zero non-matrix gradient).
 __device__ __forceinline__ bool adam_core(const AdamArgs& a, uint32_t i, float gsum, _Float16& g16, float& w, float& m1, float& m2,
                                           uint32_t& step) {
 	g16 = (_Float16)(gsum * a.grad_scale);
-	float gradient = (float)g16 / a.loss_scale;
+	// x / 2^k is exact, so a power-of-two loss scale (128) becomes a multiply
+	float gradient = a.inv_loss_scale != 0.0f ? (float)g16 * a.inv_loss_scale : (float)g16 / a.loss_scale;
 	if (i >= a.n_matrix) {
 		if (!a.opt_nonmatrix || gradient == 0.0f) return false;
 	} else {
@@ -27,7 +32,7 @@ __device__ __forceinline__ bool adam_core(const AdamArgs& a, uint32_t i, float g
 	float lr = a.lr;
 	if (i >= a.n_matrix) lr *= a.nonmat_lr_factor;
 	const uint32_t st = ++step;
-	lr *= sqrtf(1.0f - powf(a.beta2, (float)st)) / (1.0f - powf(a.beta1, (float)st));
+	lr *= (a.cached_factor && st == a.cached_step) ? *a.cached_factor : adam_bias_factor(a, st);
 	const float eff = fminf(fmaxf(lr / (sqrtf(m2) + a.eps), a.lower_lr_bound), a.upper_lr_bound);
 	const float decayed = __builtin_fmaf(1.0f - a.rel_decay * lr, wfp, -copysignf(a.abs_decay * lr, wfp));
 	float nw = __builtin_fmaf(-eff, m1, decayed);

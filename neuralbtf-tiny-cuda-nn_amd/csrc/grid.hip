@@ -284,6 +284,7 @@ __device__ void grid_bwd_mlp_tail(const GridBwdEpilogue& ep, uint32_t g, volatil
 		dst[N] = l;
 	}
 	if (!arrive_last(ep.tail_counter, G, flag)) return;
+	if (threadIdx.x == 0 && ep.factor_out) *ep.factor_out = adam_bias_factor(ep.adam_mlp, ep.factor_step);
 	const uint32_t nW0 = ep.W * ep.IN, nWh = (ep.NH - 1) * ep.W * ep.W;
 	for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) {
 		const float s = slab_sum(ep.group_slab + i, N + 4, G);

@@ -29,12 +29,17 @@ struct AdamArgs {
 	float lr, beta1, beta2, eps, l2_reg, rel_decay, abs_decay, clip, nonmat_lr_factor;
 	float lower_lr_bound, upper_lr_bound;
 	int opt_matrix, opt_nonmatrix;
+	float inv_loss_scale;  // 1 / loss_scale when that is exact (power of two), else 0
 	// parameter range [begin, n) of this launch; when part != nullptr the gradient of parameter i is
 	// the fixed-order sum of n_parts partial slabs part[j * part_stride + (i - begin)] (written back
 	// to grad32[i]) instead of grad32[i] (reduction fused into the optimizer)
 	uint32_t begin;
 	const float* part;
 	uint32_t n_parts, part_stride;
+	// bias-correction factor sqrt(1 - beta2^t) / (1 - beta1^t) precomputed on the device for
+	// t == cached_step (nullptr: always computed per parameter; same device arithmetic either way)
+	const float* cached_factor;
+	uint32_t cached_step;
 };
 
 // Optimizer state buffers (full parameter vector [network | encoding]).
@@ -64,6 +69,8 @@ struct GridBwdEpilogue {
 	float* group_slab;       // scratch [n_mlp_groups][n_mlp + 4]
 	uint32_t* tail_counter;
 	float* d_loss;
+	float* factor_out;       // receives the bias-correction factor of step adam_mlp's current step
+	uint32_t factor_step;
 	// fused weight image (mlp_fused.h FusedLayout): W0 rows of RSI halves at 0, hidden rows of RSW
 	// at oWh, output rows of RSW at oWo
 	_Float16* wimage;

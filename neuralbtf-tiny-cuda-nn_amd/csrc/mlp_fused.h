@@ -495,6 +495,17 @@ __global__ __launch_bounds__(256, 2) void k_fused_train_grid(const FusedTrainArg
 		const uint32_t base = chunk * 32;
 		h4 xt[2][NTI];
 		h4 Gext[2];
+		float tg[2][4];  // this lane's targets (outputs 4q .. 4q+3 < dims), loaded up front so the
+		                 // loss does not wait on them
+#pragma unroll
+		for (int tau = 0; tau < 2; ++tau) {
+			const uint32_t i = base + 16 * tau + c;
+#pragma unroll
+			for (int r = 0; r < 4; ++r) {
+				const uint32_t o = 4 * q + r;
+				tg[tau][r] = (!EXT_DOUT && o < a.dims) ? a.target[(size_t)i * a.dims + o] : 0.0f;
+			}
+		}
 #pragma unroll
 		for (int tau = 0; tau < 2; ++tau) {
 			const uint32_t i = base + 16 * tau + c;
@@ -514,7 +525,7 @@ __global__ __launch_bounds__(256, 2) void k_fused_train_grid(const FusedTrainArg
 			}
 		}
 		if constexpr (PROF) { t1 = stamp(); ph[0] += t1 - t0; t0 = t1; }
-		auto target = [&](int tau, uint32_t o) { return a.target[(size_t)(base + 16 * tau + c) * a.dims + o]; };
+		auto target = [&](int tau, uint32_t o) { return tg[tau][o & 3]; };
 		auto after_loss = [] {};
 		fused_slice<W, IN, NH, ACT, EXT_DOUT, PROF>(a, base, c, q, xt, target, after_loss, Gext, smem + L::oW0,
 		                                            smem + L::oWh, smem + L::oWo, bufA, bufD, acc, ph, t0);

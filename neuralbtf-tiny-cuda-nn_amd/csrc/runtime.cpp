@@ -691,6 +691,9 @@ void TrainerHost::training_step_overlapped(hipStream_t st, uint32_t B, const flo
 	ep.n_mlp_groups = 16;
 	ep.n_mlp = (uint32_t)n_mlp;
 	ep.d_loss = d_loss.as<float>();
+	d_factor.reserve(4);
+	ep.factor_out = d_factor.as<float>();
+	ep.factor_step = adam_step;  // parameters updated every step have step count == adam_step
 	TCNN_CHECK(n_mlp % 4 == 0, "network parameter count must be a multiple of 4");
 	m.grid_backward(st, ws, B, input, &ep);
 	mark(st, 2);
@@ -699,6 +702,8 @@ void TrainerHost::training_step_overlapped(hipStream_t st, uint32_t B, const flo
 	ag.part = ws.grid_partial.as<float>();
 	ag.n_parts = ws.n_grid_chunks;
 	ag.part_stride = m.grid->n_params;
+	ag.cached_factor = d_factor.as<float>();
+	ag.cached_step = adam_step;
 	launch_adam(st, ag, w32.as<float>(), w16.p, g32.as<float>(), g16.p, m1.as<float>(), m2.as<float>(), steps.as<uint32_t>());
 	mark(st, 3);
 	last_B = B;
@@ -768,6 +773,8 @@ AdamArgs TrainerHost::adam_args() const {
 	}
 	a.opt_matrix = adam.optimize_matrix_params;
 	a.opt_nonmatrix = adam.optimize_non_matrix_params;
+	int e = 0;
+	a.inv_loss_scale = (std::frexp(loss_scale, &e) == 0.5f) ? 1.0f / loss_scale : 0.0f;  // exact for powers of two
 	return a;
 }
 

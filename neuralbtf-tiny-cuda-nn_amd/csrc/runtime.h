@@ -204,7 +204,7 @@ struct TrainerHost {
 	AdamHost adam;
 	std::string loss_otype;
 	uint64_t n_params = 0, n_mlp = 0;
-	DevBuf w32, w16, g16, g32, m1, m2, steps, d_loss;
+	DevBuf w32, w16, g16, g32, m1, m2, steps, d_loss, d_factor;
 	StepWorkspace ws;
 	uint32_t adam_step = 0;
 	float grad_scale = 1.0f;

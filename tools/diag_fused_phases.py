@@ -12,7 +12,7 @@ out = (ctypes.c_uint64 * 8)()
 for _ in range(3):
     L.check(L.lib().tcnn_debug_fused_phase_cycles(t.h, None, B, ctypes.c_void_p(pos.data_ptr()), ctypes.c_void_p(tgt.data_ptr()), out))
 tot = sum(out)
-nw = 256 * 8
+nw = 512 * 4  # 512 workgroups x 4 waves
 names = ["grid encode (gathers)", "hidden fwd", "out layer + loss", "bwd hidden + dW", "dW0 (first layer)", "dL/dx + store",
          "prologue (per wave)", "epilogue reduce (per wave)"]
 for n, v in zip(names, out):
