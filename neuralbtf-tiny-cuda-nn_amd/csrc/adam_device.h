@@ -76,28 +76,46 @@ __device__ __forceinline__ T slab_sum(const T* src, size_t stride, uint32_t n) {
 	return s;
 }
 
-// In-launch hand-off between workgroups (MI355X_MICROARCH.md "inter-workgroup visibility";
-// cdna_hip_programming.md §6 Guideline 16, counter form): every wave drains its stores, lane 0 of
-// the workgroup releases at agent scope and draws a ticket; the workgroup that draws n - 1 is the
-// reducer and acquires before reading the others' slabs. The reducer resets the counter (counters
-// are zeroed once at allocation). `flag` is a word of the caller's existing LDS array.
-__device__ __forceinline__ bool arrive_last(uint32_t* counter, uint32_t n, volatile uint32_t* flag) {
-	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-	__syncthreads();
-	if (threadIdx.x == 0) {
-		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-		const uint32_t prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-		const bool last = prev == n - 1;
-		if (last) {
-			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-			__hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-		}
-		*flag = last ? 1u : 0u;
+// Column sums of n_parts fp32 slabs part[j * N + c], columns [c0, c0 + ncol), by ONE workgroup in a
+// fixed order (ncol, c0, N multiples of 4): the parts are split into S = blockDim / (ncol / 4)
+// contiguous groups; thread (s, k) sums group s of 4-column k (slab_sum order); the S group sums
+// are then added in group order. out[c - c0] and tmp (S * ncol floats) are LDS.
+__device__ inline void block_column_sums(const float* __restrict__ part, uint32_t n_parts, uint32_t N, uint32_t c0, uint32_t ncol,
+                                         float* tmp, float* out) {
+	const uint32_t nc4 = ncol / 4;
+	const uint32_t S = nc4 ? max(1u, blockDim.x / nc4) : 1u;
+	const uint32_t per = (n_parts + S - 1) / S;
+	const uint32_t t = threadIdx.x;
+	if (t < S * nc4) {
+		const uint32_t s = t / nc4, k = t % nc4;
+		const uint32_t j0 = s * per, j1 = min(n_parts, j0 + per);
+		const f4 v = j0 < j1 ? slab_sum((const f4*)(part + (size_t)j0 * N + c0) + k, N / 4, j1 - j0) : f4{0.0f, 0.0f, 0.0f, 0.0f};
+		*(f4*)(tmp + s * ncol + 4 * k) = v;
 	}
 	__syncthreads();
-	return *flag != 0;
+	for (uint32_t c = t; c < ncol; c += blockDim.x) {
+		float a = 0.0f;
+		for (uint32_t s = 0; s < S; ++s) a += tmp[s * ncol + c];
+		out[c] = a;
+	}
+	__syncthreads();
+}
+
+// Columns per workgroup when G workgroups split N columns (multiple of 4).
+__host__ __device__ inline uint32_t column_block(uint32_t N, uint32_t G) { return (N / 4 + G - 1) / G * 4; }
+
+// Fixed-order sum of x[0..n) by one workgroup (strided per-thread sums, then a pairwise LDS tree);
+// lds: blockDim floats. Result returned to thread 0.
+__device__ inline float block_sum_fixed(const float* __restrict__ x, uint32_t n, float* lds) {
+	float a = 0.0f;
+	for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) a += x[i];
+	lds[threadIdx.x] = a;
+	__syncthreads();
+	for (uint32_t h = blockDim.x / 2; h > 0; h >>= 1) {
+		if (threadIdx.x < h) lds[threadIdx.x] += lds[threadIdx.x + h];
+		__syncthreads();
+	}
+	return lds[0];
 }
 
 }  // namespace tcnn_amd

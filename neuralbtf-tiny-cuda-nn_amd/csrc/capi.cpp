@@ -152,7 +152,7 @@ struct ModuleGrid : ModuleBase {
 		launch_grid_bwd(st, grid.desc.n_pos_dims, grid.desc.n_features_per_level, grid.desc.hash_type, n, in, grid.desc.n_pos_dims,
 		                dL_dout, 2, grid.padded_output_width(), grid.d_slices.as<GridSlice>(), n_slices, n_chunks,
 		                partial.as<float>(), grid.n_params, grid.dev_levels(), grid.hash_grid(), grid.desc.interp);
-		launch_reduce_partials(st, partial.as<float>(), n_chunks, grid.n_params, grid.n_params, grad32.as<float>());
+		launch_grid_slab_reduce(st, partial.as<float>(), n_chunks, grid.n_params, grid.n_params, grad32.as<float>(), grid.slab_map());
 		launch_cast_f32_f16(st, grad32.as<float>(), dL_dparams, grid.n_params);
 	}
 	uint32_t n_input_dims() const override { return grid.desc.n_pos_dims; }

@@ -4,6 +4,11 @@
 //                   (reference grid.h:214-320; int32 fixed-point sums instead of fp16 atomics)
 #include "kernels.h"
 
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
 #include "adam_device.h"
 #include "grid_device.h"
 
@@ -268,44 +273,46 @@ __device__ __forceinline__ void grid_bwd_mode(int mode, int layout, uint32_t B, 
 	grid_bwd_points<D, F, H, KIND, 1>(layout, B, pos, pstride, dLdy, dy_stride, level, li, hash_grid, interp, begin, len, f0, i0, i1, scale, acc);
 }
 
-// Network-gradient tail of the epilogue (extra workgroups g = 0 .. n_mlp_groups-1): group sums of
-// the fused kernel's slabs (same grouping and order as launch_reduce_partials), then the last
-// group finishes the sum, runs Adam on the network parameters and writes the fused weight image.
-__device__ void grid_bwd_mlp_tail(const GridBwdEpilogue& ep, uint32_t g, volatile uint32_t* flag) {
-	const uint32_t G = ep.n_mlp_groups, N = ep.n_mlp, P = ep.n_wparts;
-	const uint32_t per = (P + G - 1) / G;
-	const uint32_t j0 = g * per, j1 = min(P, j0 + per);
-	float* dst = ep.group_slab + (size_t)g * (N + 4);
-	for (uint32_t c = threadIdx.x * 4; c < N; c += blockDim.x * 4)
-		*(f4*)(dst + c) = slab_sum((const f4*)(ep.wpart + (size_t)j0 * N + c), N / 4, j1 - j0);
-	if (threadIdx.x == 0) {
-		float l = 0.0f;
-		for (uint32_t j = j0; j < j1; ++j) l += ep.lpart[j];
-		dst[N] = l;
-	}
-	if (!arrive_last(ep.tail_counter, G, flag)) return;
-	if (threadIdx.x == 0 && ep.factor_out) *ep.factor_out = adam_bias_factor(ep.adam_mlp, ep.factor_step);
-	const uint32_t nW0 = ep.W * ep.IN, nWh = (ep.NH - 1) * ep.W * ep.W;
-	for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) {
-		const float s = slab_sum(ep.group_slab + i, N + 4, G);
-		ep.buf.g32[i] = s;
-		const _Float16 h = adam_update(ep.adam_mlp, ep.buf, i, s);
-		uint32_t o;
-		if (i < nW0) {
-			o = (i / ep.IN) * ep.RSI + i % ep.IN;
-		} else if (i < nW0 + nWh) {
-			const uint32_t k = i - nW0;
-			o = ep.oWh + (k / ep.W) * ep.RSW + k % ep.W;  // rows of all hidden matrices are consecutive
-		} else {
-			const uint32_t k = i - nW0 - nWh;
-			o = ep.oWo + (k / ep.W) * ep.RSW + k % ep.W;
+// Network-gradient tail (extra workgroups g = 0 .. n_mlp_groups-1, on CUs the grid items leave
+// free): workgroup g sums the fused kernel's slabs for its block of network-parameter columns
+// (block_column_sums: the same order as launch_column_sums of the sequential path), applies Adam
+// to those parameters and writes them into the next step's fused weight image. No cross-workgroup
+// dependency. Workgroup 0 also sums the loss partials and publishes the bias-correction factor.
+__device__ void grid_bwd_mlp_tail(const GridBwdEpilogue& ep, uint32_t g, float* lds) {
+	const uint32_t N = ep.n_mlp;
+	const uint32_t cb = column_block(N, ep.n_mlp_groups);
+	const uint32_t c0 = g * cb;
+	if (c0 < N) {
+		const uint32_t ncol = min(cb, N - c0);
+		float* out = lds;
+		float* tmp = lds + cb;
+		block_column_sums(ep.wpart, ep.n_wparts, N, c0, ncol, tmp, out);
+		const uint32_t nW0 = ep.W * ep.IN, nWh = (ep.NH - 1) * ep.W * ep.W;
+		for (uint32_t t = threadIdx.x; t < ncol; t += blockDim.x) {
+			const uint32_t i = c0 + t;
+			const float s = out[t];
+			ep.buf.g32[i] = s;
+			const _Float16 h = adam_update(ep.adam_mlp, ep.buf, i, s);
+			uint32_t o;
+			if (i < nW0) {
+				o = (i / ep.IN) * ep.RSI + i % ep.IN;
+			} else if (i < nW0 + nWh) {
+				const uint32_t k = i - nW0;
+				o = ep.oWh + (k / ep.W) * ep.RSW + k % ep.W;  // rows of all hidden matrices are consecutive
+			} else {
+				const uint32_t k = i - nW0 - nWh;
+				o = ep.oWo + (k / ep.W) * ep.RSW + k % ep.W;
+			}
+			ep.wimage[o] = h;
 		}
-		ep.wimage[o] = h;
 	}
-	if (threadIdx.x == 0) {
-		float l = 0.0f;
-		for (uint32_t k = 0; k < G; ++k) l += ep.group_slab[(size_t)k * (N + 4) + N];
-		*ep.d_loss = l;
+	if (g == 0) {
+		__syncthreads();
+		const float l = block_sum_fixed(ep.lpart, ep.n_wparts, lds);
+		if (threadIdx.x == 0) {
+			*ep.d_loss = l;
+			if (ep.factor_out) *ep.factor_out = adam_bias_factor(ep.adam_mlp, ep.factor_step);
+		}
 	}
 }
 
@@ -314,12 +321,16 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 	int layout, uint32_t B, const float* __restrict__ pos, uint32_t pstride, const _Float16* __restrict__ dLdy, uint32_t dy_stride,
 	const GridSlice* __restrict__ items, float* __restrict__ partial, uint32_t partial_stride,
 	const LevelInfo* __restrict__ levels, uint32_t hash_grid, uint32_t interp_u, uint32_t pts_per_chunk, uint32_t n_items,
-	uint32_t n_chunks, const GridBwdEpilogue ep) {
+	uint32_t n_chunks, const GridBwdEpilogue ep, unsigned long long* dbg_times) {
 	extern __shared__ __attribute__((aligned(16))) int acc[];
+	const unsigned long long t_start = dbg_times ? wall_clock64() : 0ull;
 	__shared__ float red[GRID_BWD_THREADS / 64];
-	volatile uint32_t* flag = (volatile uint32_t*)&red[0];
 	if (blockIdx.x >= n_items * n_chunks) {
-		grid_bwd_mlp_tail(ep, blockIdx.x - n_items * n_chunks, flag);
+		grid_bwd_mlp_tail(ep, blockIdx.x - n_items * n_chunks, (float*)acc);
+		if (dbg_times && threadIdx.x == 0) {
+			dbg_times[2 * blockIdx.x] = t_start;
+			dbg_times[2 * blockIdx.x + 1] = wall_clock64();
+		}
 		return;
 	}
 	const uint32_t item = blockIdx.x % n_items, chunk = blockIdx.x / n_items;
@@ -328,18 +339,36 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 	const uint32_t len = it.end - it.begin;
 	const uint32_t nf = it.nf, f0 = it.f0;
 	const Interp interp = (Interp)interp_u;
-	for (uint32_t j = threadIdx.x; j < len * nf; j += blockDim.x) acc[j] = 0;
+	// Replicas: a small level's accumulators fit the LDS several times; wave w adds into replica
+	// w % R, which divides the same-address atomic serialisation on the coarse dense levels
+	// (level 0: 256 entries hit by every point) by up to R. Integer sums: the replica merge below is
+	// exact and order-independent.
+	const uint32_t slots = len * nf;  // int32 slots of one replica (F = 2 packed pairs: 2 per entry)
+	const uint32_t R = max(1u, min(16u, GRID_BWD_SLOTS / max(slots, 1u)));
+	for (uint32_t j = threadIdx.x; j < R * slots; j += blockDim.x) acc[j] = 0;
+	int* acc_w = acc + ((threadIdx.x >> 6) % R) * slots;
 	const uint32_t i0 = chunk * pts_per_chunk;
 	const uint32_t i1 = min(B, i0 + pts_per_chunk);
 
 	// pre-pass: max |dL/dy| of this item's features over the chunk -> fixed-point scale
+	// (8 independent loads in flight per thread)
 	float m = 0.0f;
-	for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-		float dy[F];
-		load_dy<F>(layout, dLdy, dy_stride, it.level, B, i, dy);
+	for (uint32_t ib = i0 + threadIdx.x; ib < i1; ib += 8 * blockDim.x) {
+		float dy[8][F];
 #pragma unroll
-		for (uint32_t f = 0; f < F; ++f)
-			if (f - f0 < nf) m = fmaxf(m, fabsf(dy[f]));
+		for (uint32_t u = 0; u < 8; ++u) {
+			const uint32_t i = ib + u * blockDim.x;
+			if (i < i1) load_dy<F>(layout, dLdy, dy_stride, it.level, B, i, dy[u]);
+			else {
+#pragma unroll
+				for (uint32_t f = 0; f < F; ++f) dy[u][f] = 0.0f;
+			}
+		}
+#pragma unroll
+		for (uint32_t u = 0; u < 8; ++u)
+#pragma unroll
+			for (uint32_t f = 0; f < F; ++f)
+				if (f - f0 < nf) m = fmaxf(m, fabsf(dy[u][f]));
 	}
 #pragma unroll
 	for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
@@ -366,33 +395,81 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 	else if (whole && hash_grid && (li.size & (li.size - 1)) == 0) kind = IDX_HASH_POW2;
 	const int mode = nf == 1 ? 1 : (F == 2 ? 0 : 2);
 	if (kind == IDX_HASH_POW2)
-		grid_bwd_mode<D, F, H, IDX_HASH_POW2>(mode, layout, B, pos, pstride, dLdy, dy_stride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, i0, i1, scale, acc);
+		grid_bwd_mode<D, F, H, IDX_HASH_POW2>(mode, layout, B, pos, pstride, dLdy, dy_stride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, i0, i1, scale, acc_w);
 	else if (kind == IDX_DENSE)
-		grid_bwd_mode<D, F, H, IDX_DENSE>(mode, layout, B, pos, pstride, dLdy, dy_stride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, i0, i1, scale, acc);
+		grid_bwd_mode<D, F, H, IDX_DENSE>(mode, layout, B, pos, pstride, dLdy, dy_stride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, i0, i1, scale, acc_w);
 	else
-		grid_bwd_mode<D, F, H, IDX_GENERIC>(mode, layout, B, pos, pstride, dLdy, dy_stride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, i0, i1, scale, acc);
+		grid_bwd_mode<D, F, H, IDX_GENERIC>(mode, layout, B, pos, pstride, dLdy, dy_stride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, i0, i1, scale, acc_w);
 	__syncthreads();
+	if (R > 1) {  // merge the replicas into replica 0
+		if (mode == 0) {
+			long long* a64 = (long long*)acc;
+			for (uint32_t j = threadIdx.x; j < len; j += blockDim.x) {
+				long long t = a64[j];
+				for (uint32_t r = 1; r < R; ++r) t += a64[(size_t)r * len + j];
+				a64[j] = t;
+			}
+		} else {
+			for (uint32_t j = threadIdx.x; j < slots; j += blockDim.x) {
+				int t = acc[j];
+				for (uint32_t r = 1; r < R; ++r) t += acc[(size_t)r * slots + j];
+				acc[j] = t;
+			}
+		}
+		__syncthreads();
+	}
+	// write the chunk slab (GridSlabMap layout: this item's accumulators are one contiguous range)
 	const float inv = ldexpf(1.0f, -e);
-	float* dst = partial + (size_t)chunk * partial_stride + (size_t)(li.offset + it.begin) * F + f0;
-	if (mode == 0) {  // decode the packed int32 pairs
+	float* dst = partial + (size_t)chunk * partial_stride + (size_t)li.offset * F + (size_t)f0 * li.size + (size_t)it.begin * nf;
+	if (mode == 0) {  // decode the packed int32 pairs, two entries per thread (16-byte stores)
 		const long long* a64 = (const long long*)acc;
-		for (uint32_t j = threadIdx.x; j < len; j += blockDim.x) {
-			const long long t = a64[j];
+		auto dec = [&](long long t) {
 			const int lo = (int)(uint32_t)(unsigned long long)t;
 			const int hi = (int)((t - (long long)lo) >> 32);
-			*(float2*)(dst + 2 * j) = make_float2((float)lo * inv, (float)hi * inv);
+			return make_float2((float)lo * inv, (float)hi * inv);
+		};
+		const bool al = (((uintptr_t)dst) & 15) == 0;
+		for (uint32_t j = 2 * threadIdx.x; j < len; j += 2 * blockDim.x) {
+			const float2 a = dec(a64[j]);
+			if (al && j + 1 < len) {
+				const float2 b = dec(a64[j + 1]);
+				*(f4*)(dst + 2 * j) = f4{a.x, a.y, b.x, b.y};
+			} else {
+				*(float2*)(dst + 2 * j) = a;
+				if (j + 1 < len) *(float2*)(dst + 2 * j + 2) = dec(a64[j + 1]);
+			}
 		}
-	} else if (nf == F) {
-		for (uint32_t j = threadIdx.x; j < len * F; j += blockDim.x) dst[j] = (float)acc[j] * inv;
 	} else {
-		for (uint32_t j = threadIdx.x; j < len * nf; j += blockDim.x) dst[(j / nf) * F + (j % nf)] = (float)acc[j] * inv;
+		const uint32_t n = len * nf;
+		const bool al = (((uintptr_t)dst) & 15) == 0;
+		for (uint32_t j = 4 * threadIdx.x; j < n; j += 4 * blockDim.x) {
+			if (al && j + 4 <= n) {
+				const int4 v = *(const int4*)(acc + j);
+				*(f4*)(dst + j) = f4{(float)v.x * inv, (float)v.y * inv, (float)v.z * inv, (float)v.w * inv};
+			} else {
+				for (uint32_t k = j; k < n && k < j + 4; ++k) dst[k] = (float)acc[k] * inv;
+			}
+		}
+	}
+	if (dbg_times && threadIdx.x == 0) {
+		dbg_times[2 * blockIdx.x] = t_start;
+		dbg_times[2 * blockIdx.x + 1] = wall_clock64();
 	}
 }
 
 struct GridBwdLaunch {
 	uint32_t n_items, n_chunks;
 	GridBwdEpilogue ep;
+	unsigned long long* dbg_times;
 };
+
+// Diagnostic (TCNN_DEBUG_GRID_TIMES=1): per-workgroup start/end wall clock of the grid backward,
+// printed per work item to stderr after a synchronising copy. Never set in measured runs.
+static DevBufLite g_dbg_times;
+static bool dbg_grid_times() {
+	static const bool on = std::getenv("TCNN_DEBUG_GRID_TIMES") != nullptr;
+	return on;
+}
 
 template <uint32_t D, uint32_t F, HashType H>
 static void grid_bwd_t(hipStream_t st, int layout, uint32_t dys, dim3 g, size_t lds, uint32_t B, const float* pos, uint32_t ps,
@@ -404,7 +481,7 @@ static void grid_bwd_t(hipStream_t st, int layout, uint32_t dys, dim3 g, size_t 
 		attr = true;
 	}
 	hipLaunchKernelGGL((k_grid_bwd_lds<D, F, H>), g, dim3(GRID_BWD_THREADS), lds, st, layout, B, pos, ps, dy, dys, sl, part, pstr, lv, hg, in, ppc,
-	                   gl.n_items, gl.n_chunks, gl.ep);
+	                   gl.n_items, gl.n_chunks, gl.ep, gl.dbg_times);
 }
 
 template <uint32_t D, uint32_t F>
@@ -442,8 +519,10 @@ void launch_grid_bwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_
 	gl.n_chunks = n_chunks;
 	if (ep) gl.ep = *ep;
 	else gl.ep.enabled = 0;
+	gl.dbg_times = nullptr;
 	const uint32_t n_tail = (ep && ep->enabled) ? ep->n_mlp_groups : 0u;
 	dim3 g(n_slices * n_chunks + n_tail);
+	if (dbg_grid_times()) gl.dbg_times = (unsigned long long*)g_dbg_times.get((size_t)g.x * 16);
 	const size_t lds = GRID_BWD_LDS_BYTES;
 	const _Float16* dy = (const _Float16*)dLdy16;
 	switch (D) {
@@ -453,6 +532,25 @@ void launch_grid_bwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_
 		default: throw std::runtime_error("GridEncoding: number of input dims must be 2, 3 or 4");
 	}
 	TCNN_HIP_CHECK(hipGetLastError());
+	if (gl.dbg_times) {
+		std::vector<unsigned long long> t((size_t)g.x * 2);
+		TCNN_HIP_CHECK(hipStreamSynchronize(st));
+		TCNN_HIP_CHECK(hipMemcpy(t.data(), gl.dbg_times, t.size() * 8, hipMemcpyDeviceToHost));
+		unsigned long long t0 = ~0ull, t1 = 0;
+		for (uint32_t b = 0; b < g.x; ++b) { t0 = std::min(t0, t[2 * b]); t1 = std::max(t1, t[2 * b + 1]); }
+		fprintf(stderr, "grid_bwd: %u items x %u chunks + %u tail, span %.1f us\n", n_slices, n_chunks, n_tail, (t1 - t0) / 100.0);
+		for (uint32_t it = 0; it < n_slices; ++it) {
+			double sum = 0, mx = 0, st0 = 1e30;
+			for (uint32_t c = 0; c < n_chunks; ++c) {
+				const uint32_t b = c * n_slices + it;
+				const double d = (t[2 * b + 1] - t[2 * b]) / 100.0;
+				sum += d; mx = std::max(mx, d); st0 = std::min(st0, (t[2 * b] - t0) / 100.0);
+			}
+			fprintf(stderr, "  item %2u: mean %.1f max %.1f us, first start +%.1f\n", it, sum / n_chunks, mx, st0);
+		}
+		for (uint32_t b = n_slices * n_chunks; b < g.x; ++b)
+			fprintf(stderr, "  tail wg %u: %.1f us start +%.1f\n", b - n_slices * n_chunks, (t[2 * b + 1] - t[2 * b]) / 100.0, (t[2 * b] - t0) / 100.0);
+	}
 }
 
 }  // namespace tcnn_amd

@@ -23,6 +23,27 @@ enum : int {
 	ACT_SQUAREPLUS = 6, ACT_SOFTPLUS = 7, ACT_TANH = 8,
 };
 
+// Layout of the grid backward's per-chunk fp32 partial slabs: level-major like the parameters, but
+// within a level whose work items hold nf < F features the slab is feature-group-major
+// ([F/nf][size][nf]) so every item writes one contiguous range. slab index of grid parameter p,
+// level l, entry e, feature f (f0 = f - f % nf):  pbase[l] + f0 * size[l] + e * nf[l] + (f - f0).
+struct GridSlabMap {
+	uint32_t n_levels, log2F;
+	uint32_t pbase[MAX_LEVELS + 1];  // offset_l * F
+	uint32_t size[MAX_LEVELS];
+	uint32_t nf[MAX_LEVELS];
+};
+
+__device__ __forceinline__ uint32_t grid_slab_index(const GridSlabMap* __restrict__ m, uint32_t p) {
+	uint32_t l = 0;
+	while (l + 1 < m->n_levels && p >= m->pbase[l + 1]) ++l;
+	const uint32_t r = p - m->pbase[l];
+	const uint32_t e = r >> m->log2F, f = r & ((1u << m->log2F) - 1u);
+	const uint32_t nf = m->nf[l];
+	const uint32_t f0 = f & ~(nf - 1u);
+	return m->pbase[l] + f0 * m->size[l] + e * nf + (f - f0);
+}
+
 struct AdamArgs {
 	uint32_t n, n_matrix;
 	float loss_scale, grad_scale;  // grad_scale multiplies the fp32 gradient before fp16 rounding (1/N for N-rank sums)
@@ -40,6 +61,8 @@ struct AdamArgs {
 	// t == cached_step (nullptr: always computed per parameter; same device arithmetic either way)
 	const float* cached_factor;
 	uint32_t cached_step;
+	// grid slabs: parameter i reads slab element grid_slab_index(part_map, i - begin) (nullptr: i - begin)
+	const GridSlabMap* part_map;
 };
 
 // Optimizer state buffers (full parameter vector [network | encoding]).
@@ -54,9 +77,9 @@ struct AdamBuffers {
 };
 
 // Work carried by the grid backward launch (single-GPU trainer step): n_mlp_groups extra
-// workgroups, on CUs the grid items leave free, reduce the fused kernel's network-gradient slabs and
-// loss partials; the last of them runs Adam on the network parameters and writes the next step's
-// fused weight image. The counter must be zero before the first launch.
+// workgroups, on CUs the grid items leave free, each reduce one column block of the fused kernel's
+// network-gradient slabs, run Adam on those network parameters and write them into the next step's
+// fused weight image; workgroup 0 also sums the loss partials.
 struct GridBwdEpilogue {
 	int enabled;
 	AdamArgs adam_mlp;       // range [0, n_mlp)
@@ -66,8 +89,6 @@ struct GridBwdEpilogue {
 	const float* wpart;      // fused kernel slabs [n_wparts][n_mlp]
 	uint32_t n_wparts, n_mlp;
 	const float* lpart;      // loss partials [n_wparts]
-	float* group_slab;       // scratch [n_mlp_groups][n_mlp + 4]
-	uint32_t* tail_counter;
 	float* d_loss;
 	float* factor_out;       // receives the bias-correction factor of step adam_mlp's current step
 	uint32_t factor_step;
@@ -115,6 +136,13 @@ void launch_grid_bwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_
 // fused weight-image geometry (FusedLayout) for the epilogue
 void fused_image_layout(uint32_t W, uint32_t IN, uint32_t NH, uint32_t* RSI, uint32_t* RSW, uint32_t* oWh, uint32_t* oWo);
 
+// out[c] = sum_j in[j*N + c] in block_column_sums order (G = 16 column blocks of 1024 threads):
+// the network-gradient reduction of the sequential path, identical to the grid-backward tail's
+void launch_column_sums(hipStream_t st, const float* in, uint32_t n_parts, uint32_t N, float* out);
+constexpr uint32_t MLP_TAIL_GROUPS = 16;
+// out[p] = sum_j in[j*stride + grid_slab_index(map, p)] (the grid backward's slabs, fixed order)
+void launch_grid_slab_reduce(hipStream_t st, const float* in, uint32_t n_parts, uint32_t stride, uint32_t n, float* out,
+                             const GridSlabMap* map);
 // out[p] = sum_j in[j*stride + p] (p < n), optional fp16 copy
 void launch_reduce_partials(hipStream_t st, const float* in, uint32_t n_parts, uint32_t stride, uint32_t n,
                             float* out);

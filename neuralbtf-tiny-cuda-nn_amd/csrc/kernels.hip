@@ -37,6 +37,42 @@ __global__ __launch_bounds__(256) void k_reduce_groups(const float* __restrict__
 	}
 }
 
+__global__ __launch_bounds__(256) void k_grid_slab_reduce(const float* __restrict__ in, uint32_t n_parts, uint32_t stride, uint32_t n,
+                                                           float* __restrict__ out, const GridSlabMap* __restrict__ map) {
+	const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+	if (p >= n) return;
+	out[p] = slab_sum(in + grid_slab_index(map, p), stride, n_parts);
+}
+
+void launch_grid_slab_reduce(hipStream_t st, const float* in, uint32_t n_parts, uint32_t stride, uint32_t n, float* out,
+                             const GridSlabMap* map) {
+	if (!n) return;
+	hipLaunchKernelGGL(k_grid_slab_reduce, dim3(div_round_up(n, 256)), dim3(256), 0, st, in, n_parts, stride, n, out, map);
+	TCNN_HIP_CHECK(hipGetLastError());
+}
+
+__global__ __launch_bounds__(1024) void k_column_sums(const float* __restrict__ in, uint32_t n_parts, uint32_t N, uint32_t G,
+                                                      float* __restrict__ out) {
+	extern __shared__ float lds_cs[];
+	const uint32_t cb = column_block(N, G);
+	const uint32_t c0 = blockIdx.x * cb;
+	if (c0 >= N) return;
+	const uint32_t ncol = min(cb, N - c0);
+	block_column_sums(in, n_parts, N, c0, ncol, lds_cs + cb, lds_cs);
+	for (uint32_t t = threadIdx.x; t < ncol; t += blockDim.x) out[c0 + t] = lds_cs[t];
+}
+
+void launch_column_sums(hipStream_t st, const float* in, uint32_t n_parts, uint32_t N, float* out) {
+	TCNN_CHECK(N % 4 == 0, "column sums: N must be a multiple of 4");
+	if (!N) return;
+	const uint32_t G = MLP_TAIL_GROUPS, cb = column_block(N, G);
+	const uint32_t S = std::max(1u, 1024u / (cb / 4));
+	const size_t lds = (size_t)(cb + S * cb) * 4;
+	TCNN_CHECK(lds <= 64 * 1024, "column sums: column block too large");
+	hipLaunchKernelGGL(k_column_sums, dim3(G), dim3(1024), lds, st, in, n_parts, N, G, out);
+	TCNN_HIP_CHECK(hipGetLastError());
+}
+
 static DevBufLite g_red_tmp;
 
 void launch_reduce_partials(hipStream_t st, const float* in, uint32_t n_parts, uint32_t stride, uint32_t n, float* out) {
@@ -65,7 +101,8 @@ __global__ __launch_bounds__(256) void k_adam(const AdamArgs a, float* __restric
 	if (i >= a.n) return;
 	float gsum;
 	if (a.part) {
-		gsum = slab_sum(a.part + (i - a.begin), a.part_stride, a.n_parts);
+		const uint32_t q = a.part_map ? grid_slab_index(a.part_map, i - a.begin) : i - a.begin;
+		gsum = slab_sum(a.part + q, a.part_stride, a.n_parts);
 		((float*)grad32)[i] = gsum;
 	} else {
 		gsum = grad32[i];

@@ -182,19 +182,29 @@ GridEncodingHost::GridEncodingHost(uint32_t n_dims, const json& enc) {
 	// Items with all features (2 atomics per corner for F = 2) go first: they are the heaviest.
 	const uint32_t S = grid_bwd_slot_budget();
 	std::vector<GridSlice> single;
+	GridSlabMap map{};
+	map.n_levels = L;
+	while ((1u << map.log2F) < F) ++map.log2F;
 	for (uint32_t l = 0; l < L; ++l) {
 		const uint32_t size = levels[l].size;
+		map.pbase[l] = levels[l].offset * F;
+		map.size[l] = size;
+		map.nf[l] = F;
 		if ((uint64_t)size * F <= S) {
 			slices.push_back(GridSlice{l, 0, size, 0, F});
 			continue;
 		}
 		uint32_t nf = F;
 		while (nf > 1 && ((uint64_t)size * nf > S || F % nf)) --nf;
+		map.nf[l] = nf;
 		const uint32_t SL = size <= S / nf ? size : S / nf;
 		for (uint32_t f = 0; f < F; f += nf)
 			for (uint32_t b = 0; b < size; b += SL) single.push_back(GridSlice{l, b, std::min(size, b + SL), f, nf});
 	}
 	slices.insert(slices.end(), single.begin(), single.end());
+	map.pbase[L] = n_params;
+	d_slab_map.reserve(sizeof(GridSlabMap));
+	TCNN_HIP_CHECK(hipMemcpy(d_slab_map.p, &map, sizeof(GridSlabMap), hipMemcpyHostToDevice));
 
 	d_levels.reserve(levels.size() * sizeof(LevelInfo));
 	TCNN_HIP_CHECK(hipMemcpy(d_levels.p, levels.data(), levels.size() * sizeof(LevelInfo), hipMemcpyHostToDevice));
@@ -483,13 +493,6 @@ void NetworkHost::grid_backward(hipStream_t st, StepWorkspace& ws, uint32_t B, c
 	ws.n_grid_chunks = n_chunks;
 	ws.grid_partial.reserve((size_t)n_chunks * grid->n_params * 4);
 	if (ep) {
-		if (ws.counters.bytes < 64) {
-			ws.counters.reserve(64);
-			TCNN_HIP_CHECK(hipMemset(ws.counters.p, 0, ws.counters.bytes));
-		}
-		ep->tail_counter = ws.counters.as<uint32_t>();
-		ws.group_slab.reserve((size_t)ep->n_mlp_groups * (ep->n_mlp + 4) * 4);
-		ep->group_slab = ws.group_slab.as<float>();
 		ep->wimage = ws.wimage.as<_Float16>();
 		ep->W = mlp.width;
 		ep->IN = mlp.n_input;
@@ -513,8 +516,9 @@ void NetworkHost::fwd_bwd_fused(hipStream_t st, StepWorkspace& ws, uint32_t B, c
 	if (mark) mark(1);
 	grid_backward(st, ws, B, pos);
 	if (mark) mark(2);
-	launch_reduce_partials(st, ws.wgrad_partial.as<float>(), ws.n_fused_blocks, n_mlp, n_mlp, grad32);
-	launch_reduce_partials(st, ws.grid_partial.as<float>(), ws.n_grid_chunks, grid->n_params, grid->n_params, grad32 + n_mlp);
+	launch_column_sums(st, ws.wgrad_partial.as<float>(), ws.n_fused_blocks, n_mlp, grad32);
+	launch_grid_slab_reduce(st, ws.grid_partial.as<float>(), ws.n_grid_chunks, grid->n_params, grid->n_params, grad32 + n_mlp,
+	                        grid->slab_map());
 	if (mark) mark(3);
 }
 
@@ -587,7 +591,8 @@ void NetworkHost::fwd_bwd_layered(hipStream_t st, StepWorkspace& ws, uint32_t B,
 		launch_grid_bwd(st, grid->desc.n_pos_dims, grid->desc.n_features_per_level, grid->desc.hash_type, B, pos,
 		                grid->desc.n_pos_dims, dnext, 2, IN, grid->d_slices.as<GridSlice>(), (uint32_t)grid->slices.size(), n_chunks,
 		                ws.grid_partial.as<float>(), grid->n_params, grid->dev_levels(), grid->hash_grid(), grid->desc.interp);
-		launch_reduce_partials(st, ws.grid_partial.as<float>(), n_chunks, grid->n_params, grid->n_params, grad32 + n_mlp);
+		launch_grid_slab_reduce(st, ws.grid_partial.as<float>(), n_chunks, grid->n_params, grid->n_params, grad32 + n_mlp,
+		                        grid->slab_map());
 	}
 	if (mark) mark(2);
 	if (mark) mark(3);
@@ -688,7 +693,7 @@ void TrainerHost::training_step_overlapped(hipStream_t st, uint32_t B, const flo
 	ep.adam_mlp.n = (uint32_t)n_mlp;
 	ep.buf = AdamBuffers{w32.as<float>(), w16.as<_Float16>(), g32.as<float>(), g16.as<_Float16>(), m1.as<float>(), m2.as<float>(),
 	                     steps.as<uint32_t>()};
-	ep.n_mlp_groups = 16;
+	ep.n_mlp_groups = MLP_TAIL_GROUPS;
 	ep.n_mlp = (uint32_t)n_mlp;
 	ep.d_loss = d_loss.as<float>();
 	d_factor.reserve(4);
@@ -702,6 +707,7 @@ void TrainerHost::training_step_overlapped(hipStream_t st, uint32_t B, const flo
 	ag.part = ws.grid_partial.as<float>();
 	ag.n_parts = ws.n_grid_chunks;
 	ag.part_stride = m.grid->n_params;
+	ag.part_map = m.grid->slab_map();
 	ag.cached_factor = d_factor.as<float>();
 	ag.cached_step = adam_step;
 	launch_adam(st, ag, w32.as<float>(), w16.p, g32.as<float>(), g16.p, m1.as<float>(), m2.as<float>(), steps.as<uint32_t>());

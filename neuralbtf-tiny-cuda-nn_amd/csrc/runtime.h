@@ -55,7 +55,7 @@ struct GridEncodingHost {
 	bool stochastic = false;
 	std::vector<LevelInfo> levels;
 	std::vector<GridSlice> slices;
-	DevBuf d_levels, d_slices;
+	DevBuf d_levels, d_slices, d_slab_map;
 
 	GridEncodingHost(uint32_t n_dims_to_encode, const json& enc);
 	uint32_t padded_output_width() const { return n_features + n_to_pad; }
@@ -65,6 +65,7 @@ struct GridEncodingHost {
 	void initialize_params(Pcg32& rng, float* host_out, float scale = 1.0f) const;
 	json hyperparams() const;
 	const LevelInfo* dev_levels() const { return d_levels.as<LevelInfo>(); }
+	const GridSlabMap* slab_map() const { return d_slab_map.as<GridSlabMap>(); }
 	// point chunks of the backward: items x chunks workgroups of 1024 threads (one per CU: 128 KiB
 	// of LDS each) fit the CUs left after `reserved` other workgroups in ONE round, with one chunk of
 	// slack (config_hash, 26 items + 16 tail workgroups: 7 / 8 / 9 / 10 chunks -> 68.8 / 65.8 /
@@ -131,7 +132,6 @@ struct StepWorkspace {
 	DevBuf acts, delta0, delta1, dout16;  // layer-wise engine
 	uint32_t n_fused_blocks = 0, n_grid_chunks = 0, n_loss_partials = 0;
 	bool wimage_valid = false;  // fused weight image matches the current fp16 params (trainer fast path)
-	DevBuf counters, group_slab;  // grid-backward epilogue: hand-off counters (zeroed once), network-gradient group sums
 };
 
 // NetworkWithInputEncoding<__half> (reference network_with_input_encoding.h:41-190) over two engines:
