@@ -73,6 +73,20 @@ def cpu_baseline(cfg, budget_s=12.0):
     }
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary of this round's build
+    (profiles/*_pmc_traffic.json, tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")))
+    if not files:
+        return None
+    try:
+        k = json.load(open(files[-1]))["kernels"].get(kernel)
+        return k["hbm_bytes"] if k else None
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -190,13 +204,14 @@ def main():
             achieved = MLP_TRAIN_FLOP_PER_SAMPLE * B / (t_fused * 1e-3) / 1e12
             res["roofline"] = {"kernel": "k_fused_train_grid", "bound": "mfma", "achieved": achieved,
                                "peak": PEAK_FP16_TFLOPS, "unit": "TFLOP/s", "frac": achieved / PEAK_FP16_TFLOPS,
-                               "traffic": None}
+                               "traffic": pmc_traffic("k_fused_train_grid")}
         else:
             # the grid backward launch also carries the network-gradient reduction + Adam on the
             # network parameters (16 extra workgroups); their bytes are < 1 % of the grid's
             achieved = GRID_BWD_BYTES_PER_SAMPLE * B / (t_gbwd * 1e-3) / 1e9
             res["roofline"] = {"kernel": "k_grid_bwd_lds", "bound": "hbm", "achieved": achieved,
-                               "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": None}
+                               "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
+                               "traffic": pmc_traffic("k_grid_bwd_lds")}
     if world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(cfg)
     print(json.dumps(res))

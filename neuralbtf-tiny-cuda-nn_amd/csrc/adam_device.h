@@ -80,7 +80,7 @@ __device__ __forceinline__ T slab_sum(const T* src, size_t stride, uint32_t n) {
 // fixed order (ncol, c0, N multiples of 4): the parts are split into S = blockDim / (ncol / 4)
 // contiguous groups; thread (s, k) sums group s of 4-column k (slab_sum order); the S group sums
 // are then added in group order. out[c - c0] and tmp (S * ncol floats) are LDS.
-__device__ inline void block_column_sums(const float* __restrict__ part, uint32_t n_parts, uint32_t N, uint32_t c0, uint32_t ncol,
+__device__ __forceinline__ void block_column_sums(const float* __restrict__ part, uint32_t n_parts, uint32_t N, uint32_t c0, uint32_t ncol,
                                          float* tmp, float* out) {
 	const uint32_t nc4 = ncol / 4;
 	const uint32_t S = nc4 ? max(1u, blockDim.x / nc4) : 1u;
@@ -106,7 +106,7 @@ __host__ __device__ inline uint32_t column_block(uint32_t N, uint32_t G) { retur
 
 // Fixed-order sum of x[0..n) by one workgroup (strided per-thread sums, then a pairwise LDS tree);
 // lds: blockDim floats. Result returned to thread 0.
-__device__ inline float block_sum_fixed(const float* __restrict__ x, uint32_t n, float* lds) {
+__device__ __forceinline__ float block_sum_fixed(const float* __restrict__ x, uint32_t n, float* lds) {
 	float a = 0.0f;
 	for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) a += x[i];
 	lds[threadIdx.x] = a;

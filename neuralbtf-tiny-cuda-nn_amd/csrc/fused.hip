@@ -3,6 +3,8 @@
 // in their own translation unit.
 #include "kernels.h"
 
+#include <cstdlib>
+
 #include "grid_device.h"
 #include "mlp_fused.h"
 
@@ -135,6 +137,7 @@ void launch_fused_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, ui
 	a.levels = levels;
 	a.hash_grid = hash_grid ? 1u : 0u;
 	a.interp = (uint32_t)interp;
+	a.prof = nullptr;
 #define X(w, in, nh) if (W == w && IN == in && NH == nh) { launch_fused_shape<w, in, nh>(st, D, h, act, a, n_blocks); return; }
 	TCNN_FUSED_SHAPES(X)
 #undef X

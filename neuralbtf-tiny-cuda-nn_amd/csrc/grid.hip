@@ -278,7 +278,7 @@ __device__ __forceinline__ void grid_bwd_mode(int mode, int layout, uint32_t B, 
 // (block_column_sums: the same order as launch_column_sums of the sequential path), applies Adam
 // to those parameters and writes them into the next step's fused weight image. No cross-workgroup
 // dependency. Workgroup 0 also sums the loss partials and publishes the bias-correction factor.
-__device__ void grid_bwd_mlp_tail(const GridBwdEpilogue& ep, uint32_t g, float* lds) {
+__device__ __forceinline__ void grid_bwd_mlp_tail(const GridBwdEpilogue& ep, uint32_t g, float* lds) {
 	const uint32_t N = ep.n_mlp;
 	const uint32_t cb = column_block(N, ep.n_mlp_groups);
 	const uint32_t c0 = g * cb;
