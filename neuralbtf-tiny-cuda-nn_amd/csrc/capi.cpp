@@ -73,14 +73,12 @@ struct ModuleNWIE : ModuleBase {
 		model.inference(st, ws, n, in, params, out);
 	}
 	void forward(hipStream_t st, uint32_t n, const float* in, void* out, const void* params, bool prep) override {
-		TCNN_CHECK(!prep || !model.grid, "prepare_input_gradients (dL/dinput through the grid) is not implemented by the MI355X engine yet");
 		check_batch(n);
 		// The backward recomputes activations from the input, so the context carries nothing.
 		model.inference(st, ws, n, in, params, out);
 	}
 	void backward(hipStream_t st, uint32_t n, float* dL_din, const void* dL_dout, void* dL_dparams, const float* in,
 	              const void*, const void* params) override {
-		TCNN_CHECK(dL_din == nullptr || !model.grid, "dL/dinput through the grid is not implemented by the MI355X engine yet");
 		check_batch(n);
 		if (!dL_dparams && !dL_din) return;
 		grad32.reserve(n_params() * 4);
@@ -136,14 +134,17 @@ struct ModuleGrid : ModuleBase {
 		                in, grid.desc.n_pos_dims, params, out, false, W, grid.dev_levels(), grid.hash_grid(), grid.desc.interp);
 	}
 	void forward(hipStream_t st, uint32_t n, const float* in, void* out, const void* params, bool prep) override {
-		TCNN_CHECK(!prep, "prepare_input_gradients (grid dy/dx) is not implemented by the MI355X engine yet");
+		(void)prep;  // dy/dx is recomputed in backward (launch_grid_bwd_input), nothing to keep
 		inference(st, n, in, out, params);
 	}
 	void backward(hipStream_t st, uint32_t n, float* dL_din, const void* dL_dout, void* dL_dparams, const float* in,
-	              const void*, const void*) override {
-		TCNN_CHECK(dL_din == nullptr, "dL/dinput through the grid is not implemented by the MI355X engine yet");
+	              const void*, const void* params) override {
 		check_batch(n);
 		TCNN_CHECK(!grid.stochastic, "stochastic_interpolation is not implemented by the MI355X engine yet");
+		if (dL_din)
+			launch_grid_bwd_input(st, grid.desc.n_pos_dims, grid.desc.n_features_per_level, grid.desc.hash_type, n, grid.desc.n_levels, in,
+			                      grid.desc.n_pos_dims, params, dL_dout, 2, grid.padded_output_width(), dL_din, grid.desc.n_pos_dims,
+			                      grid.dev_levels(), grid.hash_grid(), grid.desc.interp);
 		if (!dL_dparams) return;
 		const uint32_t n_slices = (uint32_t)grid.slices.size();
 		const uint32_t n_chunks = grid.bwd_chunks(n);

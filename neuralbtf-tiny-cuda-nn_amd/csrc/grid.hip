@@ -457,6 +457,123 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 	}
 }
 
+// dL/dx through the grid (reference kernel_grid's dy_dx branch, grid.h:171-211, and
+// kernel_grid_backward_input, grid.h:322-349), fused: dy_dx is recomputed per point from the table
+// instead of being stored by the forward ([L*F][B][D] fp32 = 256 B/sample of HBM traffic saved).
+// Same operation order and FMA contraction points as the reference (see the oracle).
+template <uint32_t D, uint32_t F, HashType H>
+__global__ __launch_bounds__(256) void k_grid_bwd_input(uint32_t B, uint32_t L, const float* __restrict__ pos, uint32_t pstride,
+                                                        const _Float16* __restrict__ table, const _Float16* __restrict__ dLdy,
+                                                        int layout, uint32_t dy_stride, float* __restrict__ dx, uint32_t dx_stride,
+                                                        const LevelInfo* __restrict__ levels, uint32_t hash_grid, uint32_t interp_u) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= B) return;
+	const Interp interp = (Interp)interp_u;
+	float x[D], res[D];
+#pragma unroll
+	for (uint32_t d = 0; d < D; ++d) {
+		x[d] = pos[(size_t)i * pstride + d];
+		res[d] = 0.0f;
+	}
+	for (uint32_t l = 0; l < L; ++l) {
+		const LevelInfo li = levels[l];
+		float p[D], pd[D];
+		uint32_t pg[D];
+#pragma unroll
+		for (uint32_t d = 0; d < D; ++d) {
+			float v = __builtin_fmaf(li.scale, x[d], 0.5f);
+			const float t = floorf(v);
+			pg[d] = (uint32_t)(int)t;
+			v -= t;
+			if (interp == Interp::Smoothstep) {
+				pd[d] = 6.0f * v * (1.0f - v);
+				v = v * v * __builtin_fmaf(-2.0f, v, 3.0f);
+			} else {
+				pd[d] = 1.0f;
+			}
+			p[d] = v;
+		}
+		float grads[F][D];
+#pragma unroll
+		for (uint32_t f = 0; f < F; ++f)
+#pragma unroll
+			for (uint32_t d = 0; d < D; ++d) grads[f][d] = 0.0f;
+		if (interp != Interp::Nearest) {
+#pragma unroll
+			for (uint32_t gd = 0; gd < D; ++gd) {
+#pragma unroll
+				for (uint32_t idx = 0; idx < (1u << (D - 1)); ++idx) {
+					float w = li.scale;
+					uint32_t local[D];
+#pragma unroll
+					for (uint32_t nd = 0; nd < D - 1; ++nd) {
+						const uint32_t dim = nd >= gd ? nd + 1 : nd;
+						if ((idx & (1u << nd)) == 0) { w *= 1.0f - p[dim]; local[dim] = pg[dim]; }
+						else { w *= p[dim]; local[dim] = pg[dim] + 1; }
+					}
+					local[gd] = pg[gd];
+					const size_t il = (size_t)(li.offset + grid_index<D, H>(hash_grid != 0, li.size, li.res, local)) * F;
+					local[gd] = pg[gd] + 1;
+					const size_t ir = (size_t)(li.offset + grid_index<D, H>(hash_grid != 0, li.size, li.res, local)) * F;
+#pragma unroll
+					for (uint32_t f = 0; f < F; ++f) {
+						const float diff = (float)table[ir + f] - (float)table[il + f];
+						grads[f][gd] = __builtin_fmaf(w * diff, pd[gd], grads[f][gd]);
+					}
+				}
+			}
+		}
+		float dy[F];
+		load_dy<F>(layout, dLdy, dy_stride, l, B, i, dy);
+#pragma unroll
+		for (uint32_t f = 0; f < F; ++f)
+#pragma unroll
+			for (uint32_t d = 0; d < D; ++d) res[d] = __builtin_fmaf(dy[f], grads[f][d], res[d]);
+	}
+#pragma unroll
+	for (uint32_t d = 0; d < D; ++d) dx[(size_t)i * dx_stride + d] = res[d];
+}
+
+template <uint32_t D, uint32_t F>
+static void grid_bwd_input_h(hipStream_t st, HashType h, dim3 g, uint32_t B, uint32_t L, const float* pos, uint32_t ps, const _Float16* t,
+                             const _Float16* dy, int layout, uint32_t dys, float* dx, uint32_t dxs, const LevelInfo* lv, uint32_t hg,
+                             uint32_t in) {
+	switch (h) {
+		case HashType::Prime: hipLaunchKernelGGL((k_grid_bwd_input<D, F, HashType::Prime>), g, dim3(256), 0, st, B, L, pos, ps, t, dy, layout, dys, dx, dxs, lv, hg, in); break;
+		case HashType::ReversedPrime: hipLaunchKernelGGL((k_grid_bwd_input<D, F, HashType::ReversedPrime>), g, dim3(256), 0, st, B, L, pos, ps, t, dy, layout, dys, dx, dxs, lv, hg, in); break;
+		default: hipLaunchKernelGGL((k_grid_bwd_input<D, F, HashType::CoherentPrime>), g, dim3(256), 0, st, B, L, pos, ps, t, dy, layout, dys, dx, dxs, lv, hg, in); break;
+	}
+}
+
+template <uint32_t D>
+static void grid_bwd_input_f(hipStream_t st, uint32_t F, HashType h, dim3 g, uint32_t B, uint32_t L, const float* pos, uint32_t ps,
+                             const _Float16* t, const _Float16* dy, int layout, uint32_t dys, float* dx, uint32_t dxs,
+                             const LevelInfo* lv, uint32_t hg, uint32_t in) {
+	switch (F) {
+		case 1: grid_bwd_input_h<D, 1>(st, h, g, B, L, pos, ps, t, dy, layout, dys, dx, dxs, lv, hg, in); break;
+		case 2: grid_bwd_input_h<D, 2>(st, h, g, B, L, pos, ps, t, dy, layout, dys, dx, dxs, lv, hg, in); break;
+		case 4: grid_bwd_input_h<D, 4>(st, h, g, B, L, pos, ps, t, dy, layout, dys, dx, dxs, lv, hg, in); break;
+		case 8: grid_bwd_input_h<D, 8>(st, h, g, B, L, pos, ps, t, dy, layout, dys, dx, dxs, lv, hg, in); break;
+		default: throw std::runtime_error("GridEncoding: n_features_per_level must be 1, 2, 4 or 8");
+	}
+}
+
+void launch_grid_bwd_input(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_t B, uint32_t L, const float* pos,
+                           uint32_t pos_stride, const void* table16, const void* dLdy16, int dy_layout, uint32_t dy_stride, float* dx,
+                           uint32_t dx_stride, const LevelInfo* levels, bool hash_grid, Interp interp) {
+	if (B == 0) return;
+	const dim3 g(div_round_up(B, 256));
+	const _Float16* t = (const _Float16*)table16;
+	const _Float16* dy = (const _Float16*)dLdy16;
+	switch (D) {
+		case 2: grid_bwd_input_f<2>(st, F, h, g, B, L, pos, pos_stride, t, dy, dy_layout, dy_stride, dx, dx_stride, levels, hash_grid, (uint32_t)interp); break;
+		case 3: grid_bwd_input_f<3>(st, F, h, g, B, L, pos, pos_stride, t, dy, dy_layout, dy_stride, dx, dx_stride, levels, hash_grid, (uint32_t)interp); break;
+		case 4: grid_bwd_input_f<4>(st, F, h, g, B, L, pos, pos_stride, t, dy, dy_layout, dy_stride, dx, dx_stride, levels, hash_grid, (uint32_t)interp); break;
+		default: throw std::runtime_error("GridEncoding: number of input dims must be 2, 3 or 4");
+	}
+	TCNN_HIP_CHECK(hipGetLastError());
+}
+
 struct GridBwdLaunch {
 	uint32_t n_items, n_chunks;
 	GridBwdEpilogue ep;

@@ -133,6 +133,11 @@ void launch_grid_bwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_
                      uint32_t pos_stride, const void* dLdy16, int dy_layout, uint32_t dy_stride, const GridSlice* slices,
                      uint32_t n_slices, uint32_t n_chunks, float* partial, uint32_t partial_stride,
                      const LevelInfo* levels, bool hash_grid, Interp interp, const GridBwdEpilogue* ep = nullptr);
+// dL/dx fp32 [B][dx_stride] through the grid (reference grid.h:171-211 + 322-349), dy_dx recomputed
+// from the table; dLdy in the launch_grid_bwd layouts.
+void launch_grid_bwd_input(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_t B, uint32_t L, const float* pos,
+                           uint32_t pos_stride, const void* table16, const void* dLdy16, int dy_layout, uint32_t dy_stride, float* dx,
+                           uint32_t dx_stride, const LevelInfo* levels, bool hash_grid, Interp interp);
 // fused weight-image geometry (FusedLayout) for the epilogue
 void fused_image_layout(uint32_t W, uint32_t IN, uint32_t NH, uint32_t* RSI, uint32_t* RSW, uint32_t* oWh, uint32_t* oWo);
 

@@ -375,12 +375,16 @@ void EncodingHost::forward_aos(hipStream_t st, uint32_t B, const float* x, const
 	}
 }
 
-void EncodingHost::backward_input(hipStream_t st, uint32_t B, const float* x, const void* dy16, float* dx) const {
+void EncodingHost::backward_input(hipStream_t st, uint32_t B, const float* x, const void* dy16, float* dx, const void* params16) const {
 	const uint32_t W = padded_output_width();
 	switch (kind) {
 		case EncKind::OneBlob: launch_oneblob_bwd(st, B, n_dims, n_bins, x, n_dims, dy16, W, dx, n_dims); break;
 		case EncKind::Identity: launch_identity_bwd(st, B, n_dims, scale, dy16, W, dx, n_dims); break;
-		default: throw std::runtime_error("dL/dinput through the grid is not implemented by the MI355X engine yet");
+		default:
+			TCNN_CHECK(params16, "grid backward_input needs the grid parameters");
+			launch_grid_bwd_input(st, grid->desc.n_pos_dims, grid->desc.n_features_per_level, grid->desc.hash_type, B, grid->desc.n_levels,
+			                      x, grid->desc.n_pos_dims, params16, dy16, 2, W, dx, n_dims, grid->dev_levels(), grid->hash_grid(),
+			                      grid->desc.interp);
 	}
 }
 
@@ -582,7 +586,7 @@ void NetworkHost::fwd_bwd_layered(hipStream_t st, StepWorkspace& ws, uint32_t B,
 	if (enc_grad) {
 		// dL/d(encoding) = W0^T delta_0 (no transfer), AoS [B][IN]
 		launch_layer_bwd(st, B, W, IN, p16, dcur, nullptr, dnext, ACT_NONE);
-		if (dL_dinput) enc->backward_input(st, B, pos, dnext, dL_dinput);
+		if (dL_dinput) enc->backward_input(st, B, pos, dnext, dL_dinput, eparams);
 	}
 	if (grid) {
 		const uint32_t n_chunks = grid->bwd_chunks(B);

@@ -122,8 +122,8 @@ struct EncodingHost {
 	json hyperparams() const;
 	// encoded output AoS fp16 [B][padded_output_width()] (padding: grid 0, OneBlob / Identity 1)
 	void forward_aos(hipStream_t st, uint32_t B, const float* x, const void* params16, void* out16) const;
-	// dL/dx fp32 [B][n_dims] from dL/d(encoding) fp16 AoS (OneBlob / Identity; the grid's is not built)
-	void backward_input(hipStream_t st, uint32_t B, const float* x, const void* dy16, float* dx) const;
+	// dL/dx fp32 [B][n_dims] from dL/d(encoding) fp16 AoS; params16 = the encoding's parameters (grid)
+	void backward_input(hipStream_t st, uint32_t B, const float* x, const void* dy16, float* dx, const void* params16 = nullptr) const;
 };
 
 // Workspace for one fwd/bwd over a batch of B (sizes grow only).

@@ -78,6 +78,7 @@ def lib():
         _lib.orc_coherent_prime_hash.argtypes = [ctypes.c_uint32, ctypes.c_void_p]
         _lib.orc_grid_fwd.argtypes = [ctypes.POINTER(GridCfg), ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         _lib.orc_grid_bwd.argtypes = [ctypes.POINTER(GridCfg), ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        _lib.orc_grid_bwd_input.argtypes = [ctypes.POINTER(GridCfg), ctypes.c_uint32] + [ctypes.c_void_p] * 4
         _lib.orc_mlp_n_params.restype = ctypes.c_uint32
         _lib.orc_mlp_fwd.argtypes = [ctypes.c_uint32] * 5 + [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int,
                                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
@@ -209,6 +210,16 @@ def grid_bwd(g, pos, dL_dy16):
     grad = np.zeros(g.n_params, dtype=np.float32)
     lib().orc_grid_bwd(ctypes.byref(g), B, _p(pos), _p(dL_dy16), _p(grad))
     return grad
+
+
+def grid_bwd_input(g, pos, table16, dL_dy16):
+    """dL/dx float32 [B, D]; dL_dy16 uint16 SoA [L*F, B]"""
+    pos = np.ascontiguousarray(pos, dtype=np.float32)
+    B = pos.shape[0]
+    dx = np.empty(pos.shape, dtype=np.float32)
+    lib().orc_grid_bwd_input(ctypes.byref(g), B, _p(pos), _p(np.ascontiguousarray(table16, dtype=np.uint16)),
+                             _p(np.ascontiguousarray(dL_dy16, dtype=np.uint16)), _p(dx))
+    return dx
 
 
 def mlp_n_params(W, IN, NH, OUTP):

@@ -362,6 +362,63 @@ void orc_grid_bwd(const orc_grid* g, uint32_t B, const float* pos_in, const uint
 	}
 }
 
+/* kernel_grid dy_dx branch (grid.h:171-211) + kernel_grid_backward_input (grid.h:322-349):
+ * dL/dx[i][d] = sum_k dL/dy[k][i] * dy_dx[k][i][d], k = l*F + f ascending. nvcc contracts
+ * `grads += weight * diff * pos_derivative` to fmaf(weight*diff, pos_derivative, grads) and
+ * `result += dL_dy * dy_dx` to fmaf(dL_dy, dy_dx, result); written out explicitly. */
+void orc_grid_bwd_input(const orc_grid* g, uint32_t B, const float* pos_in, const uint16_t* table, const uint16_t* dL_dy,
+                        float* dL_dx) {
+	const uint32_t D = g->n_pos_dims, F = g->n_features_per_level, L = g->n_levels;
+	for (uint32_t i = 0; i < B; ++i) {
+		float res[8] = {0};
+		for (uint32_t l = 0; l < L; ++l) {
+			const float scale = g->scales[l];
+			float pos[8], pd[8];
+			uint32_t pg[8], local[8];
+			for (uint32_t d = 0; d < D; ++d) {
+				float p = fmaf(scale, pos_in[(size_t)i * D + d], 0.5f);
+				float t = floorf(p);
+				pg[d] = (uint32_t)(int)t;
+				p -= t;
+				if (g->interpolation == ORC_INTERP_SMOOTHSTEP) {
+					pd[d] = 6.0f * p * (1.0f - p);
+					p = p * p * fmaf(-2.0f, p, 3.0f);
+				} else {
+					pd[d] = 1.0f;
+				}
+				pos[d] = p;
+			}
+			float grads[8][4];
+			memset(grads, 0, sizeof(grads));
+			if (g->interpolation != ORC_INTERP_NEAREST) {
+				for (uint32_t gd = 0; gd < D; ++gd) {
+					for (uint32_t idx = 0; idx < (1u << (D - 1)); ++idx) {
+						float w = scale;
+						for (uint32_t nd = 0; nd < D - 1; ++nd) {
+							const uint32_t dim = nd >= gd ? nd + 1 : nd;
+							if ((idx & (1u << nd)) == 0) { w *= 1.0f - pos[dim]; local[dim] = pg[dim]; }
+							else { w *= pos[dim]; local[dim] = pg[dim] + 1; }
+						}
+						local[gd] = pg[gd];
+						const uint32_t il = (g->offsets[l] + orc_grid_index(g, l, local)) * F;
+						local[gd] = pg[gd] + 1;
+						const uint32_t ir = (g->offsets[l] + orc_grid_index(g, l, local)) * F;
+						for (uint32_t f = 0; f < F; ++f) {
+							const float diff = orc_h2f(table[ir + f]) - orc_h2f(table[il + f]);
+							grads[f][gd] = fmaf(w * diff, pd[gd], grads[f][gd]);
+						}
+					}
+				}
+			}
+			for (uint32_t f = 0; f < F; ++f) {
+				const float dy = orc_h2f(dL_dy[(size_t)(l * F + f) * B + i]);
+				for (uint32_t d = 0; d < D; ++d) res[d] = fmaf(dy, grads[f][d], res[d]);
+			}
+		}
+		for (uint32_t d = 0; d < D; ++d) dL_dx[(size_t)i * D + d] = res[d];
+	}
+}
+
 /* ------------------------------------------------------------------------------------------ */
 /* Fully fused MLP                                                                              */
 /* ------------------------------------------------------------------------------------------ */

@@ -1,6 +1,7 @@
 """Oracle pinning: the CPU restatement (oracle/) against the reference's own compiled sources
 (tests/golden/ref_known_answers.json, produced by oracle/_ref from /root/reference's pcg32.h +
 std::seed_seq) and the SURVEY.md §8(c) known answers."""
+import ctypes
 import json
 import os
 
@@ -166,3 +167,40 @@ def test_identity_encoding():
     x = np.array([[0.25, -3.0]], np.float32)
     e = O.h2f(O.identity_fwd(x, scale=2.0, offset=0.5, n_pad=2))
     np.testing.assert_array_equal(e, [[1.0, -5.5, 1.0, 1.0]])
+
+
+def test_grid_input_gradient_matches_analytic_derivative():
+    """orc_grid_bwd_input (grid.h:171-211 + 322-349) against a float64 evaluation of d/dx of
+    sum_k dL/dy_k * y_k(x) with the same table values and index function (linear interpolation)."""
+    enc = dict(CONFIG_HASH["encoding"])
+    g = O.grid_cfg(enc, 2)
+    rng = np.random.default_rng(3)
+    table = O.f2h(rng.uniform(-1, 1, g.n_params).astype(np.float32))
+    tf = O.h2f(table).astype(np.float64)
+    B = 48
+    pos = rng.uniform(0.02, 0.98, (B, 2)).astype(np.float32)
+    L, F = g.n_levels, g.n_features_per_level
+    dy = O.f2h(rng.standard_normal((L * F, B)).astype(np.float32))
+    dyf = O.h2f(dy).astype(np.float64)
+    got = O.grid_bwd_input(g, pos, table, dy)
+    ref = np.zeros((B, 2))
+    pg = np.zeros(2, np.uint32)
+    for i in range(B):
+        for l in range(L):
+            s = np.float32(g.scales[l])
+            p = np.float32(s * pos[i] + np.float32(0.5))
+            fl = np.floor(p)
+            fr = (p - fl).astype(np.float64)
+            base = fl.astype(np.int64)
+            vals = {}
+            for cx in (0, 1):
+                for cy in (0, 1):
+                    pg[0], pg[1] = base[0] + cx, base[1] + cy
+                    idx = O.lib().orc_grid_index(ctypes.byref(g), l, pg.ctypes.data_as(ctypes.c_void_p))
+                    vals[(cx, cy)] = tf[(g.offsets[l] + idx) * F:(g.offsets[l] + idx) * F + F]
+            dvx = float(s) * ((vals[(1, 0)] - vals[(0, 0)]) * (1 - fr[1]) + (vals[(1, 1)] - vals[(0, 1)]) * fr[1])
+            dvy = float(s) * ((vals[(0, 1)] - vals[(0, 0)]) * (1 - fr[0]) + (vals[(1, 1)] - vals[(1, 0)]) * fr[0])
+            for f in range(F):
+                ref[i, 0] += dyf[l * F + f, i] * dvx[f]
+                ref[i, 1] += dyf[l * F + f, i] * dvy[f]
+    np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-3)
