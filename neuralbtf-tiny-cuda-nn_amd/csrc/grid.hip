@@ -292,6 +292,7 @@ __device__ __forceinline__ void grid_bwd_mlp_tail(const GridBwdEpilogue& ep, uin
 			const uint32_t i = c0 + t;
 			const float s = out[t];
 			ep.buf.g32[i] = s;
+			if (!ep.apply_adam) continue;
 			const _Float16 h = adam_update(ep.adam_mlp, ep.buf, i, s);
 			uint32_t o;
 			if (i < nW0) {
@@ -311,7 +312,7 @@ __device__ __forceinline__ void grid_bwd_mlp_tail(const GridBwdEpilogue& ep, uin
 		const float l = block_sum_fixed(ep.lpart, ep.n_wparts, lds);
 		if (threadIdx.x == 0) {
 			*ep.d_loss = l;
-			if (ep.factor_out) *ep.factor_out = adam_bias_factor(ep.adam_mlp, ep.factor_step);
+			if (ep.apply_adam && ep.factor_out) *ep.factor_out = adam_bias_factor(ep.adam_mlp, ep.factor_step);
 		}
 	}
 }

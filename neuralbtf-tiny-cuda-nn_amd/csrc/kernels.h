@@ -82,6 +82,8 @@ struct AdamBuffers {
 // fused weight image; workgroup 0 also sums the loss partials.
 struct GridBwdEpilogue {
 	int enabled;
+	int apply_adam;          // 0: only the reduction (network gradients -> buf.g32, loss), for the
+	                         // multi-GPU path where the all-reduce sits between reduction and Adam
 	AdamArgs adam_mlp;       // range [0, n_mlp)
 	AdamBuffers buf;
 	// network-gradient tail

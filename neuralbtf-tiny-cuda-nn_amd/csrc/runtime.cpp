@@ -509,7 +509,7 @@ void NetworkHost::grid_backward(hipStream_t st, StepWorkspace& ws, uint32_t B, c
 	launch_grid_bwd(st, grid->desc.n_pos_dims, grid->desc.n_features_per_level, grid->desc.hash_type, B, pos, grid->desc.n_pos_dims,
 	                ws.dLdenc.p, 0, 0, grid->d_slices.as<GridSlice>(), n_slices, n_chunks, ws.grid_partial.as<float>(),
 	                grid->n_params, grid->dev_levels(), grid->hash_grid(), grid->desc.interp, ep);
-	if (ep) ws.wimage_valid = true;  // the epilogue wrote the image of the updated weights
+	if (ep && ep->apply_adam) ws.wimage_valid = true;  // the epilogue wrote the image of the updated weights
 }
 
 void NetworkHost::fwd_bwd_fused(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target,
@@ -665,8 +665,8 @@ void TrainerHost::training_step(hipStream_t st, uint32_t B, const float* input, 
 		timer.sampling = (timer.counter++ % timer.every) == 0;
 		if (timer.sampling) timer.marks.push_back({-1, -1, -1, -1, -1});
 	}
-	if (run_optimizer && overlapped_ok()) {
-		training_step_overlapped(st, B, input, target);
+	if (overlapped_ok()) {
+		training_step_overlapped(st, B, input, target, run_optimizer);
 		return;
 	}
 	mark(st, 0);
@@ -679,20 +679,23 @@ void TrainerHost::training_step(hipStream_t st, uint32_t B, const float* input, 
 }
 
 
-// Single-GPU training step in three launches on one stream (the reference's step is ~10 kernels plus
-// side streams, trainer.h:163-190): the fused grid+MLP kernel; the grid backward, whose 16 extra
-// workgroups (on CUs the grid items leave free) reduce the fused kernel's network-gradient slabs
-// and the loss, run Adam on the network and write the next step's weight image; Adam over the grid
-// parameters summing the grid backward's chunk slabs on the fly. Summation orders equal the
-// sequential path's (bit-identical parameters).
-void TrainerHost::training_step_overlapped(hipStream_t st, uint32_t B, const float* input, const float* target) {
+// Training step of the fused engine in three launches on one stream (the reference's step is ~10
+// kernels plus side streams, trainer.h:163-190): the fused grid+MLP kernel; the grid backward,
+// whose 16 extra workgroups (on CUs the grid items leave free) reduce the fused kernel's
+// network-gradient slabs and the loss and -- with the optimizer -- run Adam on the network and
+// write the next step's weight image; then either Adam over the grid parameters summing the grid
+// backward's chunk slabs on the fly, or (run_optimizer = false: the multi-GPU path, whose
+// all-reduce sits between the gradients and Adam) the slab reduction into the fp32 gradient.
+// Summation orders are the same either way (bit-identical parameters).
+void TrainerHost::training_step_overlapped(hipStream_t st, uint32_t B, const float* input, const float* target, bool run_optimizer) {
 	NetworkHost& m = *model;
 	mark(st, 0);
 	m.fused_kernel(st, ws, B, input, target, n_output_dims, loss_scale, w16.p, false);
 	mark(st, 1);
-	++adam_step;
+	if (run_optimizer) ++adam_step;
 	GridBwdEpilogue ep{};
 	ep.enabled = 1;
+	ep.apply_adam = run_optimizer ? 1 : 0;
 	ep.adam_mlp = adam_args();
 	ep.adam_mlp.n = (uint32_t)n_mlp;
 	ep.buf = AdamBuffers{w32.as<float>(), w16.as<_Float16>(), g32.as<float>(), g16.as<_Float16>(), m1.as<float>(), m2.as<float>(),
@@ -706,15 +709,20 @@ void TrainerHost::training_step_overlapped(hipStream_t st, uint32_t B, const flo
 	TCNN_CHECK(n_mlp % 4 == 0, "network parameter count must be a multiple of 4");
 	m.grid_backward(st, ws, B, input, &ep);
 	mark(st, 2);
-	AdamArgs ag = adam_args();
-	ag.begin = (uint32_t)n_mlp;
-	ag.part = ws.grid_partial.as<float>();
-	ag.n_parts = ws.n_grid_chunks;
-	ag.part_stride = m.grid->n_params;
-	ag.part_map = m.grid->slab_map();
-	ag.cached_factor = d_factor.as<float>();
-	ag.cached_step = adam_step;
-	launch_adam(st, ag, w32.as<float>(), w16.p, g32.as<float>(), g16.p, m1.as<float>(), m2.as<float>(), steps.as<uint32_t>());
+	if (run_optimizer) {
+		AdamArgs ag = adam_args();
+		ag.begin = (uint32_t)n_mlp;
+		ag.part = ws.grid_partial.as<float>();
+		ag.n_parts = ws.n_grid_chunks;
+		ag.part_stride = m.grid->n_params;
+		ag.part_map = m.grid->slab_map();
+		ag.cached_factor = d_factor.as<float>();
+		ag.cached_step = adam_step;
+		launch_adam(st, ag, w32.as<float>(), w16.p, g32.as<float>(), g16.p, m1.as<float>(), m2.as<float>(), steps.as<uint32_t>());
+	} else {
+		launch_grid_slab_reduce(st, ws.grid_partial.as<float>(), ws.n_grid_chunks, m.grid->n_params, m.grid->n_params,
+		                        g32.as<float>() + n_mlp, m.grid->slab_map());
+	}
 	mark(st, 3);
 	last_B = B;
 }

@@ -212,7 +212,7 @@ struct TrainerHost {
 	uint32_t last_B = 0;
 	// two-launch single-GPU step: reductions + Adam fused into the grid backward's epilogue
 	bool overlapped_ok() const { return model->fused_ok(); }
-	void training_step_overlapped(hipStream_t st, uint32_t B, const float* input, const float* target);
+	void training_step_overlapped(hipStream_t st, uint32_t B, const float* input, const float* target, bool run_optimizer);
 	AdamArgs adam_args() const;
 
 	TrainerHost(uint32_t n_in, uint32_t n_out, const json& cfg, uint32_t seed);
