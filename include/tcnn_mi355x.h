@@ -109,6 +109,11 @@ int tcnn_trainer_set_gradient_scale(tcnn_trainer* t, float scale);
 /* Re-upload params from a host fp32 array (Trainer::set_params_full_precision, trainer.h:231-244). */
 int tcnn_trainer_set_params_full_precision(tcnn_trainer* t, const float* host_params, uint64_t n);
 /* Adam step counter (AdamOptimizer::step(), adam.h:200-202). */
+/* Snapshot in the reference's format: the msgpack bytes of Trainer::serialize(with_optimizer)
+ * (trainer.h:275-315, adam.h:278-299). Call with buf == NULL to get the size. */
+int tcnn_trainer_serialize(tcnn_trainer* t, int with_optimizer, void* buf, uint64_t capacity, uint64_t* size);
+/* Trainer::deserialize: params_type "__half" or "float", optional optimizer state. */
+int tcnn_trainer_deserialize(tcnn_trainer* t, const void* buf, uint64_t size);
 uint32_t tcnn_trainer_optimizer_step_count(const tcnn_trainer* t);
 /* Engine diagnostics: name of the path the trainer runs ("fused" / "layered" / "unsupported"). */
 const char* tcnn_trainer_engine(const tcnn_trainer* t);

@@ -302,6 +302,19 @@ int tcnn_trainer_set_gradient_scale(tcnn_trainer* t, float s) {
 	t->t->grad_scale = s;
 	return 0;
 }
+int tcnn_trainer_serialize(tcnn_trainer* t, int with_optimizer, void* buf, uint64_t capacity, uint64_t* size) {
+	return guard([&] {
+		const std::vector<uint8_t> b = t->t->serialize(with_optimizer != 0);
+		if (size) *size = b.size();
+		if (buf) {
+			TCNN_CHECK(capacity >= b.size(), "tcnn_trainer_serialize: buffer too small");
+			std::memcpy(buf, b.data(), b.size());
+		}
+	});
+}
+int tcnn_trainer_deserialize(tcnn_trainer* t, const void* buf, uint64_t size) {
+	return guard([&] { t->t->deserialize(buf, (size_t)size); });
+}
 int tcnn_trainer_set_params_full_precision(tcnn_trainer* t, const float* host, uint64_t n) {
 	return guard([&] { t->t->set_params_full_precision(host, n); });
 }

@@ -222,6 +222,9 @@ struct TrainerHost {
 	float loss(hipStream_t st);
 	void inference(hipStream_t st, uint32_t B, const float* input, float* out);
 	void set_params_full_precision(const float* host, uint64_t n);
+	// snapshot in the reference's msgpack format (Trainer::serialize / deserialize, trainer.h:275-315)
+	std::vector<uint8_t> serialize(bool with_optimizer);
+	void deserialize(const void* data, size_t size);
 	void mark(hipStream_t st, int phase);  // records phase boundary when timing is enabled
 	void profile_end(double* ms, uint32_t n_phases, uint32_t* n_steps);
 };

@@ -62,6 +62,27 @@ class Trainer:
         a = np.ascontiguousarray(host_params, dtype=np.float32)
         L.check(L.lib().tcnn_trainer_set_params_full_precision(self.h, a.ctypes.data_as(ctypes.c_void_p), a.size))
 
+    def serialize(self, optimizer=False):
+        """Trainer::serialize as the reference's msgpack snapshot bytes (trainer.h:275-288)."""
+        n = ctypes.c_uint64(0)
+        L.check(L.lib().tcnn_trainer_serialize(self.h, int(optimizer), None, 0, ctypes.byref(n)))
+        buf = ctypes.create_string_buffer(n.value)
+        L.check(L.lib().tcnn_trainer_serialize(self.h, int(optimizer), buf, n.value, ctypes.byref(n)))
+        return buf.raw[:n.value]
+
+    def deserialize(self, data):
+        """Trainer::deserialize from msgpack snapshot bytes (trainer.h:290-315)."""
+        b = bytes(data)
+        L.check(L.lib().tcnn_trainer_deserialize(self.h, b, len(b)))
+
+    def save_snapshot(self, path, optimizer=True):
+        with open(path, "wb") as f:
+            f.write(self.serialize(optimizer))
+
+    def load_snapshot(self, path):
+        with open(path, "rb") as f:
+            self.deserialize(f.read())
+
     @property
     def optimizer_step_count(self):
         return L.lib().tcnn_trainer_optimizer_step_count(self.h)
