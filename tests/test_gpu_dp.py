@@ -1,0 +1,80 @@
+"""Data-parallel path of the HIP engine with two ranks on one GPU (gloo all-reduce on device
+tensors; the 8-GPU RCCL run is the driver's): shard gradients summed by
+tinycudann.parallel.allreduce_gradients and scaled 1/N equal the single-process full-batch
+gradient, and DataParallelTrainer keeps both replicas bit-identical."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, B, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    sys.path[:0] = [repo, os.path.join(repo, "neuralbtf-tiny-cuda-nn_amd"), here]
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from helpers import CONFIG_HASH, make_batch, trainer_arrays
+    from tinycudann import Trainer
+    from tinycudann.parallel import DataParallelTrainer, allreduce_gradients, shard_bounds
+    pos, tgt = make_batch(B)
+    lo, hi = shard_bounds(B, rank, world)
+    p, t = torch.from_numpy(pos[lo:hi]).cuda(), torch.from_numpy(tgt[lo:hi]).cuda()
+    tr = Trainer(2, 3, CONFIG_HASH, seed=1337)
+    tr.training_step(p, t, run_optimizer=False)
+    g = tr.gradients_fp32().clone()
+    scale = allreduce_gradients(g)
+    g_avg = (g * scale).cpu().numpy()
+    # full DataParallelTrainer steps on a fresh replica
+    tr2 = Trainer(2, 3, CONFIG_HASH, seed=1337)
+    dp = DataParallelTrainer(tr2)
+    for s in range(3):
+        pos_s, tgt_s = make_batch(B, step=s)
+        dp.training_step(torch.from_numpy(pos_s[lo:hi]).cuda(), torch.from_numpy(tgt_s[lo:hi]).cuda())
+    torch.cuda.synchronize()
+    q.put((rank, g_avg, trainer_arrays(tr2)["w32"]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gpu_allreduce_matches_full_batch():
+    import torch
+    import torch.multiprocessing as mp
+    from helpers import CONFIG_HASH, make_batch, rel_err, trainer_arrays
+    B, world = 4096, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, B, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    np.testing.assert_array_equal(res[0][2], res[1][2])  # replicas identical
+    np.testing.assert_array_equal(res[0][1], res[1][1])
+    from tinycudann import Trainer
+    pos, tgt = make_batch(B)
+    t = Trainer(2, 3, CONFIG_HASH, seed=1337)
+    t.training_step(torch.from_numpy(pos).cuda(), torch.from_numpy(tgt).cuda(), run_optimizer=False)
+    g_full = trainer_arrays(t)["g32"]
+    nm = t.n_network_params
+    assert rel_err(res[0][1][:nm], g_full[:nm]) < 2e-3
+    assert rel_err(res[0][1][nm:], g_full[nm:]) < 2e-3
