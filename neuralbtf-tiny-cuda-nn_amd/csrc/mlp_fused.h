@@ -216,17 +216,18 @@ struct WgradAcc {
 // external dL/dy, backward, weight-gradient accumulation, dL/d(encoding) stores.
 // xt: encoded input (B fragments, 16-sample tiles tau = 0, 1); target(tau, o): the target of sample
 // base + 16 tau + c, output o (read only for o < dims); after_loss(): hook run once the targets are used.
-template <int W, int IN, int NH, Act ACT, bool EXT_DOUT, bool PROF, class TargetFn, class AfterLossFn>
-__device__ __forceinline__ void fused_slice(const FusedTrainArgs& a, uint32_t base, int c, int q, const h4 (&xt)[2][IN / 16],
-                                            TargetFn target, AfterLossFn after_loss, const h4 (&Gext)[2], const _Float16* sW0,
-                                            const _Float16* sWh, const _Float16* sWo, _Float16* bufA, _Float16* bufD,
-                                            WgradAcc<W, IN, NH>& acc, unsigned long long (&ph)[8], unsigned long long& t0) {
+// Forward + loss of one 32-sample slice (shared by both fused kernels): post-activations act[j] (B
+// fragments of the next layer), dL/dy G (loss-scaled fp16, or Gext with EXT_DOUT), loss sum.
+template <int W, int IN, int NH, Act ACT, bool EXT_DOUT, bool PROF, class TargetFn>
+__device__ __forceinline__ void slice_fwd_loss(const FusedTrainArgs& a, uint32_t base, int c, int q, const h4 (&xt)[2][IN / 16],
+                                               TargetFn target, const h4 (&Gext)[2], const _Float16* sW0, const _Float16* sWh,
+                                               const _Float16* sWo, h4 (&act)[NH][2][W / 16], h4 (&G)[2], float& loss,
+                                               unsigned long long (&ph)[8], unsigned long long& t0) {
 	using L = FusedLayout<W, IN, NH>;
-	constexpr int NT = L::NT, KW = L::KW, NTI = L::NTI, KI = L::KI;
+	constexpr int NT = L::NT, KW = L::KW, KI = L::KI;
 	const f4 fz = {0.0f, 0.0f, 0.0f, 0.0f};
 	unsigned long long t1;
 	// ---------------- forward ----------------
-	h4 act[NH][2][NT];
 	{
 		f4 ac[2][NT];
 #pragma unroll
@@ -260,7 +261,6 @@ __device__ __forceinline__ void fused_slice(const FusedTrainArgs& a, uint32_t ba
 		for (int t = 0; t < NT; ++t) { act[j][0][t] = act_fwd<ACT>(ac[0][t]); act[j][1][t] = act_fwd<ACT>(ac[1][t]); }
 	}
 	if constexpr (PROF) { t1 = stamp(); ph[1] += t1 - t0; t0 = t1; }
-	h4 G[2];
 	{
 		f4 yacc[2] = {fz, fz};
 #pragma unroll
@@ -286,7 +286,7 @@ __device__ __forceinline__ void fused_slice(const FusedTrainArgs& a, uint32_t ba
 					const float p = (float)y[r];
 					const float pse = __builtin_fmaf(p, p, 0.01f);
 					const float d = p - target(tau, o);
-					acc.loss += d * d / pse / a.n_total;
+					loss += d * d / pse / a.n_total;
 					const float gr = 2.0f * d / pse;
 					g[r] = (_Float16)(a.loss_scale * gr / a.n_total);
 				}
@@ -294,6 +294,20 @@ __device__ __forceinline__ void fused_slice(const FusedTrainArgs& a, uint32_t ba
 			G[tau] = g;
 		}
 	}
+}
+
+template <int W, int IN, int NH, Act ACT, bool EXT_DOUT, bool PROF, class TargetFn, class AfterLossFn>
+__device__ __forceinline__ void fused_slice(const FusedTrainArgs& a, uint32_t base, int c, int q, const h4 (&xt)[2][IN / 16],
+                                            TargetFn target, AfterLossFn after_loss, const h4 (&Gext)[2], const _Float16* sW0,
+                                            const _Float16* sWh, const _Float16* sWo, _Float16* bufA, _Float16* bufD,
+                                            WgradAcc<W, IN, NH>& acc, unsigned long long (&ph)[8], unsigned long long& t0) {
+	using L = FusedLayout<W, IN, NH>;
+	constexpr int NT = L::NT, KW = L::KW, NTI = L::NTI;
+	const f4 fz = {0.0f, 0.0f, 0.0f, 0.0f};
+	unsigned long long t1;
+	h4 act[NH][2][NT];
+	h4 G[2];
+	slice_fwd_loss<W, IN, NH, ACT, EXT_DOUT, PROF>(a, base, c, q, xt, target, Gext, sW0, sWh, sWo, act, G, acc.loss, ph, t0);
 	after_loss();
 	if constexpr (PROF) { t1 = stamp(); ph[2] += t1 - t0; t0 = t1; }
 	// ---------------- backward + weight gradients ----------------
@@ -539,6 +553,7 @@ __global__ __launch_bounds__(256, 2) void k_fused_train_grid(const FusedTrainArg
 	__syncthreads();
 	block_reduce_wgrad<W, IN, NH, 4>(acc, (float*)smem, a, tid, wave, lane);
 }
+
 
 // Forward-only pass (inference / forward context): input fp16 from memory, SoA ([IN][B], the grid
 // encoding's layout) or AoS ([B][IN]); output fp16 [B][16] (the reference's CM [16 x B]).
