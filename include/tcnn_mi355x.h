@@ -67,6 +67,14 @@ tcnn_context* tcnn_module_forward(tcnn_module* m, void* stream, uint32_t n, cons
 int tcnn_module_backward(tcnn_module* m, void* stream, const tcnn_context* ctx, uint32_t n, float* dL_dinput,
                          const void* dL_doutput, void* dL_dparams, const float* input, const void* output,
                          const void* params);
+/* Module::backward_backward_input(stream, ctx, n, dL_ddLdinput, input, dL_doutput?, dL_dparams?,
+ * dL_ddLdoutput?, dL_dinput?, params) (cpp_api.h:94): second-order gradients from dL/d(dL/dinput)
+ * fp32 [n][n_input_dims]. Implemented by grid encodings (grid.h:902-1026); every other module
+ * fails like the reference's DifferentiableObject (object.h:278-288). Returns without work when
+ * both dL_ddLdoutput and dL_dparams are NULL (grid.h:913-915). */
+int tcnn_module_backward_backward_input(tcnn_module* m, void* stream, const tcnn_context* ctx, uint32_t n,
+                                        const float* dL_ddLdinput, const float* input, const void* dL_doutput,
+                                        void* dL_dparams, void* dL_ddLdoutput, float* dL_dinput, const void* params);
 void tcnn_context_destroy(tcnn_context* ctx);
 
 uint32_t tcnn_module_n_input_dims(const tcnn_module* m);

@@ -50,6 +50,11 @@ struct ModuleBase {
 	virtual void forward(hipStream_t st, uint32_t n, const float* in, void* out, const void* params, bool prep) = 0;
 	virtual void backward(hipStream_t st, uint32_t n, float* dL_din, const void* dL_dout, void* dL_dparams, const float* in,
 	                      const void* out, const void* params) = 0;
+	// object.h:278-288: only encodings that define it (the grid) support second-order gradients
+	virtual void backward_backward_input(hipStream_t, uint32_t, const float*, const float*, const void*, void*, void*, float*,
+	                                     const void*) {
+		throw std::runtime_error("DifferentiableObject::backward_backward_input_impl: not implemented error");
+	}
 	virtual uint32_t n_input_dims() const = 0;
 	virtual uint32_t n_output_dims() const = 0;
 	virtual uint64_t n_params() const = 0;
@@ -156,6 +161,21 @@ struct ModuleGrid : ModuleBase {
 		launch_grid_slab_reduce(st, partial.as<float>(), n_chunks, grid.n_params, grid.n_params, grad32.as<float>(), grid.slab_map());
 		launch_cast_f32_f16(st, grad32.as<float>(), dL_dparams, grid.n_params);
 	}
+	void backward_backward_input(hipStream_t st, uint32_t n, const float* dL_ddLdin, const float* in, const void* dL_dout,
+	                             void* dL_dparams, void* dL_ddLdout, float* dL_din, const void* params) override {
+		check_batch(n);
+		if (!dL_ddLdout && !dL_dparams) return;  // grid.h:913-915
+		TCNN_CHECK(params, "backward_backward_input needs the grid parameters");
+		if (dL_dparams) {
+			grad32.reserve((size_t)grid.n_params * 4);
+			TCNN_HIP_CHECK(hipMemsetAsync(grad32.p, 0, (size_t)grid.n_params * 4, st));  // GradientMode::Overwrite
+		}
+		const uint32_t W = grid.padded_output_width();
+		launch_grid_bwd_bwd(st, grid.desc.n_pos_dims, grid.desc.n_features_per_level, grid.desc.hash_type, n, grid.desc.n_levels, in,
+		                    grid.desc.n_pos_dims, params, dL_ddLdin, dL_dout, W, dL_dparams ? grad32.as<float>() : nullptr, dL_ddLdout, W,
+		                    dL_din, grid.dev_levels(), grid.hash_grid(), grid.desc.interp);
+		if (dL_dparams) launch_cast_f32_f16(st, grad32.as<float>(), dL_dparams, grid.n_params);
+	}
 	uint32_t n_input_dims() const override { return grid.desc.n_pos_dims; }
 	uint32_t n_output_dims() const override { return grid.padded_output_width(); }
 	uint64_t n_params() const override { return grid.n_params; }
@@ -248,6 +268,15 @@ int tcnn_module_backward(tcnn_module* m, void* stream, const tcnn_context* ctx, 
 	return guard([&] {
 		TCNN_CHECK(ctx != nullptr, "backward: null context");
 		m->m->backward((hipStream_t)stream, n, dL_din, dL_dout, dL_dparams, in, out, params);
+	});
+}
+
+int tcnn_module_backward_backward_input(tcnn_module* m, void* stream, const tcnn_context* ctx, uint32_t n, const float* dL_ddLdin,
+                                        const float* in, const void* dL_dout, void* dL_dparams, void* dL_ddLdout, float* dL_din,
+                                        const void* params) {
+	return guard([&] {
+		TCNN_CHECK(ctx != nullptr, "backward_backward_input: null context");
+		m->m->backward_backward_input((hipStream_t)stream, n, dL_ddLdin, in, dL_dout, dL_dparams, dL_ddLdout, dL_din, params);
 	});
 }
 

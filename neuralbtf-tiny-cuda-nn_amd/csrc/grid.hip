@@ -575,6 +575,161 @@ void launch_grid_bwd_input(hipStream_t st, uint32_t D, uint32_t F, HashType h, u
 	TCNN_HIP_CHECK(hipGetLastError());
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Second-order grid gradients: backward of backward_input (reference grid.h:351-627, host
+// :902-1026). One thread per point walks all levels; per corner c of a level it forms
+//   A_c      = sum_e g_e s pd_e sign_e(c) prod_{d!=e} w_d(c)          (d/dx of the corner weight . g)
+//   K_e(c)   = s^2 [pd2_e g_e sign_e(c) prod_{d!=e} w_d + sum_{o!=e} pd_e pd_o g_o sign_e sign_o prod_{d!=e,o} w_d]
+// so that dL/dgrid[c] += A_c dL/dy, dL/d(dL/dy) = sum_c A_c T[c], dL/dx_e = sum_c K_e(c) (T[c] . dL/dy)
+// (g = dL/d(dL/dx); the reference's per-edge loops regrouped per corner; fp32 throughout, grid
+// gradient by fp32 atomics). dLdy AoS fp16 [B][dy_stride]; dLddLdy AoS fp16 [B][ddy_stride] with
+// the padding columns zeroed; dx fp32 [B][D] overwritten.
+// ---------------------------------------------------------------------------------------------
+template <uint32_t D, uint32_t F, HashType H>
+__global__ __launch_bounds__(256) void k_grid_bwd_bwd(uint32_t B, uint32_t L, const float* __restrict__ pos, uint32_t pstride,
+                                                      const _Float16* __restrict__ table, const float* __restrict__ gxx,
+                                                      const _Float16* __restrict__ dLdy, uint32_t dy_stride, float* __restrict__ grad,
+                                                      _Float16* __restrict__ dLddLdy, uint32_t ddy_stride, float* __restrict__ dx,
+                                                      const LevelInfo* __restrict__ levels, uint32_t hash_grid, uint32_t interp_u) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= B) return;
+	const Interp interp = (Interp)interp_u;
+	float x[D], gx[D], res[D];
+#pragma unroll
+	for (uint32_t d = 0; d < D; ++d) {
+		x[d] = pos[(size_t)i * pstride + d];
+		gx[d] = gxx[(size_t)i * D + d];
+		res[d] = 0.0f;
+	}
+	for (uint32_t l = 0; l < L; ++l) {
+		const LevelInfo li = levels[l];
+		float dy[F];
+#pragma unroll
+		for (uint32_t f = 0; f < F; ++f) dy[f] = dLdy ? (float)dLdy[(size_t)i * dy_stride + l * F + f] : 0.0f;
+		float ddy[F];
+#pragma unroll
+		for (uint32_t f = 0; f < F; ++f) ddy[f] = 0.0f;
+		if (interp != Interp::Nearest) {  // nearest: dy/dx == 0, so every second-order term is 0
+			const float s = li.scale;
+			float p[D], pd[D], pd2[D];
+			uint32_t pg[D];
+#pragma unroll
+			for (uint32_t d = 0; d < D; ++d) {
+				float v = __builtin_fmaf(s, x[d], 0.5f);
+				const float t = floorf(v);
+				pg[d] = (uint32_t)(int)t;
+				v -= t;
+				if (interp == Interp::Smoothstep) {
+					pd2[d] = __builtin_fmaf(-12.0f, v, 6.0f);
+					pd[d] = 6.0f * v * (1.0f - v);
+					v = v * v * __builtin_fmaf(-2.0f, v, 3.0f);
+				} else {
+					pd2[d] = 0.0f;
+					pd[d] = 1.0f;
+				}
+				p[d] = v;
+			}
+#pragma unroll
+			for (uint32_t c = 0; c < (1u << D); ++c) {
+				uint32_t local[D];
+				float w[D], sg[D];
+#pragma unroll
+				for (uint32_t d = 0; d < D; ++d) {
+					const bool hi = (c >> d) & 1u;
+					local[d] = pg[d] + (hi ? 1u : 0u);
+					w[d] = hi ? p[d] : 1.0f - p[d];
+					sg[d] = hi ? 1.0f : -1.0f;
+				}
+				const uint32_t idx = (li.offset + grid_index<D, H>(hash_grid != 0, li.size, li.res, local)) * F;
+				float A = 0.0f, K[D];
+#pragma unroll
+				for (uint32_t e = 0; e < D; ++e) {
+					float pe = 1.0f;  // prod_{d != e} w_d
+#pragma unroll
+					for (uint32_t d = 0; d < D; ++d)
+						if (d != e) pe *= w[d];
+					A += gx[e] * s * pd[e] * sg[e] * pe;
+					float k = pd2[e] * gx[e] * sg[e] * pe;
+#pragma unroll
+					for (uint32_t o = 0; o < D; ++o) {
+						if (o == e) continue;
+						float po = 1.0f;  // prod_{d != e, o} w_d
+#pragma unroll
+						for (uint32_t d = 0; d < D; ++d)
+							if (d != e && d != o) po *= w[d];
+						k += pd[e] * pd[o] * gx[o] * sg[e] * sg[o] * po;
+					}
+					K[e] = s * s * k;
+				}
+				float tdy = 0.0f;
+#pragma unroll
+				for (uint32_t f = 0; f < F; ++f) {
+					const float t = (float)table[idx + f];
+					ddy[f] += A * t;
+					tdy += t * dy[f];
+					if (grad && dLdy) unsafeAtomicAdd(grad + idx + f, A * dy[f]);
+				}
+#pragma unroll
+				for (uint32_t e = 0; e < D; ++e) res[e] += K[e] * tdy;
+			}
+		}
+		if (dLddLdy)
+#pragma unroll
+			for (uint32_t f = 0; f < F; ++f) dLddLdy[(size_t)i * ddy_stride + l * F + f] = (_Float16)ddy[f];
+	}
+	if (dLddLdy)
+		for (uint32_t k = L * F; k < ddy_stride; ++k) dLddLdy[(size_t)i * ddy_stride + k] = (_Float16)0.0f;
+	if (dx)
+#pragma unroll
+		for (uint32_t d = 0; d < D; ++d) dx[(size_t)i * D + d] = res[d];
+}
+
+template <uint32_t D, uint32_t F>
+static void grid_bwd_bwd_h(hipStream_t st, HashType h, dim3 g, uint32_t B, uint32_t L, const float* pos, uint32_t ps,
+                           const _Float16* t, const float* gx, const _Float16* dy, uint32_t dys, float* grad, _Float16* ddy,
+                           uint32_t ddys, float* dx, const LevelInfo* lv, uint32_t hg, uint32_t in) {
+#define GBB_LAUNCH(HH) hipLaunchKernelGGL((k_grid_bwd_bwd<D, F, HH>), g, dim3(256), 0, st, B, L, pos, ps, t, gx, dy, dys, grad, ddy, ddys, dx, lv, hg, in)
+	switch (h) {
+		case HashType::Prime: GBB_LAUNCH(HashType::Prime); break;
+		case HashType::ReversedPrime: GBB_LAUNCH(HashType::ReversedPrime); break;
+		default: GBB_LAUNCH(HashType::CoherentPrime); break;
+	}
+#undef GBB_LAUNCH
+}
+
+template <uint32_t D>
+static void grid_bwd_bwd_f(hipStream_t st, uint32_t F, HashType h, dim3 g, uint32_t B, uint32_t L, const float* pos, uint32_t ps,
+                           const _Float16* t, const float* gx, const _Float16* dy, uint32_t dys, float* grad, _Float16* ddy,
+                           uint32_t ddys, float* dx, const LevelInfo* lv, uint32_t hg, uint32_t in) {
+	switch (F) {
+		case 1: grid_bwd_bwd_h<D, 1>(st, h, g, B, L, pos, ps, t, gx, dy, dys, grad, ddy, ddys, dx, lv, hg, in); break;
+		case 2: grid_bwd_bwd_h<D, 2>(st, h, g, B, L, pos, ps, t, gx, dy, dys, grad, ddy, ddys, dx, lv, hg, in); break;
+		case 4: grid_bwd_bwd_h<D, 4>(st, h, g, B, L, pos, ps, t, gx, dy, dys, grad, ddy, ddys, dx, lv, hg, in); break;
+		case 8: grid_bwd_bwd_h<D, 8>(st, h, g, B, L, pos, ps, t, gx, dy, dys, grad, ddy, ddys, dx, lv, hg, in); break;
+		default: throw std::runtime_error("GridEncoding: n_features_per_level must be 1, 2, 4 or 8");
+	}
+}
+
+void launch_grid_bwd_bwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_t B, uint32_t L, const float* pos,
+                         uint32_t pos_stride, const void* table16, const float* dL_ddLdx, const void* dLdy16, uint32_t dy_stride,
+                         float* grad32, void* dLddLdy16, uint32_t ddy_stride, float* dx, const LevelInfo* levels, bool hash_grid,
+                         Interp interp) {
+	if (B == 0) return;
+	const dim3 g(div_round_up(B, 256));
+	const _Float16* t = (const _Float16*)table16;
+	const _Float16* dy = (const _Float16*)dLdy16;
+	_Float16* ddy = (_Float16*)dLddLdy16;
+	const uint32_t hg = hash_grid ? 1u : 0u, in = (uint32_t)interp;
+	switch (D) {
+		case 2: grid_bwd_bwd_f<2>(st, F, h, g, B, L, pos, pos_stride, t, dL_ddLdx, dy, dy_stride, grad32, ddy, ddy_stride, dx, levels, hg, in); break;
+		case 3: grid_bwd_bwd_f<3>(st, F, h, g, B, L, pos, pos_stride, t, dL_ddLdx, dy, dy_stride, grad32, ddy, ddy_stride, dx, levels, hg, in); break;
+		case 4: grid_bwd_bwd_f<4>(st, F, h, g, B, L, pos, pos_stride, t, dL_ddLdx, dy, dy_stride, grad32, ddy, ddy_stride, dx, levels, hg, in); break;
+		default: throw std::runtime_error("GridEncoding: number of input dims must be 2, 3 or 4");
+	}
+	TCNN_HIP_CHECK(hipGetLastError());
+}
+
 struct GridBwdLaunch {
 	uint32_t n_items, n_chunks;
 	GridBwdEpilogue ep;

@@ -140,6 +140,13 @@ void launch_grid_bwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_
 void launch_grid_bwd_input(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_t B, uint32_t L, const float* pos,
                            uint32_t pos_stride, const void* table16, const void* dLdy16, int dy_layout, uint32_t dy_stride, float* dx,
                            uint32_t dx_stride, const LevelInfo* levels, bool hash_grid, Interp interp);
+// Second-order grid gradients (reference grid.h:351-627, 902-1026): from dL/d(dL/dx) fp32 [B][D]
+// and dL/dy (AoS fp16 [B][dy_stride], nullable) -> grad32 += dL/dgrid (fp32 atomics, nullable),
+// dL/d(dL/dy) AoS fp16 [B][ddy_stride] (nullable), dL/dx fp32 [B][D] (nullable).
+void launch_grid_bwd_bwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_t B, uint32_t L, const float* pos,
+                         uint32_t pos_stride, const void* table16, const float* dL_ddLdx, const void* dLdy16, uint32_t dy_stride,
+                         float* grad32, void* dLddLdy16, uint32_t ddy_stride, float* dx, const LevelInfo* levels, bool hash_grid,
+                         Interp interp);
 // fused weight-image geometry (FusedLayout) for the epilogue
 void fused_image_layout(uint32_t W, uint32_t IN, uint32_t NH, uint32_t* RSI, uint32_t* RSW, uint32_t* oWh, uint32_t* oWo);
 

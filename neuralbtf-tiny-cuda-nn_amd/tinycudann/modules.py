@@ -89,6 +89,24 @@ class _NativeModule:
                                              _ptr(dL_dparams), _ptr(input), _ptr(output), _ptr(params)))
         return dL_dinput, dL_dparams
 
+    def bwd_bwd_input(self, ctx, input, params, dL_ddLdinput, dL_doutput):
+        """bindings.cpp:185-239: second-order gradients from dL/d(dL/dinput)."""
+        B = input.shape[0]
+        dev = input.device
+        dL_ddLdoutput = (torch.zeros(B, self.n_output_dims, dtype=_torch_precision(self.output_precision()), device=dev)
+                         if dL_doutput.requires_grad else None)
+        dL_dparams = (torch.zeros(self.n_params, dtype=_torch_precision(self.param_precision()), device=dev)
+                      if params.requires_grad else None)
+        dL_dinput = torch.zeros(B, self.n_input_dims, dtype=torch.float32, device=dev) if input.requires_grad else None
+        if dL_doutput.requires_grad or params.requires_grad:
+            dL_ddLdinput = dL_ddLdinput.to(torch.float32).contiguous()
+            dout = dL_doutput.detach().to(_torch_precision(self.output_precision())).contiguous()
+            L.check(L.lib().tcnn_module_backward_backward_input(
+                self.h, _stream(), ctx.h, B, _ptr(dL_ddLdinput), _ptr(input),
+                _ptr(dout) if (params.requires_grad or input.requires_grad) else None,
+                _ptr(dL_dparams), _ptr(dL_ddLdoutput), _ptr(dL_dinput), _ptr(params)))
+        return dL_ddLdoutput, dL_dparams, dL_dinput
+
 
 class _NativeContext:
     def __init__(self, h):
@@ -130,12 +148,38 @@ class _module_function(torch.autograd.Function):
             warnings.warn("doutput must be a CUDA tensor, but isn't. This indicates suboptimal performance.")
             doutput = doutput.cuda()
         input, params, output = ctx.saved_tensors
+        input_grad, params_grad = _module_function_backward.apply(ctx, doutput, input, params, output)
+        return None, null_tensor_to_none(input_grad), null_tensor_to_none(params_grad), None
+
+
+class _module_function_backward(torch.autograd.Function):
+    """modules.py:128-170 of the reference: the backward as a differentiable function, so that
+    d(dL/dinput)/d(doutput, params, input) flows through Module.bwd_bwd_input."""
+
+    @staticmethod
+    def forward(ctx, ctx_fwd, doutput, input, params, output):
+        ctx.ctx_fwd = ctx_fwd
+        ctx.save_for_backward(input, params, doutput)
         with torch.no_grad():
-            scaled_grad = doutput * ctx.loss_scale
-            input_grad, params_grad = ctx.native_tcnn_module.bwd(ctx.native_ctx, input, params, output, scaled_grad)
-            input_grad = None if input_grad is None else (input_grad / ctx.loss_scale)
-            params_grad = None if params_grad is None else (params_grad / ctx.loss_scale)
-        return None, input_grad, params_grad, None
+            scaled_grad = doutput * ctx_fwd.loss_scale
+            input_grad, params_grad = ctx_fwd.native_tcnn_module.bwd(ctx_fwd.native_ctx, input, params, output, scaled_grad)
+            input_grad = null_tensor_like(input) if input_grad is None else (input_grad / ctx_fwd.loss_scale)
+            params_grad = null_tensor_like(params) if params_grad is None else (params_grad / ctx_fwd.loss_scale)
+        return input_grad, params_grad
+
+    @staticmethod
+    def backward(ctx, dinput_grad, dparams_grad):
+        input, params, doutput = ctx.saved_tensors
+        if dinput_grad is None:
+            return None, None, None, None, None
+        with torch.enable_grad():
+            doutput = doutput * ctx.ctx_fwd.loss_scale
+        with torch.no_grad():
+            doutput_grad, params_grad, input_grad = ctx.ctx_fwd.native_tcnn_module.bwd_bwd_input(
+                ctx.ctx_fwd.native_ctx, input, params, dinput_grad, doutput)
+            params_grad = None if params_grad is None else (params_grad / ctx.ctx_fwd.loss_scale)
+            input_grad = None if input_grad is None else (input_grad / ctx.ctx_fwd.loss_scale)
+        return None, doutput_grad, input_grad, params_grad, None
 
 
 class Module(torch.nn.Module):

@@ -79,6 +79,7 @@ def lib():
         _lib.orc_grid_fwd.argtypes = [ctypes.POINTER(GridCfg), ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         _lib.orc_grid_bwd.argtypes = [ctypes.POINTER(GridCfg), ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         _lib.orc_grid_bwd_input.argtypes = [ctypes.POINTER(GridCfg), ctypes.c_uint32] + [ctypes.c_void_p] * 4
+        _lib.orc_grid_bwd_bwd.argtypes = [ctypes.POINTER(GridCfg), ctypes.c_uint32] + [ctypes.c_void_p] * 7
         _lib.orc_mlp_n_params.restype = ctypes.c_uint32
         _lib.orc_mlp_fwd.argtypes = [ctypes.c_uint32] * 5 + [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int,
                                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
@@ -220,6 +221,24 @@ def grid_bwd_input(g, pos, table16, dL_dy16):
     lib().orc_grid_bwd_input(ctypes.byref(g), B, _p(pos), _p(np.ascontiguousarray(table16, dtype=np.uint16)),
                              _p(np.ascontiguousarray(dL_dy16, dtype=np.uint16)), _p(dx))
     return dx
+
+
+def grid_bwd_bwd(g, pos, table16, dL_ddLdx, dL_dy16=None, want_grad=True, want_ddLdy=True, want_dx=True):
+    """Second-order grid gradients (grid.h:351-627). dL_ddLdx float32 [B, D]; dL_dy16 uint16 SoA
+    [L*F, B] or None. Returns (grad fp32 [n_params] | None, dL_ddLdy fp32 [B, L*F] | None,
+    dL_dx fp32 [B, D] | None)."""
+    pos = np.ascontiguousarray(pos, dtype=np.float32)
+    B = pos.shape[0]
+    LF = g.n_levels * g.n_features_per_level
+    grad = np.zeros(g.n_params, dtype=np.float32) if want_grad else None
+    ddy = np.empty((B, LF), dtype=np.float32) if want_ddLdy else None
+    dx = np.empty(pos.shape, dtype=np.float32) if want_dx else None
+    dy = None if dL_dy16 is None else np.ascontiguousarray(dL_dy16, dtype=np.uint16)
+    lib().orc_grid_bwd_bwd(ctypes.byref(g), B, _p(pos), _p(np.ascontiguousarray(table16, dtype=np.uint16)),
+                           _p(np.ascontiguousarray(dL_ddLdx, dtype=np.float32)), _p(dy) if dy is not None else None,
+                           _p(grad) if grad is not None else None, _p(ddy) if ddy is not None else None,
+                           _p(dx) if dx is not None else None)
+    return grad, ddy, dx
 
 
 def mlp_n_params(W, IN, NH, OUTP):

@@ -419,6 +419,138 @@ void orc_grid_bwd_input(const orc_grid* g, uint32_t B, const float* pos_in, cons
 	}
 }
 
+
+/* pos_fract with first and second derivative (common_device.h:801-829) */
+static void orc_pos_fract2(uint32_t interp, float x, float scale, float* p, float* pd, float* pd2, uint32_t* pg) {
+	float v = fmaf(scale, x, 0.5f);
+	const float t = floorf(v);
+	*pg = (uint32_t)(int)t;
+	v -= t;
+	if (interp == ORC_INTERP_SMOOTHSTEP) {
+		/* nvcc contracts a - b*c into one fma (its default --fmad=true) */
+		*pd2 = fmaf(-12.0f, v, 6.0f);
+		*pd = 6.0f * v * (1.0f - v);
+		*p = v * v * fmaf(-2.0f, v, 3.0f);
+	} else {
+		*pd2 = 0.0f;
+		*pd = 1.0f;
+		*p = v;
+	}
+}
+
+void orc_grid_bwd_bwd(const orc_grid* g, uint32_t B, const float* pos_in, const uint16_t* table, const float* dL_ddLdx,
+                      const uint16_t* dL_dy, float* grad, float* dL_ddLdy, float* dL_dx) {
+	const uint32_t D = g->n_pos_dims, F = g->n_features_per_level, L = g->n_levels;
+	const int linear_like = g->interpolation != ORC_INTERP_NEAREST;
+	for (uint32_t i = 0; i < B; ++i) {
+		const float* gx = dL_ddLdx + (size_t)i * D;
+		float dx[8] = {0};
+		for (uint32_t l = 0; l < L; ++l) {
+			const float scale = g->scales[l];
+			float p[8], pd[8], pd2[8], dy[8];
+			uint32_t pg[8], local[8];
+			for (uint32_t d = 0; d < D; ++d) orc_pos_fract2(g->interpolation, pos_in[(size_t)i * D + d], scale, &p[d], &pd[d], &pd2[d], &pg[d]);
+			for (uint32_t f = 0; f < F; ++f) dy[f] = dL_dy ? orc_h2f(dL_dy[(size_t)(l * F + f) * B + i]) : 0.0f;
+			const uint32_t base = g->offsets[l] * F;
+#define ORC_IDX(loc) (base + orc_grid_index(g, l, (loc)) * F)
+			/* (1) dL/dgrid: grid.h:433-454 -- per gradient dim, the 2^(D-1) edges along it */
+			if (grad && dL_dy && linear_like) {
+				for (uint32_t gd = 0; gd < D; ++gd) {
+					const float grad_in = scale * gx[gd] * pd[gd];
+					for (uint32_t idx = 0; idx < (1u << (D - 1)); ++idx) {
+						float w = grad_in;
+						for (uint32_t nd = 0; nd < D - 1; ++nd) {
+							const uint32_t dim = nd >= gd ? nd + 1 : nd;
+							if ((idx & (1u << nd)) == 0) { w *= 1.0f - p[dim]; local[dim] = pg[dim]; }
+							else { w *= p[dim]; local[dim] = pg[dim] + 1; }
+						}
+						local[gd] = pg[gd];
+						const uint32_t il = ORC_IDX(local);
+						local[gd] = pg[gd] + 1;
+						const uint32_t ir = ORC_IDX(local);
+						for (uint32_t f = 0; f < F; ++f) {
+							grad[il + f] += -w * dy[f];
+							grad[ir + f] += w * dy[f];
+						}
+					}
+				}
+			}
+			/* (2) dL/d(dL/dy) = dy_dx . dL/d(dL/dx): dy_dx as kernel_grid computes it (grid.h:171-211) */
+			if (dL_ddLdy) {
+				for (uint32_t f = 0; f < F; ++f) {
+					float r = 0.0f;
+					if (linear_like) {
+						for (uint32_t gd = 0; gd < D; ++gd) {
+							float dydx = 0.0f;
+							for (uint32_t idx = 0; idx < (1u << (D - 1)); ++idx) {
+								float w = scale;
+								for (uint32_t nd = 0; nd < D - 1; ++nd) {
+									const uint32_t dim = nd >= gd ? nd + 1 : nd;
+									if ((idx & (1u << nd)) == 0) { w *= 1.0f - p[dim]; local[dim] = pg[dim]; }
+									else { w *= p[dim]; local[dim] = pg[dim] + 1; }
+								}
+								local[gd] = pg[gd];
+								const float vl = orc_h2f(table[ORC_IDX(local) + f]);
+								local[gd] = pg[gd] + 1;
+								const float vr = orc_h2f(table[ORC_IDX(local) + f]);
+								dydx += w * (vr - vl) * pd[gd];
+							}
+							r += dydx * gx[gd];
+						}
+					}
+					dL_ddLdy[(size_t)i * L * F + l * F + f] = r;
+				}
+			}
+			/* (3) dL/dx through the Hessian of y (grid.h:542-598) */
+			if (dL_dx && dL_dy && linear_like) {
+				for (uint32_t gd = 0; gd < D; ++gd) {
+					float out = 0.0f;
+					for (uint32_t idx = 0; idx < (1u << (D - 1)); ++idx) {
+						if (g->interpolation == ORC_INTERP_SMOOTHSTEP) { /* diagonal part */
+							float w = scale * scale * gx[gd] * pd2[gd];
+							for (uint32_t nd = 0; nd < D - 1; ++nd) {
+								const uint32_t dim = nd >= gd ? nd + 1 : nd;
+								if ((idx & (1u << nd)) == 0) { w *= 1.0f - p[dim]; local[dim] = pg[dim]; }
+								else { w *= p[dim]; local[dim] = pg[dim] + 1; }
+							}
+							local[gd] = pg[gd];
+							const uint32_t il = ORC_IDX(local);
+							local[gd] = pg[gd] + 1;
+							const uint32_t ir = ORC_IDX(local);
+							for (uint32_t f = 0; f < F; ++f)
+								out += (orc_h2f(table[ir + f]) - orc_h2f(table[il + f])) * dy[f] * w;
+						}
+						for (uint32_t oo = 0; oo < D - 1; ++oo) { /* mixed part, d/dx_gd of dy/dx_od */
+							const uint32_t od = oo >= gd ? oo + 1 : oo;
+							float w = scale * scale * gx[od] * pd[od] * pd[gd];
+							for (uint32_t nd = 0; nd < D - 1; ++nd) {
+								const uint32_t dim = nd >= od ? nd + 1 : nd;
+								if ((idx & (1u << nd)) == 0) {
+									w *= dim != gd ? 1.0f - p[dim] : -1.0f;
+									local[dim] = pg[dim];
+								} else {
+									if (dim != gd) w *= p[dim];
+									local[dim] = pg[dim] + 1;
+								}
+							}
+							local[od] = pg[od];
+							const uint32_t il = ORC_IDX(local);
+							local[od] = pg[od] + 1;
+							const uint32_t ir = ORC_IDX(local);
+							for (uint32_t f = 0; f < F; ++f)
+								out += (orc_h2f(table[ir + f]) - orc_h2f(table[il + f])) * dy[f] * w;
+						}
+					}
+					dx[gd] += out;
+				}
+			}
+#undef ORC_IDX
+		}
+		if (dL_dx)
+			for (uint32_t d = 0; d < D; ++d) dL_dx[(size_t)i * D + d] = dx[d];
+	}
+}
+
 /* ------------------------------------------------------------------------------------------ */
 /* Fully fused MLP                                                                              */
 /* ------------------------------------------------------------------------------------------ */

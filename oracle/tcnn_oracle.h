@@ -76,6 +76,13 @@ void orc_grid_bwd(const orc_grid* g, uint32_t B, const float* pos, const uint16_
  * dL_dy SoA fp16 [(l*F+f)*B + i] (F <= 4, D <= 8) */
 void orc_grid_bwd_input(const orc_grid* g, uint32_t B, const float* pos, const uint16_t* table, const uint16_t* dL_dy,
                         float* dL_dx);
+/* backward_backward_input (grid.h:351-627 kernels, 902-1026 host): given dL/d(dL/dx) fp32 [B][D],
+ *   grad      += dL/dgrid        (kernel_grid_backward_input_backward_grid, grid.h:351-455), fp32
+ *   dL_ddLdy   = dL/d(dL/dy)     fp32 [B][L*F] (kernel_grid_backward_input_backward_dLdoutput, :602-627)
+ *   dL_dx      = dL/dx           fp32 [B][D]   (kernel_grid_backward_input_backward_input, :457-600)
+ * dL_dy SoA fp16 [(l*F+f)*B + i]; any output may be NULL (D <= 8, F <= 8). */
+void orc_grid_bwd_bwd(const orc_grid* g, uint32_t B, const float* pos, const uint16_t* table, const float* dL_ddLdx,
+                      const uint16_t* dL_dy, float* grad, float* dL_ddLdy, float* dL_dx);
 
 /* ---- fully fused MLP (src/fully_fused_mlp.cu:47-557, 635-891) ----
  * params fp16: W0 [W x IN] RM, W_1..W_{NH-1} [W x W] RM, Wout [OUTP x W] RM (contiguous).

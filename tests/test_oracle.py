@@ -6,6 +6,7 @@ import json
 import os
 
 import numpy as np
+import pytest
 
 from oracle import oracle as O
 
@@ -204,3 +205,92 @@ def test_grid_input_gradient_matches_analytic_derivative():
                 ref[i, 0] += dyf[l * F + f, i] * dvx[f]
                 ref[i, 1] += dyf[l * F + f, i] * dvy[f]
     np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-3)
+
+
+def _grid_level_geometry(g, l, x):
+    """float64 restatement of one level of the grid for one point: corner table indices and the
+    fractional coordinate as a smooth function of x inside the point's cell."""
+    s = float(g.scales[l])
+    base = np.floor(s * x.astype(np.float64) + 0.5)
+    D = len(x)
+    idx = []
+    pg = np.zeros(D, np.uint32)
+    for c in range(1 << D):
+        for d in range(D):
+            pg[d] = int(base[d]) + ((c >> d) & 1)
+        idx.append(O.lib().orc_grid_index(ctypes.byref(g), l, pg.ctypes.data_as(ctypes.c_void_p)))
+    return s, base, idx
+
+
+def _interp(interp, fr):
+    if interp == "Smoothstep":
+        return fr * fr * (3 - 2 * fr), 6 * fr * (1 - fr)
+    return fr, np.ones_like(fr)
+
+
+def _dydx64(g, interp, l, s, base, idx, x, tf):
+    """d y_f / d x_e [F, D] in float64 for the cell given by base."""
+    D, F = len(x), g.n_features_per_level
+    fr = s * x + 0.5 - base
+    p, pd = _interp(interp, fr)
+    out = np.zeros((F, D))
+    for c in range(1 << D):
+        v = tf[(g.offsets[l] + idx[c]) * F:(g.offsets[l] + idx[c]) * F + F]
+        for e in range(D):
+            w = (1.0 if (c >> e) & 1 else -1.0) * s * pd[e]
+            for d in range(D):
+                if d != e:
+                    w *= p[d] if (c >> d) & 1 else 1 - p[d]
+            out[:, e] += w * v
+    return out, p, pd
+
+
+@pytest.mark.parametrize("interp", ["Linear", "Smoothstep"])
+def test_grid_second_order_matches_float64_derivatives(interp):
+    """orc_grid_bwd_bwd (grid.h:351-627) against float64 derivatives of
+    G = sum_{l,f} dL/dy_{l,f} * sum_e dL/d(dL/dx)_e * d y_{l,f} / d x_e:
+    dG/dtable analytic, dG/d(dL/dy) analytic, dG/dx by central differences of the analytic dy/dx."""
+    enc = dict(CONFIG_HASH["encoding"], interpolation=interp, n_levels=6)
+    g = O.grid_cfg(enc, 2)
+    rng = np.random.default_rng(11)
+    table = O.f2h(rng.uniform(-1, 1, g.n_params).astype(np.float32))
+    tf = O.h2f(table).astype(np.float64)
+    B, D = 24, 2
+    L, F = g.n_levels, g.n_features_per_level
+    pos = rng.uniform(0.02, 0.98, (B, D)).astype(np.float32)
+    gx = rng.standard_normal((B, D)).astype(np.float32)
+    dy = O.f2h(rng.standard_normal((L * F, B)).astype(np.float32))
+    dyf = O.h2f(dy).astype(np.float64)
+    grad, ddy, dx = O.grid_bwd_bwd(g, pos, table, gx, dy)
+    ref_grad = np.zeros(g.n_params)
+    ref_ddy = np.zeros((B, L * F))
+    ref_dx = np.zeros((B, D))
+    h = 1e-9
+    for i in range(B):
+        x = pos[i].astype(np.float64)
+        gi = gx[i].astype(np.float64)
+        for l in range(L):
+            s, base, idx = _grid_level_geometry(g, l, pos[i])
+            J, p, pd = _dydx64(g, interp, l, s, base, idx, x, tf)
+            dyl = dyf[l * F:(l + 1) * F, i]
+            ref_ddy[i, l * F:(l + 1) * F] = J @ gi
+            for c in range(1 << D):
+                a = 0.0
+                for e in range(D):
+                    w = (1.0 if (c >> e) & 1 else -1.0) * s * pd[e] * gi[e]
+                    for d in range(D):
+                        if d != e:
+                            w *= p[d] if (c >> d) & 1 else 1 - p[d]
+                    a += w
+                o = (g.offsets[l] + idx[c]) * F
+                ref_grad[o:o + F] += a * dyl
+            for e in range(D):
+                xp, xm = x.copy(), x.copy()
+                xp[e] += h
+                xm[e] -= h
+                Jp = _dydx64(g, interp, l, s, base, idx, xp, tf)[0]
+                Jm = _dydx64(g, interp, l, s, base, idx, xm, tf)[0]
+                ref_dx[i, e] += dyl @ ((Jp - Jm) / (2 * h)) @ gi
+    np.testing.assert_allclose(ddy, ref_ddy, rtol=2e-4, atol=2e-4 * np.abs(ref_ddy).max())
+    np.testing.assert_allclose(grad, ref_grad, rtol=2e-4, atol=2e-4 * np.abs(ref_grad).max())
+    np.testing.assert_allclose(dx, ref_dx, rtol=2e-3, atol=2e-3 * np.abs(ref_dx).max())
