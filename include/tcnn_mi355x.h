@@ -77,6 +77,16 @@ int tcnn_module_backward_backward_input(tcnn_module* m, void* stream, const tcnn
                                         void* dL_dparams, void* dL_ddLdoutput, float* dL_dinput, const void* params);
 void tcnn_context_destroy(tcnn_context* ctx);
 
+/* GridEncoding::set_max_level / max_level / set_max_level_gpu (grid_interface.h:101-123), on a grid
+ * encoding module or the grid of a NetworkWithInputEncoding module: levels above
+ * max_level * n_levels output 0 and get no gradient (grid.h:69-91, 236-244). max_level_per_point is
+ * a device pointer to n floats (one per point of every later call), or NULL. Modules without a grid
+ * fail (status != 0). With masking or stochastic interpolation in effect, networks run on the
+ * layer-wise engine. */
+int tcnn_module_set_max_level(tcnn_module* m, float max_level);
+float tcnn_module_max_level(tcnn_module* m);
+int tcnn_module_set_max_level_gpu(tcnn_module* m, const float* max_level_per_point);
+
 uint32_t tcnn_module_n_input_dims(const tcnn_module* m);
 uint32_t tcnn_module_n_output_dims(const tcnn_module* m); /* padded width (cpp_api.cu:130) */
 uint64_t tcnn_module_n_params(const tcnn_module* m);
@@ -125,6 +135,8 @@ int tcnn_trainer_deserialize(tcnn_trainer* t, const void* buf, uint64_t size);
 uint32_t tcnn_trainer_optimizer_step_count(const tcnn_trainer* t);
 /* Engine diagnostics: name of the path the trainer runs ("fused" / "layered" / "unsupported"). */
 const char* tcnn_trainer_engine(const tcnn_trainer* t);
+/* set_max_level on the trainer model's grid encoding (see tcnn_module_set_max_level) */
+int tcnn_trainer_set_max_level(tcnn_trainer* t, float max_level);
 
 /* ---- per-phase hipEvent timing of training steps (measurement hook, not in the reference) ----
  * Between begin and end training_step records events around its phases on its stream:

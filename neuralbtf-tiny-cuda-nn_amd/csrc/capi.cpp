@@ -55,6 +55,7 @@ struct ModuleBase {
 	                                     const void*) {
 		throw std::runtime_error("DifferentiableObject::backward_backward_input_impl: not implemented error");
 	}
+	virtual GridEncodingHost* grid_encoding() { return nullptr; }
 	virtual uint32_t n_input_dims() const = 0;
 	virtual uint32_t n_output_dims() const = 0;
 	virtual uint64_t n_params() const = 0;
@@ -90,6 +91,7 @@ struct ModuleNWIE : ModuleBase {
 		model.fwd_bwd(st, ws, n, in, nullptr, model.n_output_dims, 1.0f, params, dL_dout, nullptr, grad32.as<float>(), nullptr, dL_din);
 		if (dL_dparams) launch_cast_f32_f16(st, grad32.as<float>(), dL_dparams, n_params());
 	}
+	GridEncodingHost* grid_encoding() override { return model.grid; }
 	uint32_t n_input_dims() const override { return model.n_input_dims; }
 	uint32_t n_output_dims() const override { return model.mlp.padded_output; }
 	uint64_t n_params() const override { return model.n_params(); }
@@ -136,7 +138,7 @@ struct ModuleGrid : ModuleBase {
 		const uint32_t W = grid.padded_output_width();
 		if (grid.n_to_pad) TCNN_HIP_CHECK(hipMemsetAsync(out, 0, (size_t)n * W * 2, st));
 		launch_grid_fwd(st, grid.desc.n_pos_dims, grid.desc.n_features_per_level, grid.desc.hash_type, n, grid.desc.n_levels,
-		                in, grid.desc.n_pos_dims, params, out, false, W, grid.dev_levels(), grid.hash_grid(), grid.desc.interp);
+		                in, grid.desc.n_pos_dims, params, out, false, W, grid.dev_levels(), grid.hash_grid(), grid.desc.interp, grid.opts());
 	}
 	void forward(hipStream_t st, uint32_t n, const float* in, void* out, const void* params, bool prep) override {
 		(void)prep;  // dy/dx is recomputed in backward (launch_grid_bwd_input), nothing to keep
@@ -145,11 +147,10 @@ struct ModuleGrid : ModuleBase {
 	void backward(hipStream_t st, uint32_t n, float* dL_din, const void* dL_dout, void* dL_dparams, const float* in,
 	              const void*, const void* params) override {
 		check_batch(n);
-		TCNN_CHECK(!grid.stochastic, "stochastic_interpolation is not implemented by the MI355X engine yet");
 		if (dL_din)
 			launch_grid_bwd_input(st, grid.desc.n_pos_dims, grid.desc.n_features_per_level, grid.desc.hash_type, n, grid.desc.n_levels, in,
 			                      grid.desc.n_pos_dims, params, dL_dout, 2, grid.padded_output_width(), dL_din, grid.desc.n_pos_dims,
-			                      grid.dev_levels(), grid.hash_grid(), grid.desc.interp);
+			                      grid.dev_levels(), grid.hash_grid(), grid.desc.interp, grid.opts());
 		if (!dL_dparams) return;
 		const uint32_t n_slices = (uint32_t)grid.slices.size();
 		const uint32_t n_chunks = grid.bwd_chunks(n);
@@ -157,7 +158,7 @@ struct ModuleGrid : ModuleBase {
 		grad32.reserve((size_t)grid.n_params * 4);
 		launch_grid_bwd(st, grid.desc.n_pos_dims, grid.desc.n_features_per_level, grid.desc.hash_type, n, in, grid.desc.n_pos_dims,
 		                dL_dout, 2, grid.padded_output_width(), grid.d_slices.as<GridSlice>(), n_slices, n_chunks,
-		                partial.as<float>(), grid.n_params, grid.dev_levels(), grid.hash_grid(), grid.desc.interp);
+		                partial.as<float>(), grid.n_params, grid.dev_levels(), grid.hash_grid(), grid.desc.interp, nullptr, grid.opts());
 		launch_grid_slab_reduce(st, partial.as<float>(), n_chunks, grid.n_params, grid.n_params, grad32.as<float>(), grid.slab_map());
 		launch_cast_f32_f16(st, grad32.as<float>(), dL_dparams, grid.n_params);
 	}
@@ -173,9 +174,10 @@ struct ModuleGrid : ModuleBase {
 		const uint32_t W = grid.padded_output_width();
 		launch_grid_bwd_bwd(st, grid.desc.n_pos_dims, grid.desc.n_features_per_level, grid.desc.hash_type, n, grid.desc.n_levels, in,
 		                    grid.desc.n_pos_dims, params, dL_ddLdin, dL_dout, W, dL_dparams ? grad32.as<float>() : nullptr, dL_ddLdout, W,
-		                    dL_din, grid.dev_levels(), grid.hash_grid(), grid.desc.interp);
+		                    dL_din, grid.dev_levels(), grid.hash_grid(), grid.desc.interp, grid.opts());
 		if (dL_dparams) launch_cast_f32_f16(st, grad32.as<float>(), dL_dparams, grid.n_params);
 	}
+	GridEncodingHost* grid_encoding() override { return &grid; }
 	uint32_t n_input_dims() const override { return grid.desc.n_pos_dims; }
 	uint32_t n_output_dims() const override { return grid.padded_output_width(); }
 	uint64_t n_params() const override { return grid.n_params; }
@@ -281,6 +283,23 @@ int tcnn_module_backward_backward_input(tcnn_module* m, void* stream, const tcnn
 }
 
 void tcnn_context_destroy(tcnn_context* c) { delete c; }
+
+static GridEncodingHost& module_grid(tcnn_module* m) {
+	GridEncodingHost* g = m->m->grid_encoding();
+	TCNN_CHECK(g != nullptr, "module has no grid encoding");
+	return *g;
+}
+int tcnn_module_set_max_level(tcnn_module* m, float max_level) {
+	return guard([&] { module_grid(m).max_level = max_level; });
+}
+float tcnn_module_max_level(tcnn_module* m) {
+	float v = -1.0f;
+	guard([&] { v = module_grid(m).max_level; });
+	return v;
+}
+int tcnn_module_set_max_level_gpu(tcnn_module* m, const float* max_level_per_point) {
+	return guard([&] { module_grid(m).max_level_gpu = max_level_per_point; });
+}
 uint32_t tcnn_module_n_input_dims(const tcnn_module* m) { return m->m->n_input_dims(); }
 uint32_t tcnn_module_n_output_dims(const tcnn_module* m) { return m->m->n_output_dims(); }
 uint64_t tcnn_module_n_params(const tcnn_module* m) { return m->m->n_params(); }
@@ -349,6 +368,12 @@ int tcnn_trainer_set_params_full_precision(tcnn_trainer* t, const float* host, u
 }
 uint32_t tcnn_trainer_optimizer_step_count(const tcnn_trainer* t) { return t->t->adam_step; }
 const char* tcnn_trainer_engine(const tcnn_trainer* t) { return t->t->model->engine(); }
+int tcnn_trainer_set_max_level(tcnn_trainer* t, float max_level) {
+	return guard([&] {
+		TCNN_CHECK(t->t->model->grid != nullptr, "trainer model has no grid encoding");
+		t->t->model->grid->max_level = max_level;
+	});
+}
 
 int tcnn_trainer_profile_begin(tcnn_trainer* t) { return tcnn_trainer_profile_begin_sampled(t, 1); }
 int tcnn_trainer_profile_begin_sampled(tcnn_trainer* t, uint32_t every) {

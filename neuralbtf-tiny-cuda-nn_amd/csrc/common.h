@@ -48,6 +48,18 @@ enum class GridType : uint32_t { Hash = 0, Dense = 1, Tiled = 2 };
 enum class HashType : uint32_t { Prime = 0, CoherentPrime = 1, ReversedPrime = 2 };
 enum class Interp : uint32_t { Nearest = 0, Linear = 1, Smoothstep = 2 };
 
+// Grid options the fused engine does not take (reference grid_interface.h:101-123, grid.h:284-298):
+// max_level masking -- a fraction of the levels, scalar or one value per point (levels above
+// max_level * n_levels output 0 and receive no gradient) -- and stochastic interpolation (the
+// backward sends each point's gradient to one random corner of its cell).
+struct GridOpts {
+	float max_level = 1000.0f;
+	const float* max_level_gpu = nullptr;  // [B] per point, overrides max_level
+	uint32_t stochastic = 0;
+	uint32_t n_features = 0;  // n_levels * F (num_grid_features)
+	uint32_t active = 0;      // any option in effect (uniform fast-path test)
+};
+
 struct GridDesc {
 	uint32_t n_pos_dims;
 	uint32_t n_features_per_level;

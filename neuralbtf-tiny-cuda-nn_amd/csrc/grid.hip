@@ -24,7 +24,7 @@ template <uint32_t D, uint32_t F, HashType H>
 __global__ __launch_bounds__(256) void k_grid_fwd(uint32_t B, const float* __restrict__ pos, uint32_t pstride,
                                                   const _Float16* __restrict__ table, _Float16* __restrict__ out,
                                                   uint32_t soa, uint32_t out_stride, const LevelInfo* __restrict__ levels,
-                                                  uint32_t hash_grid, uint32_t interp_u) {
+                                                  uint32_t hash_grid, uint32_t interp_u, const GridOpts o) {
 	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
 	if (i >= B) return;
 	const uint32_t level = blockIdx.y;
@@ -38,7 +38,9 @@ __global__ __launch_bounds__(256) void k_grid_fwd(uint32_t B, const float* __res
 #pragma unroll
 	for (uint32_t f = 0; f < F; ++f) r[f] = (_Float16)0.0f;
 	const HVec<F>* tv = (const HVec<F>*)table;
-	if (interp == Interp::Nearest) {
+	if (o.active && (float)level >= grid_max_level(o, i, F) + 1e-3f) {
+		// masked level: output 0 (grid.h:75-91)
+	} else if (interp == Interp::Nearest) {
 		const HVec<F> v = tv[li.offset + grid_index<D, H>(hash_grid != 0, li.size, li.res, pg)];
 #pragma unroll
 		for (uint32_t f = 0; f < F; ++f) r[f] = v.v[f];
@@ -85,37 +87,38 @@ __global__ __launch_bounds__(256) void k_grid_fwd(uint32_t B, const float* __res
 
 template <uint32_t D, uint32_t F>
 static void grid_fwd_h(hipStream_t st, HashType h, dim3 g, uint32_t B, const float* pos, uint32_t ps, const _Float16* t,
-                       _Float16* o, uint32_t soa, uint32_t os, const LevelInfo* lv, uint32_t hg, uint32_t in) {
+                       _Float16* o, uint32_t soa, uint32_t os, const LevelInfo* lv, uint32_t hg, uint32_t in, const GridOpts& go) {
 	switch (h) {
-		case HashType::Prime: hipLaunchKernelGGL((k_grid_fwd<D, F, HashType::Prime>), g, dim3(256), 0, st, B, pos, ps, t, o, soa, os, lv, hg, in); break;
-		case HashType::ReversedPrime: hipLaunchKernelGGL((k_grid_fwd<D, F, HashType::ReversedPrime>), g, dim3(256), 0, st, B, pos, ps, t, o, soa, os, lv, hg, in); break;
-		default: hipLaunchKernelGGL((k_grid_fwd<D, F, HashType::CoherentPrime>), g, dim3(256), 0, st, B, pos, ps, t, o, soa, os, lv, hg, in); break;
+		case HashType::Prime: hipLaunchKernelGGL((k_grid_fwd<D, F, HashType::Prime>), g, dim3(256), 0, st, B, pos, ps, t, o, soa, os, lv, hg, in, go); break;
+		case HashType::ReversedPrime: hipLaunchKernelGGL((k_grid_fwd<D, F, HashType::ReversedPrime>), g, dim3(256), 0, st, B, pos, ps, t, o, soa, os, lv, hg, in, go); break;
+		default: hipLaunchKernelGGL((k_grid_fwd<D, F, HashType::CoherentPrime>), g, dim3(256), 0, st, B, pos, ps, t, o, soa, os, lv, hg, in, go); break;
 	}
 }
 
 template <uint32_t D>
 static void grid_fwd_f(hipStream_t st, uint32_t F, HashType h, dim3 g, uint32_t B, const float* pos, uint32_t ps,
-                       const _Float16* t, _Float16* o, uint32_t soa, uint32_t os, const LevelInfo* lv, uint32_t hg, uint32_t in) {
+                       const _Float16* t, _Float16* o, uint32_t soa, uint32_t os, const LevelInfo* lv, uint32_t hg, uint32_t in,
+                       const GridOpts& go) {
 	switch (F) {
-		case 1: grid_fwd_h<D, 1>(st, h, g, B, pos, ps, t, o, soa, os, lv, hg, in); break;
-		case 2: grid_fwd_h<D, 2>(st, h, g, B, pos, ps, t, o, soa, os, lv, hg, in); break;
-		case 4: grid_fwd_h<D, 4>(st, h, g, B, pos, ps, t, o, soa, os, lv, hg, in); break;
-		case 8: grid_fwd_h<D, 8>(st, h, g, B, pos, ps, t, o, soa, os, lv, hg, in); break;
+		case 1: grid_fwd_h<D, 1>(st, h, g, B, pos, ps, t, o, soa, os, lv, hg, in, go); break;
+		case 2: grid_fwd_h<D, 2>(st, h, g, B, pos, ps, t, o, soa, os, lv, hg, in, go); break;
+		case 4: grid_fwd_h<D, 4>(st, h, g, B, pos, ps, t, o, soa, os, lv, hg, in, go); break;
+		case 8: grid_fwd_h<D, 8>(st, h, g, B, pos, ps, t, o, soa, os, lv, hg, in, go); break;
 		default: throw std::runtime_error("GridEncoding: n_features_per_level must be 1, 2, 4 or 8");
 	}
 }
 
 void launch_grid_fwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_t B, uint32_t L,
                      const float* pos, uint32_t pos_stride, const void* table16, void* out16, bool soa,
-                     uint32_t out_stride, const LevelInfo* levels, bool hash_grid, Interp interp) {
+                     uint32_t out_stride, const LevelInfo* levels, bool hash_grid, Interp interp, const GridOpts& go) {
 	if (B == 0) return;
 	dim3 g(div_round_up(B, 256), L);
 	const _Float16* t = (const _Float16*)table16;
 	_Float16* o = (_Float16*)out16;
 	switch (D) {
-		case 2: grid_fwd_f<2>(st, F, h, g, B, pos, pos_stride, t, o, soa, out_stride, levels, hash_grid, (uint32_t)interp); break;
-		case 3: grid_fwd_f<3>(st, F, h, g, B, pos, pos_stride, t, o, soa, out_stride, levels, hash_grid, (uint32_t)interp); break;
-		case 4: grid_fwd_f<4>(st, F, h, g, B, pos, pos_stride, t, o, soa, out_stride, levels, hash_grid, (uint32_t)interp); break;
+		case 2: grid_fwd_f<2>(st, F, h, g, B, pos, pos_stride, t, o, soa, out_stride, levels, hash_grid, (uint32_t)interp, go); break;
+		case 3: grid_fwd_f<3>(st, F, h, g, B, pos, pos_stride, t, o, soa, out_stride, levels, hash_grid, (uint32_t)interp, go); break;
+		case 4: grid_fwd_f<4>(st, F, h, g, B, pos, pos_stride, t, o, soa, out_stride, levels, hash_grid, (uint32_t)interp, go); break;
 		default: throw std::runtime_error("GridEncoding: number of input dims must be 2, 3 or 4");
 	}
 	TCNN_HIP_CHECK(hipGetLastError());
@@ -190,11 +193,12 @@ __device__ __forceinline__ uint32_t level_index(bool hash_grid, uint32_t size, u
 
 // MODE: 0 = F == 2, both features as one packed int64 (two int32 halves) per entry -> one
 // ds_add_u64 per corner; 1 = one feature (f0) per entry, ds_add_u32; 2 = all F features, ds_add_u32.
-template <uint32_t D, uint32_t F, HashType H, int KIND, int MODE>
+template <uint32_t D, uint32_t F, HashType H, int KIND, int MODE, bool OPTS>
 __device__ __forceinline__ void grid_bwd_points(int layout, uint32_t B, const float* __restrict__ pos, uint32_t pstride,
                                                 const _Float16* __restrict__ dLdy, uint32_t dy_stride, uint32_t level,
                                                 const LevelInfo& li, bool hash_grid, Interp interp, uint32_t begin,
-                                                uint32_t len, uint32_t f0, uint32_t i0, uint32_t i1, float scale, int* acc) {
+                                                uint32_t len, uint32_t f0, uint32_t i0, uint32_t i1, float scale, int* acc,
+                                                const GridOpts& o) {
 	constexpr uint32_t NF = MODE == 1 ? 1 : F;
 	constexpr uint32_t U = 8;  // points in flight per thread
 	for (uint32_t base = i0 + threadIdx.x; base < i1; base += U * blockDim.x) {
@@ -210,6 +214,10 @@ __device__ __forceinline__ void grid_bwd_points(int layout, uint32_t B, const fl
 			} else {
 #pragma unroll
 				for (uint32_t d = 0; d < D; ++d) xs[u][d] = 0.0f;
+#pragma unroll
+				for (uint32_t f = 0; f < F; ++f) v[f] = 0.0f;
+			}
+			if (OPTS && i < i1 && (float)level > grid_max_level(o, i, F) + 1e-3f) {  // masked (grid.h:242-244)
 #pragma unroll
 				for (uint32_t f = 0; f < F; ++f) v[f] = 0.0f;
 			}
@@ -231,9 +239,18 @@ __device__ __forceinline__ void grid_bwd_points(int layout, uint32_t B, const fl
 #pragma unroll
 			for (uint32_t d = 0; d < D; ++d) pos_fract(xs[u][d], li.scale, interp, p[d], pg[d]);
 			const bool nearest = interp == Interp::Nearest;
+			// stochastic interpolation (grid.h:284-298): one corner, chosen per (point, level), weight 1
+			const bool single = nearest || (OPTS && o.stochastic);
+			uint32_t cbits = 0;
+			if (single && !nearest) {
+				const float smp = random_val_1337(base + u * blockDim.x + level * B);
 #pragma unroll
-			for (uint32_t c = 0; c < (1u << D); ++c) {
-				if (nearest && c > 0) break;
+				for (uint32_t d = 0; d < D; ++d) cbits |= (smp >= p[d] ? 0u : 1u) << d;
+			}
+#pragma unroll
+			for (uint32_t c0 = 0; c0 < (1u << D); ++c0) {
+				if (single && c0 > 0) break;
+				const uint32_t c = single ? cbits : c0;
 				float w = 1.0f;
 				uint32_t local[D];
 #pragma unroll
@@ -241,7 +258,7 @@ __device__ __forceinline__ void grid_bwd_points(int layout, uint32_t B, const fl
 					if ((c & (1u << d)) == 0) { w *= 1.0f - p[d]; local[d] = pg[d]; }
 					else { w *= p[d]; local[d] = pg[d] + 1; }
 				}
-				const float wh = nearest ? 1.0f : (float)(_Float16)w;
+				const float wh = single ? 1.0f : (float)(_Float16)w;
 				const uint32_t rel = level_index<D, H, KIND>(hash_grid, li.size, li.res, local) - begin;
 				if constexpr (KIND == IDX_GENERIC) {  // entry slices may not cover the level
 					if (rel >= len) continue;
@@ -260,17 +277,17 @@ __device__ __forceinline__ void grid_bwd_points(int layout, uint32_t B, const fl
 	}
 }
 
-template <uint32_t D, uint32_t F, HashType H, int KIND>
+template <uint32_t D, uint32_t F, HashType H, int KIND, bool OPTS>
 __device__ __forceinline__ void grid_bwd_mode(int mode, int layout, uint32_t B, const float* pos, uint32_t pstride,
                                               const _Float16* dLdy, uint32_t dy_stride, uint32_t level, const LevelInfo& li,
                                               bool hash_grid, Interp interp, uint32_t begin, uint32_t len, uint32_t f0,
-                                              uint32_t i0, uint32_t i1, float scale, int* acc) {
+                                              uint32_t i0, uint32_t i1, float scale, int* acc, const GridOpts& o) {
 	if constexpr (F == 2) {
-		if (mode == 0) { grid_bwd_points<D, F, H, KIND, 0>(layout, B, pos, pstride, dLdy, dy_stride, level, li, hash_grid, interp, begin, len, f0, i0, i1, scale, acc); return; }
+		if (mode == 0) { grid_bwd_points<D, F, H, KIND, 0, OPTS>(layout, B, pos, pstride, dLdy, dy_stride, level, li, hash_grid, interp, begin, len, f0, i0, i1, scale, acc, o); return; }
 	} else if constexpr (F > 2) {
-		if (mode == 2) { grid_bwd_points<D, F, H, KIND, 2>(layout, B, pos, pstride, dLdy, dy_stride, level, li, hash_grid, interp, begin, len, f0, i0, i1, scale, acc); return; }
+		if (mode == 2) { grid_bwd_points<D, F, H, KIND, 2, OPTS>(layout, B, pos, pstride, dLdy, dy_stride, level, li, hash_grid, interp, begin, len, f0, i0, i1, scale, acc, o); return; }
 	}
-	grid_bwd_points<D, F, H, KIND, 1>(layout, B, pos, pstride, dLdy, dy_stride, level, li, hash_grid, interp, begin, len, f0, i0, i1, scale, acc);
+	grid_bwd_points<D, F, H, KIND, 1, OPTS>(layout, B, pos, pstride, dLdy, dy_stride, level, li, hash_grid, interp, begin, len, f0, i0, i1, scale, acc, o);
 }
 
 // Network-gradient tail (extra workgroups g = 0 .. n_mlp_groups-1, on CUs the grid items leave
@@ -317,12 +334,12 @@ __device__ __forceinline__ void grid_bwd_mlp_tail(const GridBwdEpilogue& ep, uin
 	}
 }
 
-template <uint32_t D, uint32_t F, HashType H>
+template <uint32_t D, uint32_t F, HashType H, bool OPTS>
 __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 	int layout, uint32_t B, const float* __restrict__ pos, uint32_t pstride, const _Float16* __restrict__ dLdy, uint32_t dy_stride,
 	const GridSlice* __restrict__ items, float* __restrict__ partial, uint32_t partial_stride,
 	const LevelInfo* __restrict__ levels, uint32_t hash_grid, uint32_t interp_u, uint32_t pts_per_chunk, uint32_t n_items,
-	uint32_t n_chunks, const GridBwdEpilogue ep, unsigned long long* dbg_times) {
+	uint32_t n_chunks, const GridBwdEpilogue ep, unsigned long long* dbg_times, const GridOpts o) {
 	extern __shared__ __attribute__((aligned(16))) int acc[];
 	const unsigned long long t_start = dbg_times ? wall_clock64() : 0ull;
 	__shared__ float red[GRID_BWD_THREADS / 64];
@@ -396,11 +413,11 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 	else if (whole && hash_grid && (li.size & (li.size - 1)) == 0) kind = IDX_HASH_POW2;
 	const int mode = nf == 1 ? 1 : (F == 2 ? 0 : 2);
 	if (kind == IDX_HASH_POW2)
-		grid_bwd_mode<D, F, H, IDX_HASH_POW2>(mode, layout, B, pos, pstride, dLdy, dy_stride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, i0, i1, scale, acc_w);
+		grid_bwd_mode<D, F, H, IDX_HASH_POW2, OPTS>(mode, layout, B, pos, pstride, dLdy, dy_stride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, i0, i1, scale, acc_w, o);
 	else if (kind == IDX_DENSE)
-		grid_bwd_mode<D, F, H, IDX_DENSE>(mode, layout, B, pos, pstride, dLdy, dy_stride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, i0, i1, scale, acc_w);
+		grid_bwd_mode<D, F, H, IDX_DENSE, OPTS>(mode, layout, B, pos, pstride, dLdy, dy_stride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, i0, i1, scale, acc_w, o);
 	else
-		grid_bwd_mode<D, F, H, IDX_GENERIC>(mode, layout, B, pos, pstride, dLdy, dy_stride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, i0, i1, scale, acc_w);
+		grid_bwd_mode<D, F, H, IDX_GENERIC, OPTS>(mode, layout, B, pos, pstride, dLdy, dy_stride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, i0, i1, scale, acc_w, o);
 	__syncthreads();
 	if (R > 1) {  // merge the replicas into replica 0
 		if (mode == 0) {
@@ -466,10 +483,12 @@ template <uint32_t D, uint32_t F, HashType H>
 __global__ __launch_bounds__(256) void k_grid_bwd_input(uint32_t B, uint32_t L, const float* __restrict__ pos, uint32_t pstride,
                                                         const _Float16* __restrict__ table, const _Float16* __restrict__ dLdy,
                                                         int layout, uint32_t dy_stride, float* __restrict__ dx, uint32_t dx_stride,
-                                                        const LevelInfo* __restrict__ levels, uint32_t hash_grid, uint32_t interp_u) {
+                                                        const LevelInfo* __restrict__ levels, uint32_t hash_grid, uint32_t interp_u,
+                                                        const GridOpts o) {
 	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
 	if (i >= B) return;
 	const Interp interp = (Interp)interp_u;
+	const float ml = o.active ? grid_max_level(o, i, F) + 1e-3f : 3.0e38f;
 	float x[D], res[D];
 #pragma unroll
 	for (uint32_t d = 0; d < D; ++d) {
@@ -477,6 +496,7 @@ __global__ __launch_bounds__(256) void k_grid_bwd_input(uint32_t B, uint32_t L, 
 		res[d] = 0.0f;
 	}
 	for (uint32_t l = 0; l < L; ++l) {
+		if ((float)l >= ml) continue;  // masked: dy_dx = 0 (grid.h:75-91)
 		const LevelInfo li = levels[l];
 		float p[D], pd[D];
 		uint32_t pg[D];
@@ -538,38 +558,38 @@ __global__ __launch_bounds__(256) void k_grid_bwd_input(uint32_t B, uint32_t L, 
 template <uint32_t D, uint32_t F>
 static void grid_bwd_input_h(hipStream_t st, HashType h, dim3 g, uint32_t B, uint32_t L, const float* pos, uint32_t ps, const _Float16* t,
                              const _Float16* dy, int layout, uint32_t dys, float* dx, uint32_t dxs, const LevelInfo* lv, uint32_t hg,
-                             uint32_t in) {
+                             uint32_t in, const GridOpts& go) {
 	switch (h) {
-		case HashType::Prime: hipLaunchKernelGGL((k_grid_bwd_input<D, F, HashType::Prime>), g, dim3(256), 0, st, B, L, pos, ps, t, dy, layout, dys, dx, dxs, lv, hg, in); break;
-		case HashType::ReversedPrime: hipLaunchKernelGGL((k_grid_bwd_input<D, F, HashType::ReversedPrime>), g, dim3(256), 0, st, B, L, pos, ps, t, dy, layout, dys, dx, dxs, lv, hg, in); break;
-		default: hipLaunchKernelGGL((k_grid_bwd_input<D, F, HashType::CoherentPrime>), g, dim3(256), 0, st, B, L, pos, ps, t, dy, layout, dys, dx, dxs, lv, hg, in); break;
+		case HashType::Prime: hipLaunchKernelGGL((k_grid_bwd_input<D, F, HashType::Prime>), g, dim3(256), 0, st, B, L, pos, ps, t, dy, layout, dys, dx, dxs, lv, hg, in, go); break;
+		case HashType::ReversedPrime: hipLaunchKernelGGL((k_grid_bwd_input<D, F, HashType::ReversedPrime>), g, dim3(256), 0, st, B, L, pos, ps, t, dy, layout, dys, dx, dxs, lv, hg, in, go); break;
+		default: hipLaunchKernelGGL((k_grid_bwd_input<D, F, HashType::CoherentPrime>), g, dim3(256), 0, st, B, L, pos, ps, t, dy, layout, dys, dx, dxs, lv, hg, in, go); break;
 	}
 }
 
 template <uint32_t D>
 static void grid_bwd_input_f(hipStream_t st, uint32_t F, HashType h, dim3 g, uint32_t B, uint32_t L, const float* pos, uint32_t ps,
                              const _Float16* t, const _Float16* dy, int layout, uint32_t dys, float* dx, uint32_t dxs,
-                             const LevelInfo* lv, uint32_t hg, uint32_t in) {
+                             const LevelInfo* lv, uint32_t hg, uint32_t in, const GridOpts& go) {
 	switch (F) {
-		case 1: grid_bwd_input_h<D, 1>(st, h, g, B, L, pos, ps, t, dy, layout, dys, dx, dxs, lv, hg, in); break;
-		case 2: grid_bwd_input_h<D, 2>(st, h, g, B, L, pos, ps, t, dy, layout, dys, dx, dxs, lv, hg, in); break;
-		case 4: grid_bwd_input_h<D, 4>(st, h, g, B, L, pos, ps, t, dy, layout, dys, dx, dxs, lv, hg, in); break;
-		case 8: grid_bwd_input_h<D, 8>(st, h, g, B, L, pos, ps, t, dy, layout, dys, dx, dxs, lv, hg, in); break;
+		case 1: grid_bwd_input_h<D, 1>(st, h, g, B, L, pos, ps, t, dy, layout, dys, dx, dxs, lv, hg, in, go); break;
+		case 2: grid_bwd_input_h<D, 2>(st, h, g, B, L, pos, ps, t, dy, layout, dys, dx, dxs, lv, hg, in, go); break;
+		case 4: grid_bwd_input_h<D, 4>(st, h, g, B, L, pos, ps, t, dy, layout, dys, dx, dxs, lv, hg, in, go); break;
+		case 8: grid_bwd_input_h<D, 8>(st, h, g, B, L, pos, ps, t, dy, layout, dys, dx, dxs, lv, hg, in, go); break;
 		default: throw std::runtime_error("GridEncoding: n_features_per_level must be 1, 2, 4 or 8");
 	}
 }
 
 void launch_grid_bwd_input(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_t B, uint32_t L, const float* pos,
                            uint32_t pos_stride, const void* table16, const void* dLdy16, int dy_layout, uint32_t dy_stride, float* dx,
-                           uint32_t dx_stride, const LevelInfo* levels, bool hash_grid, Interp interp) {
+                           uint32_t dx_stride, const LevelInfo* levels, bool hash_grid, Interp interp, const GridOpts& go) {
 	if (B == 0) return;
 	const dim3 g(div_round_up(B, 256));
 	const _Float16* t = (const _Float16*)table16;
 	const _Float16* dy = (const _Float16*)dLdy16;
 	switch (D) {
-		case 2: grid_bwd_input_f<2>(st, F, h, g, B, L, pos, pos_stride, t, dy, dy_layout, dy_stride, dx, dx_stride, levels, hash_grid, (uint32_t)interp); break;
-		case 3: grid_bwd_input_f<3>(st, F, h, g, B, L, pos, pos_stride, t, dy, dy_layout, dy_stride, dx, dx_stride, levels, hash_grid, (uint32_t)interp); break;
-		case 4: grid_bwd_input_f<4>(st, F, h, g, B, L, pos, pos_stride, t, dy, dy_layout, dy_stride, dx, dx_stride, levels, hash_grid, (uint32_t)interp); break;
+		case 2: grid_bwd_input_f<2>(st, F, h, g, B, L, pos, pos_stride, t, dy, dy_layout, dy_stride, dx, dx_stride, levels, hash_grid, (uint32_t)interp, go); break;
+		case 3: grid_bwd_input_f<3>(st, F, h, g, B, L, pos, pos_stride, t, dy, dy_layout, dy_stride, dx, dx_stride, levels, hash_grid, (uint32_t)interp, go); break;
+		case 4: grid_bwd_input_f<4>(st, F, h, g, B, L, pos, pos_stride, t, dy, dy_layout, dy_stride, dx, dx_stride, levels, hash_grid, (uint32_t)interp, go); break;
 		default: throw std::runtime_error("GridEncoding: number of input dims must be 2, 3 or 4");
 	}
 	TCNN_HIP_CHECK(hipGetLastError());
@@ -591,10 +611,13 @@ __global__ __launch_bounds__(256) void k_grid_bwd_bwd(uint32_t B, uint32_t L, co
                                                       const _Float16* __restrict__ table, const float* __restrict__ gxx,
                                                       const _Float16* __restrict__ dLdy, uint32_t dy_stride, float* __restrict__ grad,
                                                       _Float16* __restrict__ dLddLdy, uint32_t ddy_stride, float* __restrict__ dx,
-                                                      const LevelInfo* __restrict__ levels, uint32_t hash_grid, uint32_t interp_u) {
+                                                      const LevelInfo* __restrict__ levels, uint32_t hash_grid, uint32_t interp_u,
+                                                      const GridOpts o) {
 	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
 	if (i >= B) return;
 	const Interp interp = (Interp)interp_u;
+	// forward-side mask (dy_dx = 0, grid.h:75) uses >=, the second-order kernels > (grid.h:382, 488)
+	const float ml = o.active ? grid_max_level(o, i, F) + 1e-3f : 3.0e38f;
 	float x[D], gx[D], res[D];
 #pragma unroll
 	for (uint32_t d = 0; d < D; ++d) {
@@ -610,7 +633,8 @@ __global__ __launch_bounds__(256) void k_grid_bwd_bwd(uint32_t B, uint32_t L, co
 		float ddy[F];
 #pragma unroll
 		for (uint32_t f = 0; f < F; ++f) ddy[f] = 0.0f;
-		if (interp != Interp::Nearest) {  // nearest: dy/dx == 0, so every second-order term is 0
+		const bool fwd_masked = (float)l >= ml;
+		if (interp != Interp::Nearest && !((float)l > ml)) {  // nearest: dy/dx == 0, so every second-order term is 0
 			const float s = li.scale;
 			float p[D], pd[D], pd2[D];
 			uint32_t pg[D];
@@ -676,7 +700,7 @@ __global__ __launch_bounds__(256) void k_grid_bwd_bwd(uint32_t B, uint32_t L, co
 		}
 		if (dLddLdy)
 #pragma unroll
-			for (uint32_t f = 0; f < F; ++f) dLddLdy[(size_t)i * ddy_stride + l * F + f] = (_Float16)ddy[f];
+			for (uint32_t f = 0; f < F; ++f) dLddLdy[(size_t)i * ddy_stride + l * F + f] = (_Float16)(fwd_masked ? 0.0f : ddy[f]);
 	}
 	if (dLddLdy)
 		for (uint32_t k = L * F; k < ddy_stride; ++k) dLddLdy[(size_t)i * ddy_stride + k] = (_Float16)0.0f;
@@ -688,8 +712,8 @@ __global__ __launch_bounds__(256) void k_grid_bwd_bwd(uint32_t B, uint32_t L, co
 template <uint32_t D, uint32_t F>
 static void grid_bwd_bwd_h(hipStream_t st, HashType h, dim3 g, uint32_t B, uint32_t L, const float* pos, uint32_t ps,
                            const _Float16* t, const float* gx, const _Float16* dy, uint32_t dys, float* grad, _Float16* ddy,
-                           uint32_t ddys, float* dx, const LevelInfo* lv, uint32_t hg, uint32_t in) {
-#define GBB_LAUNCH(HH) hipLaunchKernelGGL((k_grid_bwd_bwd<D, F, HH>), g, dim3(256), 0, st, B, L, pos, ps, t, gx, dy, dys, grad, ddy, ddys, dx, lv, hg, in)
+                           uint32_t ddys, float* dx, const LevelInfo* lv, uint32_t hg, uint32_t in, const GridOpts& go) {
+#define GBB_LAUNCH(HH) hipLaunchKernelGGL((k_grid_bwd_bwd<D, F, HH>), g, dim3(256), 0, st, B, L, pos, ps, t, gx, dy, dys, grad, ddy, ddys, dx, lv, hg, in, go)
 	switch (h) {
 		case HashType::Prime: GBB_LAUNCH(HashType::Prime); break;
 		case HashType::ReversedPrime: GBB_LAUNCH(HashType::ReversedPrime); break;
@@ -701,12 +725,12 @@ static void grid_bwd_bwd_h(hipStream_t st, HashType h, dim3 g, uint32_t B, uint3
 template <uint32_t D>
 static void grid_bwd_bwd_f(hipStream_t st, uint32_t F, HashType h, dim3 g, uint32_t B, uint32_t L, const float* pos, uint32_t ps,
                            const _Float16* t, const float* gx, const _Float16* dy, uint32_t dys, float* grad, _Float16* ddy,
-                           uint32_t ddys, float* dx, const LevelInfo* lv, uint32_t hg, uint32_t in) {
+                           uint32_t ddys, float* dx, const LevelInfo* lv, uint32_t hg, uint32_t in, const GridOpts& go) {
 	switch (F) {
-		case 1: grid_bwd_bwd_h<D, 1>(st, h, g, B, L, pos, ps, t, gx, dy, dys, grad, ddy, ddys, dx, lv, hg, in); break;
-		case 2: grid_bwd_bwd_h<D, 2>(st, h, g, B, L, pos, ps, t, gx, dy, dys, grad, ddy, ddys, dx, lv, hg, in); break;
-		case 4: grid_bwd_bwd_h<D, 4>(st, h, g, B, L, pos, ps, t, gx, dy, dys, grad, ddy, ddys, dx, lv, hg, in); break;
-		case 8: grid_bwd_bwd_h<D, 8>(st, h, g, B, L, pos, ps, t, gx, dy, dys, grad, ddy, ddys, dx, lv, hg, in); break;
+		case 1: grid_bwd_bwd_h<D, 1>(st, h, g, B, L, pos, ps, t, gx, dy, dys, grad, ddy, ddys, dx, lv, hg, in, go); break;
+		case 2: grid_bwd_bwd_h<D, 2>(st, h, g, B, L, pos, ps, t, gx, dy, dys, grad, ddy, ddys, dx, lv, hg, in, go); break;
+		case 4: grid_bwd_bwd_h<D, 4>(st, h, g, B, L, pos, ps, t, gx, dy, dys, grad, ddy, ddys, dx, lv, hg, in, go); break;
+		case 8: grid_bwd_bwd_h<D, 8>(st, h, g, B, L, pos, ps, t, gx, dy, dys, grad, ddy, ddys, dx, lv, hg, in, go); break;
 		default: throw std::runtime_error("GridEncoding: n_features_per_level must be 1, 2, 4 or 8");
 	}
 }
@@ -714,7 +738,7 @@ static void grid_bwd_bwd_f(hipStream_t st, uint32_t F, HashType h, dim3 g, uint3
 void launch_grid_bwd_bwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_t B, uint32_t L, const float* pos,
                          uint32_t pos_stride, const void* table16, const float* dL_ddLdx, const void* dLdy16, uint32_t dy_stride,
                          float* grad32, void* dLddLdy16, uint32_t ddy_stride, float* dx, const LevelInfo* levels, bool hash_grid,
-                         Interp interp) {
+                         Interp interp, const GridOpts& go) {
 	if (B == 0) return;
 	const dim3 g(div_round_up(B, 256));
 	const _Float16* t = (const _Float16*)table16;
@@ -722,9 +746,9 @@ void launch_grid_bwd_bwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uin
 	_Float16* ddy = (_Float16*)dLddLdy16;
 	const uint32_t hg = hash_grid ? 1u : 0u, in = (uint32_t)interp;
 	switch (D) {
-		case 2: grid_bwd_bwd_f<2>(st, F, h, g, B, L, pos, pos_stride, t, dL_ddLdx, dy, dy_stride, grad32, ddy, ddy_stride, dx, levels, hg, in); break;
-		case 3: grid_bwd_bwd_f<3>(st, F, h, g, B, L, pos, pos_stride, t, dL_ddLdx, dy, dy_stride, grad32, ddy, ddy_stride, dx, levels, hg, in); break;
-		case 4: grid_bwd_bwd_f<4>(st, F, h, g, B, L, pos, pos_stride, t, dL_ddLdx, dy, dy_stride, grad32, ddy, ddy_stride, dx, levels, hg, in); break;
+		case 2: grid_bwd_bwd_f<2>(st, F, h, g, B, L, pos, pos_stride, t, dL_ddLdx, dy, dy_stride, grad32, ddy, ddy_stride, dx, levels, hg, in, go); break;
+		case 3: grid_bwd_bwd_f<3>(st, F, h, g, B, L, pos, pos_stride, t, dL_ddLdx, dy, dy_stride, grad32, ddy, ddy_stride, dx, levels, hg, in, go); break;
+		case 4: grid_bwd_bwd_f<4>(st, F, h, g, B, L, pos, pos_stride, t, dL_ddLdx, dy, dy_stride, grad32, ddy, ddy_stride, dx, levels, hg, in, go); break;
 		default: throw std::runtime_error("GridEncoding: number of input dims must be 2, 3 or 4");
 	}
 	TCNN_HIP_CHECK(hipGetLastError());
@@ -734,6 +758,7 @@ struct GridBwdLaunch {
 	uint32_t n_items, n_chunks;
 	GridBwdEpilogue ep;
 	unsigned long long* dbg_times;
+	GridOpts opts;
 };
 
 // Diagnostic (TCNN_DEBUG_GRID_TIMES=1): per-workgroup start/end wall clock of the grid backward,
@@ -748,13 +773,19 @@ template <uint32_t D, uint32_t F, HashType H>
 static void grid_bwd_t(hipStream_t st, int layout, uint32_t dys, dim3 g, size_t lds, uint32_t B, const float* pos, uint32_t ps,
                        const _Float16* dy, const GridSlice* sl, float* part, uint32_t pstr, const LevelInfo* lv,
                        uint32_t hg, uint32_t in, uint32_t ppc, const GridBwdLaunch& gl) {
+	// the options (max_level, stochastic) are a separate instantiation: the default kernel stays lean
 	static bool attr = false;
 	if (!attr) {
-		TCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k_grid_bwd_lds<D, F, H>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GRID_BWD_LDS_BYTES));
+		TCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k_grid_bwd_lds<D, F, H, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GRID_BWD_LDS_BYTES));
+		TCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k_grid_bwd_lds<D, F, H, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GRID_BWD_LDS_BYTES));
 		attr = true;
 	}
-	hipLaunchKernelGGL((k_grid_bwd_lds<D, F, H>), g, dim3(GRID_BWD_THREADS), lds, st, layout, B, pos, ps, dy, dys, sl, part, pstr, lv, hg, in, ppc,
-	                   gl.n_items, gl.n_chunks, gl.ep, gl.dbg_times);
+	if (gl.opts.active)
+		hipLaunchKernelGGL((k_grid_bwd_lds<D, F, H, true>), g, dim3(GRID_BWD_THREADS), lds, st, layout, B, pos, ps, dy, dys, sl, part, pstr, lv, hg, in,
+		                   ppc, gl.n_items, gl.n_chunks, gl.ep, gl.dbg_times, gl.opts);
+	else
+		hipLaunchKernelGGL((k_grid_bwd_lds<D, F, H, false>), g, dim3(GRID_BWD_THREADS), lds, st, layout, B, pos, ps, dy, dys, sl, part, pstr, lv, hg, in,
+		                   ppc, gl.n_items, gl.n_chunks, gl.ep, gl.dbg_times, gl.opts);
 }
 
 template <uint32_t D, uint32_t F>
@@ -784,7 +815,7 @@ static void grid_bwd_f(hipStream_t st, uint32_t F, HashType h, int pairs, uint32
 void launch_grid_bwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_t B, const float* pos,
                      uint32_t pos_stride, const void* dLdy16, int dy_layout, uint32_t dy_stride, const GridSlice* slices,
                      uint32_t n_slices, uint32_t n_chunks, float* partial, uint32_t partial_stride,
-                     const LevelInfo* levels, bool hash_grid, Interp interp, const GridBwdEpilogue* ep) {
+                     const LevelInfo* levels, bool hash_grid, Interp interp, const GridBwdEpilogue* ep, const GridOpts& go) {
 	if (B == 0 || n_slices == 0) return;
 	const uint32_t ppc = div_round_up(B, n_chunks);
 	GridBwdLaunch gl{};
@@ -793,6 +824,7 @@ void launch_grid_bwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_
 	if (ep) gl.ep = *ep;
 	else gl.ep.enabled = 0;
 	gl.dbg_times = nullptr;
+	gl.opts = go;
 	const uint32_t n_tail = (ep && ep->enabled) ? ep->n_mlp_groups : 0u;
 	dim3 g(n_slices * n_chunks + n_tail);
 	if (dbg_grid_times()) gl.dbg_times = (unsigned long long*)g_dbg_times.get((size_t)g.x * 16);

@@ -79,6 +79,36 @@ __device__ __forceinline__ void pos_fract(float x, float scale, Interp interp, f
 	pos = p;
 }
 
+// max_level in levels for point i: (max_level * num_grid_features) / F (grid.h:69-73)
+__device__ __forceinline__ float grid_max_level(const GridOpts& o, uint32_t i, uint32_t F) {
+	const float ml = o.max_level_gpu ? o.max_level_gpu[i] : o.max_level;
+	return (ml * (float)o.n_features) / (float)F;
+}
+
+// random_val(1337, idx) (common_device.h:333-337): pcg32{1337} (initseq 1, pcg32.h:45), advance(idx),
+// next_float() -- pcg32.h:53-69, 100-110, 139-158.
+__device__ __forceinline__ float random_val_1337(uint32_t idx) {
+	constexpr uint64_t MULT = 0x5851f42d4c957f2dULL, INC = (1ull << 1) | 1u;
+	uint64_t state = 0u;
+	state = state * MULT + INC;
+	state += 1337u;
+	state = state * MULT + INC;
+	uint64_t cur_mult = MULT, cur_plus = INC, acc_mult = 1u, acc_plus = 0u;
+	for (uint64_t delta = idx; delta > 0; delta >>= 1) {
+		if (delta & 1u) {
+			acc_mult *= cur_mult;
+			acc_plus = acc_plus * cur_mult + cur_plus;
+		}
+		cur_plus = (cur_mult + 1u) * cur_plus;
+		cur_mult *= cur_mult;
+	}
+	const uint64_t old = acc_mult * state + acc_plus;
+	const uint32_t xorshifted = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+	const uint32_t rot = (uint32_t)(old >> 59u);
+	const uint32_t u = ((xorshifted >> rot) | (xorshifted << ((~rot + 1u) & 31))) >> 9 | 0x3f800000u;
+	return __builtin_bit_cast(float, u) - 1.0f;
+}
+
 // Corner indices (absolute entry index) and fp16 weights of one level; no memory access, so a
 // caller can issue the gathers of many levels back to back before consuming any of them.
 template <uint32_t D, HashType H>

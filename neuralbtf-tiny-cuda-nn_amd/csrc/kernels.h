@@ -126,7 +126,7 @@ void launch_trim_cast(hipStream_t st, uint32_t B, uint32_t in_stride, uint32_t n
 // AoS [i*out_stride + l*F + f].
 void launch_grid_fwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_t B, uint32_t L,
                      const float* pos, uint32_t pos_stride, const void* table16, void* out16, bool soa,
-                     uint32_t out_stride, const LevelInfo* levels, bool hash_grid, Interp interp);
+                     uint32_t out_stride, const LevelInfo* levels, bool hash_grid, Interp interp, const GridOpts& opts = GridOpts{});
 
 // Grid backward: dLdy layout 0 = level-major pairs ([l][i][F] halves), 1 = SoA ([(l*F+f)*B + i]),
 // 2 = AoS ([i*dy_stride + l*F + f]).
@@ -134,19 +134,20 @@ uint32_t grid_bwd_slot_budget();
 void launch_grid_bwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_t B, const float* pos,
                      uint32_t pos_stride, const void* dLdy16, int dy_layout, uint32_t dy_stride, const GridSlice* slices,
                      uint32_t n_slices, uint32_t n_chunks, float* partial, uint32_t partial_stride,
-                     const LevelInfo* levels, bool hash_grid, Interp interp, const GridBwdEpilogue* ep = nullptr);
+                     const LevelInfo* levels, bool hash_grid, Interp interp, const GridBwdEpilogue* ep = nullptr,
+                     const GridOpts& opts = GridOpts{});
 // dL/dx fp32 [B][dx_stride] through the grid (reference grid.h:171-211 + 322-349), dy_dx recomputed
 // from the table; dLdy in the launch_grid_bwd layouts.
 void launch_grid_bwd_input(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_t B, uint32_t L, const float* pos,
                            uint32_t pos_stride, const void* table16, const void* dLdy16, int dy_layout, uint32_t dy_stride, float* dx,
-                           uint32_t dx_stride, const LevelInfo* levels, bool hash_grid, Interp interp);
+                           uint32_t dx_stride, const LevelInfo* levels, bool hash_grid, Interp interp, const GridOpts& opts = GridOpts{});
 // Second-order grid gradients (reference grid.h:351-627, 902-1026): from dL/d(dL/dx) fp32 [B][D]
 // and dL/dy (AoS fp16 [B][dy_stride], nullable) -> grad32 += dL/dgrid (fp32 atomics, nullable),
 // dL/d(dL/dy) AoS fp16 [B][ddy_stride] (nullable), dL/dx fp32 [B][D] (nullable).
 void launch_grid_bwd_bwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_t B, uint32_t L, const float* pos,
                          uint32_t pos_stride, const void* table16, const float* dL_ddLdx, const void* dLdy16, uint32_t dy_stride,
                          float* grad32, void* dLddLdy16, uint32_t ddy_stride, float* dx, const LevelInfo* levels, bool hash_grid,
-                         Interp interp);
+                         Interp interp, const GridOpts& opts = GridOpts{});
 // fused weight-image geometry (FusedLayout) for the epilogue
 void fused_image_layout(uint32_t W, uint32_t IN, uint32_t NH, uint32_t* RSI, uint32_t* RSW, uint32_t* oWh, uint32_t* oWo);
 

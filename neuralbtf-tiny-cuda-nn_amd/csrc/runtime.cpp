@@ -368,10 +368,10 @@ void EncodingHost::forward_aos(hipStream_t st, uint32_t B, const float* x, const
 		case EncKind::OneBlob: launch_oneblob_fwd(st, B, n_dims, n_bins, x, n_dims, out16, W, n_to_pad); break;
 		case EncKind::Identity: launch_identity_fwd(st, B, n_dims, scale, offset, x, n_dims, out16, W, n_to_pad); break;
 		default:
-			TCNN_CHECK(!grid->stochastic, "stochastic_interpolation is not implemented by the MI355X engine yet");
 			if (grid->n_to_pad) TCNN_HIP_CHECK(hipMemsetAsync(out16, 0, (size_t)B * W * 2, st));
 			launch_grid_fwd(st, grid->desc.n_pos_dims, grid->desc.n_features_per_level, grid->desc.hash_type, B, grid->desc.n_levels, x,
-			                grid->desc.n_pos_dims, params16, out16, false, W, grid->dev_levels(), grid->hash_grid(), grid->desc.interp);
+			                grid->desc.n_pos_dims, params16, out16, false, W, grid->dev_levels(), grid->hash_grid(), grid->desc.interp,
+			                grid->opts());
 	}
 }
 
@@ -384,7 +384,7 @@ void EncodingHost::backward_input(hipStream_t st, uint32_t B, const float* x, co
 			TCNN_CHECK(params16, "grid backward_input needs the grid parameters");
 			launch_grid_bwd_input(st, grid->desc.n_pos_dims, grid->desc.n_features_per_level, grid->desc.hash_type, B, grid->desc.n_levels,
 			                      x, grid->desc.n_pos_dims, params16, dy16, 2, W, dx, n_dims, grid->dev_levels(), grid->hash_grid(),
-			                      grid->desc.interp);
+			                      grid->desc.interp, grid->opts());
 	}
 }
 
@@ -403,7 +403,7 @@ NetworkHost::NetworkHost(uint32_t n_in, uint32_t n_out, const json& e, const jso
 bool NetworkHost::fused_ok() const {
 	// CutlassMLP / "MLP" run on the layer-wise engine (the reference's separate GEMM-per-layer network)
 	const bool ff = ieq(mlp.otype, "FullyFusedMLP") || ieq(mlp.otype, "MegakernelMLP");
-	return ff && grid && grid->n_to_pad == 0 && !grid->stochastic && mlp.output_activation == 0 &&
+	return ff && grid && grid->n_to_pad == 0 && !grid->opts().active && mlp.output_activation == 0 &&
 	       (mlp.activation == ACT_NONE || mlp.activation == ACT_RELU) &&
 	       fused_train_supported(mlp.width, mlp.n_input, mlp.n_hidden_layers, grid->desc.n_pos_dims,
 	                             grid->desc.n_features_per_level, mlp.padded_output, mlp.activation, grid->desc.hash_type);
@@ -594,7 +594,8 @@ void NetworkHost::fwd_bwd_layered(hipStream_t st, StepWorkspace& ws, uint32_t B,
 		ws.grid_partial.reserve((size_t)n_chunks * grid->n_params * 4);
 		launch_grid_bwd(st, grid->desc.n_pos_dims, grid->desc.n_features_per_level, grid->desc.hash_type, B, pos,
 		                grid->desc.n_pos_dims, dnext, 2, IN, grid->d_slices.as<GridSlice>(), (uint32_t)grid->slices.size(), n_chunks,
-		                ws.grid_partial.as<float>(), grid->n_params, grid->dev_levels(), grid->hash_grid(), grid->desc.interp);
+		                ws.grid_partial.as<float>(), grid->n_params, grid->dev_levels(), grid->hash_grid(), grid->desc.interp, nullptr,
+		                grid->opts());
 		launch_grid_slab_reduce(st, ws.grid_partial.as<float>(), n_chunks, grid->n_params, grid->n_params, grad32 + n_mlp,
 		                        grid->slab_map());
 	}

@@ -53,6 +53,8 @@ struct GridEncodingHost {
 	uint32_t n_to_pad = 0;       // alignment padding (reference set_padded_output_width)
 	uint32_t n_params = 0;       // offset[L] * F
 	bool stochastic = false;
+	float max_level = 1000.0f;              // GridEncoding::set_max_level (grid_interface.h:101-107)
+	const float* max_level_gpu = nullptr;   // set_max_level_gpu: [B] per point (grid_interface.h:109-123)
 	std::vector<LevelInfo> levels;
 	std::vector<GridSlice> slices;
 	DevBuf d_levels, d_slices, d_slab_map;
@@ -65,6 +67,16 @@ struct GridEncodingHost {
 	void initialize_params(Pcg32& rng, float* host_out, float scale = 1.0f) const;
 	json hyperparams() const;
 	const LevelInfo* dev_levels() const { return d_levels.as<LevelInfo>(); }
+	GridOpts opts() const {
+		GridOpts o;
+		o.max_level = max_level;
+		o.max_level_gpu = max_level_gpu;
+		o.stochastic = stochastic ? 1u : 0u;
+		o.n_features = n_features;
+		const float t = (max_level * (float)n_features) / (float)desc.n_features_per_level + 1e-3f;
+		o.active = (stochastic || max_level_gpu || (float)(desc.n_levels - 1) >= t) ? 1u : 0u;
+		return o;
+	}
 	const GridSlabMap* slab_map() const { return d_slab_map.as<GridSlabMap>(); }
 	// point chunks of the backward: items x chunks workgroups of 1024 threads (one per CU: 128 KiB
 	// of LDS each) fit the CUs left after `reserved` other workgroups in ONE round, with one chunk of

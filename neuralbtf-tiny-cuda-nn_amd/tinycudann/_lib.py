@@ -33,6 +33,10 @@ _SIGS = {
     "tcnn_module_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "tcnn_module_backward_backward_input": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32] + [c_void_p] * 7),
     "tcnn_context_destroy": (None, [c_void_p]),
+    "tcnn_module_set_max_level": (c_int, [c_void_p, c_float]),
+    "tcnn_module_max_level": (c_float, [c_void_p]),
+    "tcnn_module_set_max_level_gpu": (c_int, [c_void_p, c_void_p]),
+    "tcnn_trainer_set_max_level": (c_int, [c_void_p, c_float]),
     "tcnn_module_n_input_dims": (c_uint32, [c_void_p]),
     "tcnn_module_n_output_dims": (c_uint32, [c_void_p]),
     "tcnn_module_n_params": (c_uint64, [c_void_p]),

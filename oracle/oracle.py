@@ -29,6 +29,8 @@ class GridCfg(ctypes.Structure):
         ("grid_type", ctypes.c_uint32), ("hash_type", ctypes.c_uint32), ("interpolation", ctypes.c_uint32),
         ("offsets", ctypes.c_uint32 * (MAX_LEVELS + 1)), ("scales", ctypes.c_float * MAX_LEVELS),
         ("res", ctypes.c_uint32 * MAX_LEVELS), ("n_params", ctypes.c_uint32),
+        ("opts", ctypes.c_uint32), ("max_level", ctypes.c_float), ("max_level_gpu", ctypes.c_void_p),
+        ("stochastic", ctypes.c_uint32),
     ]
 
 
@@ -72,6 +74,8 @@ def lib():
         _lib.orc_pcg32_advance.argtypes = [ctypes.POINTER(Pcg32), ctypes.c_int64]
         _lib.orc_generate_uniform.argtypes = [ctypes.POINTER(Pcg32), ctypes.c_size_t, ctypes.c_void_p, ctypes.c_float, ctypes.c_float]
         _lib.orc_xavier_uniform.argtypes = [ctypes.POINTER(Pcg32), ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_float]
+        _lib.orc_random_val.restype = ctypes.c_float
+        _lib.orc_random_val.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
         _lib.orc_grid_index.restype = ctypes.c_uint32
         _lib.orc_grid_index.argtypes = [ctypes.POINTER(GridCfg), ctypes.c_uint32, ctypes.c_void_p]
         _lib.orc_coherent_prime_hash.restype = ctypes.c_uint32
@@ -137,8 +141,23 @@ def grid_cfg(enc, n_pos_dims):
     g.grid_type = GRID_TYPES[gtype]
     g.hash_type = HASH_TYPES[enc.get("hash", "CoherentPrime").lower()]
     g.interpolation = INTERP[enc.get("interpolation", "Linear").lower()]
+    g.stochastic = int(bool(enc.get("stochastic_interpolation", False)))
+    g.max_level = 1000.0
+    g.opts = g.stochastic
     assert lib().orc_grid_init(ctypes.byref(g)) == 0
     return g
+
+
+def grid_set_max_level(g, max_level, per_point=None):
+    """GridEncoding::set_max_level / set_max_level_gpu (grid_interface.h:101-123); per_point must be
+    kept alive by the caller while g is used."""
+    g.max_level = float(max_level)
+    g.max_level_gpu = per_point.ctypes.data if per_point is not None else None
+    g.opts = 1
+
+
+def random_val(seed, idx):
+    return lib().orc_random_val(seed, idx)
 
 
 def adam_cfg(opt):

@@ -302,6 +302,22 @@ static void pos_fract(float x, float scale, int smooth, float* pos, uint32_t* gr
 }
 
 /* kernel_grid, grid.h:48-212 (encoded_positions part; dy_dx not restated here) */
+float orc_random_val(uint32_t seed, uint32_t idx) {
+	orc_pcg32 r;
+	orc_pcg32_seed(&r, seed, 1u);
+	orc_pcg32_advance(&r, (int64_t)idx);
+	return orc_pcg32_next_float(&r);
+}
+
+/* max_level in levels for point i: (max_level * num_grid_features) / F (grid.h:69-73) */
+static float orc_max_level(const orc_grid* g, uint32_t i) {
+	const float ml = g->max_level_gpu ? g->max_level_gpu[i] : g->max_level;
+	return (ml * (float)(g->n_levels * g->n_features_per_level)) / (float)g->n_features_per_level;
+}
+/* grid.h:75 (forward, dy_dx) masks level >= max_level + 1e-3; grid.h:242, 382, 488 (backwards) use > */
+static int orc_masked_fwd(const orc_grid* g, uint32_t l, uint32_t i) { return g->opts && (float)l >= orc_max_level(g, i) + 1e-3f; }
+static int orc_masked_bwd(const orc_grid* g, uint32_t l, uint32_t i) { return g->opts && (float)l > orc_max_level(g, i) + 1e-3f; }
+
 void orc_grid_fwd(const orc_grid* g, uint32_t B, const float* pos_in, const uint16_t* table, uint16_t* enc) {
 	const uint32_t D = g->n_pos_dims, F = g->n_features_per_level, L = g->n_levels;
 	for (uint32_t l = 0; l < L; ++l) {
@@ -312,7 +328,9 @@ void orc_grid_fwd(const orc_grid* g, uint32_t B, const float* pos_in, const uint
 			uint32_t pg[8], local[8];
 			for (uint32_t d = 0; d < D; ++d) pos_fract(pos_in[(size_t)i * D + d], scale, g->interpolation == ORC_INTERP_SMOOTHSTEP, &pos[d], &pg[d]);
 			uint16_t result[8] = {0};
-			if (g->interpolation == ORC_INTERP_NEAREST) {
+			if (orc_masked_fwd(g, l, i)) {
+				/* masked level: 0 */
+			} else if (g->interpolation == ORC_INTERP_NEAREST) {
 				uint32_t idx = orc_grid_index(g, l, pg) * F;
 				for (uint32_t f = 0; f < F; ++f) result[f] = grid[idx + f];
 			} else {
@@ -343,8 +361,16 @@ void orc_grid_bwd(const orc_grid* g, uint32_t B, const float* pos_in, const uint
 			uint32_t pg[8], local[8];
 			for (uint32_t d = 0; d < D; ++d) pos_fract(pos_in[(size_t)i * D + d], scale, g->interpolation == ORC_INTERP_SMOOTHSTEP, &pos[d], &pg[d]);
 			for (uint32_t f = 0; f < F; ++f) dy[f] = orc_h2f(dL_dy[(size_t)(l * F + f) * B + i]);
+			if (orc_masked_bwd(g, l, i)) continue;
 			if (g->interpolation == ORC_INTERP_NEAREST) {
 				uint32_t idx = orc_grid_index(g, l, pg) * F;
+				for (uint32_t f = 0; f < F; ++f) gg[idx + f] += dy[f];
+				continue;
+			}
+			if (g->opts && g->stochastic) { /* grid.h:284-298 */
+				const float sample = orc_random_val(1337u, i + l * B);
+				for (uint32_t d = 0; d < D; ++d) local[d] = sample >= pos[d] ? pg[d] : pg[d] + 1;
+				uint32_t idx = orc_grid_index(g, l, local) * F;
 				for (uint32_t f = 0; f < F; ++f) gg[idx + f] += dy[f];
 				continue;
 			}
@@ -372,6 +398,7 @@ void orc_grid_bwd_input(const orc_grid* g, uint32_t B, const float* pos_in, cons
 	for (uint32_t i = 0; i < B; ++i) {
 		float res[8] = {0};
 		for (uint32_t l = 0; l < L; ++l) {
+			if (orc_masked_fwd(g, l, i)) continue; /* dy_dx = 0 */
 			const float scale = g->scales[l];
 			float pos[8], pd[8];
 			uint32_t pg[8], local[8];
@@ -452,9 +479,10 @@ void orc_grid_bwd_bwd(const orc_grid* g, uint32_t B, const float* pos_in, const 
 			for (uint32_t d = 0; d < D; ++d) orc_pos_fract2(g->interpolation, pos_in[(size_t)i * D + d], scale, &p[d], &pd[d], &pd2[d], &pg[d]);
 			for (uint32_t f = 0; f < F; ++f) dy[f] = dL_dy ? orc_h2f(dL_dy[(size_t)(l * F + f) * B + i]) : 0.0f;
 			const uint32_t base = g->offsets[l] * F;
+			const int mfwd = orc_masked_fwd(g, l, i), mbwd = orc_masked_bwd(g, l, i);
 #define ORC_IDX(loc) (base + orc_grid_index(g, l, (loc)) * F)
 			/* (1) dL/dgrid: grid.h:433-454 -- per gradient dim, the 2^(D-1) edges along it */
-			if (grad && dL_dy && linear_like) {
+			if (grad && dL_dy && linear_like && !mbwd) {
 				for (uint32_t gd = 0; gd < D; ++gd) {
 					const float grad_in = scale * gx[gd] * pd[gd];
 					for (uint32_t idx = 0; idx < (1u << (D - 1)); ++idx) {
@@ -479,7 +507,7 @@ void orc_grid_bwd_bwd(const orc_grid* g, uint32_t B, const float* pos_in, const 
 			if (dL_ddLdy) {
 				for (uint32_t f = 0; f < F; ++f) {
 					float r = 0.0f;
-					if (linear_like) {
+					if (linear_like && !mfwd) {
 						for (uint32_t gd = 0; gd < D; ++gd) {
 							float dydx = 0.0f;
 							for (uint32_t idx = 0; idx < (1u << (D - 1)); ++idx) {
@@ -502,7 +530,7 @@ void orc_grid_bwd_bwd(const orc_grid* g, uint32_t B, const float* pos_in, const 
 				}
 			}
 			/* (3) dL/dx through the Hessian of y (grid.h:542-598) */
-			if (dL_dx && dL_dy && linear_like) {
+			if (dL_dx && dL_dy && linear_like && !mbwd) {
 				for (uint32_t gd = 0; gd < D; ++gd) {
 					float out = 0.0f;
 					for (uint32_t idx = 0; idx < (1u << (D - 1)); ++idx) {

@@ -62,10 +62,17 @@ typedef struct {
 	float scales[ORC_MAX_LEVELS];         /* grid_scale (common_device.h:709-714) */
 	uint32_t res[ORC_MAX_LEVELS];         /* grid_resolution (common_device.h:716-718) */
 	uint32_t n_params;                    /* offsets[L] * F */
+	/* options (grid_interface.h:101-123, grid.h:284-298); ignored unless opts != 0 */
+	uint32_t opts;
+	float max_level;                      /* fraction of the levels */
+	const float* max_level_gpu;           /* [B] per point, overrides max_level */
+	uint32_t stochastic;                  /* stochastic interpolation in the backward */
 } orc_grid;
 int orc_grid_init(orc_grid* g);
 uint32_t orc_grid_index(const orc_grid* g, uint32_t level, const uint32_t* pos_grid);
 uint32_t orc_coherent_prime_hash(uint32_t d, const uint32_t* pos_grid);
+/* random_val(seed, idx) (common_device.h:333-337): pcg32{seed}.advance(idx).next_float() */
+float orc_random_val(uint32_t seed, uint32_t idx);
 /* kernel_grid (grid.h:48-212): pos CM [D][B] (pos[i*D+d]); table fp16 [n_params];
  * enc SoA: enc[(l*F+f)*B + i]. */
 void orc_grid_fwd(const orc_grid* g, uint32_t B, const float* pos, const uint16_t* table, uint16_t* enc);

@@ -294,3 +294,74 @@ def test_grid_second_order_matches_float64_derivatives(interp):
     np.testing.assert_allclose(ddy, ref_ddy, rtol=2e-4, atol=2e-4 * np.abs(ref_ddy).max())
     np.testing.assert_allclose(grad, ref_grad, rtol=2e-4, atol=2e-4 * np.abs(ref_grad).max())
     np.testing.assert_allclose(dx, ref_dx, rtol=2e-3, atol=2e-3 * np.abs(ref_dx).max())
+
+
+def _u2f(u):
+    return np.float32(np.uint32((u >> 9) | 0x3F800000).view(np.float32) - np.float32(1.0))
+
+
+def test_random_val_pinned_to_reference_pcg32():
+    """random_val(1337, idx) (common_device.h:333-337) -- the stochastic-interpolation sample --
+    against the reference's own pcg32 known answers (oracle/_ref, tests/golden)."""
+    assert np.float32(O.random_val(1337, 0)) == _u2f(KA["pcg32_1337_next_uint"])
+    assert np.float32(O.random_val(1337, 1)) == np.float32(KA["pcg32_1337_next_float"])
+    assert np.float32(O.random_val(1337, 1000003)) == _u2f(KA["pcg32_1337_advance_1000003_next_uint"])
+
+
+def test_grid_stochastic_backward():
+    """kernel_grid_backward with stochastic_interpolation (grid.h:284-298): each (point, level)
+    sends its whole dL/dy to the one corner picked by random_val(1337, i + level * B)."""
+    enc = dict(CONFIG_HASH["encoding"], n_levels=4, stochastic_interpolation=True)
+    g = O.grid_cfg(enc, 2)
+    assert g.stochastic == 1
+    rng = np.random.default_rng(2)
+    B, F, L = 64, g.n_features_per_level, g.n_levels
+    pos = rng.uniform(0, 1, (B, 2)).astype(np.float32)
+    dy = O.f2h(rng.standard_normal((L * F, B)).astype(np.float32))
+    got = O.grid_bwd(g, pos, dy)
+    ref = np.zeros(g.n_params, np.float64)
+    pg = np.zeros(2, np.uint32)
+    for l in range(L):
+        s = np.float32(g.scales[l])
+        for i in range(B):
+            sample = np.float32(O.random_val(1337, i + l * B))
+            for d in range(2):
+                p = np.float32(np.float64(s) * pos[i, d] + 0.5)  # = fmaf(scale, x, 0.5): one rounding
+                fl = np.floor(p)
+                pg[d] = int(fl) + (0 if sample >= np.float32(p - fl) else 1)
+            idx = O.lib().orc_grid_index(ctypes.byref(g), l, pg.ctypes.data_as(ctypes.c_void_p))
+            o = (g.offsets[l] + idx) * F
+            ref[o:o + F] += O.h2f(dy[l * F:(l + 1) * F, i])
+    np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-6)
+
+
+def test_grid_max_level_masking():
+    """max_level (grid_interface.h:101-123): levels >= max_level * n_levels (+1e-3) output 0 and
+    receive no gradient (grid.h:69-91, 236-244); scalar and per-point variants."""
+    enc = dict(CONFIG_HASH["encoding"])
+    rng = np.random.default_rng(4)
+    g0 = O.grid_cfg(enc, 2)
+    table = O.f2h(rng.uniform(-1, 1, g0.n_params).astype(np.float32))
+    B, F, L = 256, g0.n_features_per_level, g0.n_levels
+    pos = rng.uniform(0, 1, (B, 2)).astype(np.float32)
+    full = O.grid_fwd(g0, pos, table)
+    g = O.grid_cfg(enc, 2)
+    O.grid_set_max_level(g, 0.5)  # 8 levels
+    half = O.grid_fwd(g, pos, table)
+    np.testing.assert_array_equal(half[:9 * F], full[:9 * F])  # level 8 itself stays (8 >= 8.001 is false)
+    assert np.all(half[9 * F:] == 0)
+    per_point = rng.uniform(0, 1, B).astype(np.float32)
+    gp = O.grid_cfg(enc, 2)
+    O.grid_set_max_level(gp, 0.0, per_point)
+    pp = O.grid_fwd(gp, pos, table)
+    for i in range(B):
+        lim = (np.float32(per_point[i]) * np.float32(L * F)) / np.float32(F) + np.float32(1e-3)
+        for l in range(L):
+            exp = 0 if np.float32(l) >= lim else full[l * F:(l + 1) * F, i]
+            np.testing.assert_array_equal(pp[l * F:(l + 1) * F, i], exp)
+    dy = O.f2h(rng.standard_normal((L * F, B)).astype(np.float32))
+    gb = O.grid_bwd(g, pos, dy)
+    gfull = O.grid_bwd(g0, pos, dy)
+    cut = g0.offsets[9] * F
+    np.testing.assert_array_equal(gb[:cut], gfull[:cut])
+    assert np.all(gb[cut:] == 0)
