@@ -229,14 +229,18 @@ static uint32_t pow2_ceil_steps(uint32_t k) {  // 32-wide K steps, rounded up to
 
 static uint32_t layer_blocks(uint32_t B) { return std::max(1u, std::min(div_round_up(B / 32, 4), 1024u)); }
 
-bool layered_width_supported(uint32_t w) { return w == 16 || w == 32 || w == 64 || w == 128; }
+// CutlassMLP widths (reference cutlass_mlp.h:115-121, REQUIRED_ALIGNMENT 16): any multiple of 16 up
+// to 128 (output tiles 1..8; K zero-filled up to 32, 64 or 128).
+bool layered_width_supported(uint32_t w) { return w >= 16 && w <= 128 && w % 16 == 0; }
 
+#define TCNN_KS_DISPATCH(NT_, KSV, CALL)                                                                  \
+	switch (KSV) { case 1: CALL(NT_, 1); break; case 2: CALL(NT_, 2); break; case 4: CALL(NT_, 4); break; default: ok = false; }
 #define TCNN_LAYER_DISPATCH(NTV, KSV, CALL)                                                              \
 	switch (NTV) {                                                                                       \
-		case 1: switch (KSV) { case 1: CALL(1, 1); break; case 2: CALL(1, 2); break; case 4: CALL(1, 4); break; default: ok = false; } break; \
-		case 2: switch (KSV) { case 1: CALL(2, 1); break; case 2: CALL(2, 2); break; case 4: CALL(2, 4); break; default: ok = false; } break; \
-		case 4: switch (KSV) { case 1: CALL(4, 1); break; case 2: CALL(4, 2); break; case 4: CALL(4, 4); break; default: ok = false; } break; \
-		case 8: switch (KSV) { case 1: CALL(8, 1); break; case 2: CALL(8, 2); break; case 4: CALL(8, 4); break; default: ok = false; } break; \
+		case 1: TCNN_KS_DISPATCH(1, KSV, CALL) break; case 2: TCNN_KS_DISPATCH(2, KSV, CALL) break;      \
+		case 3: TCNN_KS_DISPATCH(3, KSV, CALL) break; case 4: TCNN_KS_DISPATCH(4, KSV, CALL) break;      \
+		case 5: TCNN_KS_DISPATCH(5, KSV, CALL) break; case 6: TCNN_KS_DISPATCH(6, KSV, CALL) break;      \
+		case 7: TCNN_KS_DISPATCH(7, KSV, CALL) break; case 8: TCNN_KS_DISPATCH(8, KSV, CALL) break;      \
 		default: ok = false;                                                                             \
 	}
 
@@ -277,18 +281,17 @@ void launch_wgrad(hipStream_t st, uint32_t B, uint32_t N, uint32_t K, const void
 	if (nc < n_chunks) TCNN_HIP_CHECK(hipMemsetAsync(partial + (size_t)nc * N * K, 0, (size_t)(n_chunks - nc) * N * K * 4, st));
 	bool ok = true;
 	const dim3 g(nc);
-	// MT = N / 16 (output tiles), KT = K / 16 (input tiles): both from {1, 2, 4, 8, 16}
+	// MT = N / 16 (output tiles), KT = K / 16 (input tiles): both 1..8
 #define WG(mt, kt) hipLaunchKernelGGL((k_wgrad<mt, kt>), g, dim3(256), 0, st, B, ppc, (const _Float16*)dy16, (const _Float16*)x16, partial)
 #define WGK(mt)                                                                          \
 	switch (K / 16) {                                                                    \
-		case 1: WG(mt, 1); break; case 2: WG(mt, 2); break; case 4: WG(mt, 4); break;    \
-		case 8: WG(mt, 8); break; default: ok = false;       \
+		case 1: WG(mt, 1); break; case 2: WG(mt, 2); break; case 3: WG(mt, 3); break;    \
+		case 4: WG(mt, 4); break; case 5: WG(mt, 5); break; case 6: WG(mt, 6); break;    \
+		case 7: WG(mt, 7); break; case 8: WG(mt, 8); break; default: ok = false;         \
 	}
 	switch (N / 16) {
-		case 1: WGK(1); break;
-		case 2: WGK(2); break;
-		case 4: WGK(4); break;
-		case 8: WGK(8); break;
+		case 1: WGK(1); break; case 2: WGK(2); break; case 3: WGK(3); break; case 4: WGK(4); break;
+		case 5: WGK(5); break; case 6: WGK(6); break; case 7: WGK(7); break; case 8: WGK(8); break;
 		default: ok = false;
 	}
 #undef WGK

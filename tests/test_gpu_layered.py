@@ -47,6 +47,9 @@ CONFIGS = {
     "hashgrid_w128_h4": (_cfg(CONFIG_HASH["encoding"], _net(128, 4)), 2e-3),
     "hashgrid_cutlass_w64_h2": (_cfg(CONFIG_HASH["encoding"], _net(64, 2, "CutlassMLP")), 1e-3),
     "identity_w32_h3": (_cfg({"otype": "Identity"}, _net(32, 3)), 1e-3),
+    # CutlassMLP at widths FullyFusedMLP does not take (any multiple of 16, cutlass_mlp.h:115-121)
+    "hashgrid_cutlass_w48_h3": (_cfg(CONFIG_HASH["encoding"], _net(48, 3, "CutlassMLP")), 1e-3),
+    "oneblob_cutlass_w112_h2": (_cfg({"otype": "OneBlob", "n_bins": 32}, _net(112, 2, "CutlassMLP")), 2e-3),
 }
 
 
