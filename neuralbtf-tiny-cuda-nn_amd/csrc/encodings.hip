@@ -64,6 +64,42 @@ __global__ __launch_bounds__(256) void k_oneblob_fwd(uint32_t B, uint32_t D, uin
 	}
 }
 
+// Same values, 8 bins per thread and one 16-byte store (n_bins >= 8): consecutive threads write
+// consecutive 16 B of a row. Bin b = g + j of the S-bin group g reads cdf(b + 1) for j + 1 < S and
+// cdf(g) (+1 for the dimension's last bin) for the group's last bin, exactly as above.
+__global__ __launch_bounds__(256) void k_oneblob_fwd8(uint32_t B, uint32_t D, uint32_t n_bins, uint32_t log2_bins,
+                                                       const float* __restrict__ x, uint32_t x_stride, _Float16* __restrict__ out,
+                                                       uint32_t out_stride) {
+	const uint32_t per_row = D * (n_bins / 8);
+	const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+	if (t >= B * per_row) return;
+	const uint32_t i = t / per_row, rem = t % per_row;
+	const uint32_t d = rem / (n_bins / 8), b0 = 8 * (rem % (n_bins / 8));
+	const float xv = x[(size_t)i * x_stride + d];
+	const float nb = (float)n_bins;
+	const uint32_t S = n_bins < 32 ? n_bins : 32;
+	const uint32_t g = b0 & ~(S - 1);
+	float left = wrapped_cdf(scalbnf((float)b0, -(int)log2_bins), xv, nb);
+	h8 o;
+#pragma unroll
+	for (uint32_t j = 0; j < 8; ++j) {
+		const uint32_t b = b0 + j;
+		float right;
+		if (b - g + 1 < S) right = wrapped_cdf(scalbnf((float)(b + 1), -(int)log2_bins), xv, nb);
+		else right = wrapped_cdf(scalbnf((float)g, -(int)log2_bins), xv, nb) + (b == n_bins - 1 ? 1.0f : 0.0f);
+		o[j] = (_Float16)(right - left);
+		left = right;
+	}
+	*(h8*)(out + (size_t)i * out_stride + d * n_bins + b0) = o;
+}
+
+__global__ __launch_bounds__(256) void k_fill_pad(uint32_t B, _Float16* __restrict__ out, uint32_t out_stride, uint32_t col0,
+                                                  uint32_t n_pad) {
+	const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+	if (t >= B * n_pad) return;
+	out[(size_t)(t / n_pad) * out_stride + col0 + t % n_pad] = (_Float16)1.0f;
+}
+
 // kernel_one_blob_backward (oneblob.h:116-147): dL/dx[d] = sum_k dL/dy[d*n_bins + k] * (D_left - D_right).
 __global__ __launch_bounds__(256) void k_oneblob_bwd(uint32_t B, uint32_t D, uint32_t n_bins, uint32_t log2_bins,
                                                       const float* __restrict__ x, uint32_t x_stride,
@@ -96,9 +132,18 @@ void launch_oneblob_fwd(hipStream_t st, uint32_t B, uint32_t D, uint32_t n_bins,
                         uint32_t out_stride, uint32_t n_pad) {
 	TCNN_CHECK(n_bins > 0 && (n_bins & (n_bins - 1)) == 0, "Number of bins must be a power of 2");
 	if (!B) return;
-	const uint32_t n = B * (D + (n_pad ? 1 : 0));
-	hipLaunchKernelGGL(k_oneblob_fwd, dim3(div_round_up(n, 256)), dim3(256), 0, st, B, D, n_bins, ilog2(n_bins), x, x_stride,
-	                   (_Float16*)out16, out_stride, n_pad);
+	if (n_bins >= 8 && out_stride % 8 == 0) {
+		const uint32_t n = B * D * (n_bins / 8);
+		hipLaunchKernelGGL(k_oneblob_fwd8, dim3(div_round_up(n, 256)), dim3(256), 0, st, B, D, n_bins, ilog2(n_bins), x, x_stride,
+		                   (_Float16*)out16, out_stride);
+		if (n_pad)
+			hipLaunchKernelGGL(k_fill_pad, dim3(div_round_up(B * n_pad, 256)), dim3(256), 0, st, B, (_Float16*)out16, out_stride,
+			                   D * n_bins, n_pad);
+	} else {
+		const uint32_t n = B * (D + (n_pad ? 1 : 0));
+		hipLaunchKernelGGL(k_oneblob_fwd, dim3(div_round_up(n, 256)), dim3(256), 0, st, B, D, n_bins, ilog2(n_bins), x, x_stride,
+		                   (_Float16*)out16, out_stride, n_pad);
+	}
 	TCNN_HIP_CHECK(hipGetLastError());
 }
 

@@ -18,6 +18,8 @@
 //   k_relative_l2_partial RelativeL2 with per-workgroup loss partial sums
 #include "kernels.h"
 
+#include <type_traits>
+
 #include "mlp_fused.h"
 
 namespace tcnn_amd {
@@ -66,30 +68,53 @@ __device__ __forceinline__ float act_bwd_rt(int a, float g, float y) {
 
 // Stage a row-major [rows][cols] fp16 matrix into LDS with row stride rs, zero-filling columns
 // [cols, zc) (transpose = false), or its transpose [cols][rows] with columns [rows, zc) zeroed.
+// Untransposed rows go 8 halves (16 B) per load when cols % 8 == 0 (every shape here).
 template <bool TRANSPOSE>
 __device__ __forceinline__ void stage_matrix(_Float16* s, const _Float16* __restrict__ m, uint32_t rows, uint32_t cols,
                                              uint32_t rs, uint32_t zc, int tid, int nthr) {
 	if (!TRANSPOSE) {
+		if (cols % 8 == 0) {
+			const uint32_t z8 = zc / 8, c8n = cols / 8;
+			for (uint32_t idx = tid; idx < rows * z8; idx += nthr) {
+				const uint32_t r = idx / z8, c8 = idx % z8;
+				h8 v = h8{0, 0, 0, 0, 0, 0, 0, 0};
+				if (c8 < c8n) v = *(const h8*)(m + (size_t)r * cols + 8 * c8);
+				*(h8*)(s + r * rs + 8 * c8) = v;
+			}
+			return;
+		}
 		for (uint32_t idx = tid; idx < rows * zc; idx += nthr) {
 			const uint32_t r = idx / zc, cc = idx % zc;
 			s[r * rs + cc] = cc < cols ? m[r * cols + cc] : (_Float16)0.0f;
 		}
 	} else {
-		for (uint32_t idx = tid; idx < cols * zc; idx += nthr) {
-			const uint32_t r = idx / zc, cc = idx % zc;  // s[r][cc] = m[cc][r]
-			s[r * rs + cc] = cc < rows ? m[cc * cols + r] : (_Float16)0.0f;
+		// s[r][cc] = m[cc][r]: 16-byte loads along the rows of m, scattered into columns of s
+		if (cols % 8 == 0) {
+			const uint32_t c8n = cols / 8;
+			for (uint32_t idx = tid; idx < rows * c8n; idx += nthr) {
+				const uint32_t cc = idx / c8n, r0 = 8 * (idx % c8n);
+				const h8 v = *(const h8*)(m + (size_t)cc * cols + r0);
+#pragma unroll
+				for (int e = 0; e < 8; ++e) s[(r0 + e) * rs + cc] = v[e];
+			}
+			for (uint32_t idx = tid; idx < cols * (zc - rows); idx += nthr) {
+				const uint32_t r = idx / (zc - rows), cc = rows + idx % (zc - rows);
+				s[r * rs + cc] = (_Float16)0.0f;
+			}
+			return;
+		}
+		for (uint32_t idx = tid; idx < zc * cols; idx += nthr) {
+			const uint32_t cc = idx / cols, r = idx % cols;
+			s[r * rs + cc] = cc < rows ? m[(size_t)cc * cols + r] : (_Float16)0.0f;
 		}
 	}
 }
 
-// One 32-sample slice of  Out[i][16t + 4q + r] = epi( sum_k Amat[16t + c'][k] In[i][k] )  in the
-// transposed MFMA form: A = LDS matrix rows (output features), B = In rows loaded from HBM with
-// 16-byte loads (lane (c, q) of tile tau: sample base + 16 tau + c, k = 32 s + 8 q .. +7).
-template <int NT, int KS, class Epi>
-__device__ __forceinline__ void layer_slice(const _Float16* sA, int rs, const _Float16* __restrict__ in, uint32_t in_stride,
-                                            uint32_t K, uint32_t base, int c, int q, Epi epi) {
-	const f4 fz = {0.0f, 0.0f, 0.0f, 0.0f};
-	h8 xb[2][KS];
+// B operand of one 32-sample slice: lane (c, q) of tile tau holds sample base + 16 tau + c,
+// k = 32 s + 8 q .. +7 (16-byte loads; zero beyond K).
+template <int KS>
+__device__ __forceinline__ void load_slice_rows(h8 (&xb)[2][KS], const _Float16* __restrict__ in, uint32_t in_stride, uint32_t K,
+                                                uint32_t base, int c, int q) {
 #pragma unroll
 	for (int tau = 0; tau < 2; ++tau) {
 		const _Float16* row = in + (size_t)(base + 16 * tau + c) * in_stride;
@@ -100,6 +125,13 @@ __device__ __forceinline__ void layer_slice(const _Float16* sA, int rs, const _F
 			else xb[tau][s] = h8{0, 0, 0, 0, 0, 0, 0, 0};
 		}
 	}
+}
+
+// One 32-sample slice of  Out[i][16t + 4q + r] = epi( sum_k Amat[16t + c'][k] In[i][k] )  in the
+// transposed MFMA form: A = LDS matrix rows (output features), B = the slice's input rows.
+template <int NT, int KS, class Epi>
+__device__ __forceinline__ void layer_slice_mma(const _Float16* sA, int rs, const h8 (&xb)[2][KS], int c, int q, Epi epi) {
+	const f4 fz = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
 	for (int t = 0; t < NT; ++t) {
 		f4 a0 = fz, a1 = fz;
@@ -114,8 +146,59 @@ __device__ __forceinline__ void layer_slice(const _Float16* sA, int rs, const _F
 	}
 }
 
+// Persistent slice loop: the next slice's rows are in flight while this one multiplies.
+template <int NT, int KS, class Epi, class Pre>
+__device__ __forceinline__ void layer_slices(const _Float16* sA, int rs, const _Float16* __restrict__ in, uint32_t in_stride,
+                                             uint32_t K, uint32_t B, int wave, int c, int q, Epi epi, Pre pre) {
+	const uint32_t n_slices = B / 32, stride = gridDim.x * 4;
+	uint32_t sl = blockIdx.x * 4 + wave;
+	if (sl >= n_slices) return;
+	h8 xb[2][KS];
+	load_slice_rows<KS>(xb, in, in_stride, K, sl * 32, c, q);
+	for (; sl < n_slices; sl += stride) {
+		h8 xn[2][KS];
+		const bool more = sl + stride < n_slices;
+		if (more) load_slice_rows<KS>(xn, in, in_stride, K, (sl + stride) * 32, c, q);
+		pre(sl * 32);  // epilogue operands of this slice, in flight during its MFMAs
+		layer_slice_mma<NT, KS>(sA, rs, xb, c, q, [&](int tau, int t, f4 v) { epi(sl * 32, tau, t, v); });
+		if (more) {
+#pragma unroll
+			for (int tau = 0; tau < 2; ++tau)
+#pragma unroll
+				for (int s = 0; s < KS; ++s) xb[tau][s] = xn[tau][s];
+		}
+	}
+}
+
+// Out-of-line activation for the rare activations: the MFMA loops inline only None / ReLU, so
+// the kernels stay a few thousand instructions (inlining every activation per element made them
+// ~22K instructions, far beyond the instruction cache).
+__device__ __noinline__ float act_fwd_ool(int a, float x) { return act_fwd_rt(a, x); }
+__device__ __noinline__ float act_bwd_ool(int a, float g, float y) { return act_bwd_rt(a, g, y); }
+
+template <int A>  // ACT_NONE, ACT_RELU, or -1 (any, out of line)
+__device__ __forceinline__ float act_fwd_sel(int a, float x) {
+	if constexpr (A == ACT_NONE) return x;
+	else if constexpr (A == ACT_RELU) return x > 0.0f ? x : 0.0f;
+	else return act_fwd_ool(a, x);
+}
+template <int A>
+__device__ __forceinline__ float act_bwd_sel(int a, float g, float y) {
+	if constexpr (A == ACT_NONE) return g;
+	else if constexpr (A == ACT_RELU) return y > 0.0f ? g : 0.0f;
+	else return act_bwd_ool(a, g, y);
+}
+
+// run f with the activation as a compile-time constant where it is None / ReLU
+template <class F>
+__device__ __forceinline__ void with_act(int act, F f) {
+	if (act == ACT_NONE) f(std::integral_constant<int, ACT_NONE>{});
+	else if (act == ACT_RELU) f(std::integral_constant<int, ACT_RELU>{});
+	else f(std::integral_constant<int, -1>{});
+}
+
 template <int NT, int KS>
-__global__ __launch_bounds__(256) void k_layer_fwd(uint32_t B, uint32_t K, const _Float16* __restrict__ w,
+__global__ __launch_bounds__(256, 2) void k_layer_fwd(uint32_t B, uint32_t K, const _Float16* __restrict__ w,
                                                     const _Float16* __restrict__ x, _Float16* __restrict__ y, int act) {
 	constexpr int N = 16 * NT, RS = 32 * KS + 8;
 	__shared__ __attribute__((aligned(16))) _Float16 sW[N * RS];
@@ -123,21 +206,19 @@ __global__ __launch_bounds__(256) void k_layer_fwd(uint32_t B, uint32_t K, const
 	const int c = lane & 15, q = lane >> 4;
 	stage_matrix<false>(sW, w, N, K, RS, 32 * KS, tid, 256);
 	__syncthreads();
-	const uint32_t n_slices = B / 32;
-	for (uint32_t sl = blockIdx.x * 4 + wave; sl < n_slices; sl += gridDim.x * 4) {
-		const uint32_t base = sl * 32;
-		layer_slice<NT, KS>(sW, RS, x, K, K, base, c, q, [&](int tau, int t, f4 v) {
+	with_act(act, [&](auto A) {
+		layer_slices<NT, KS>(sW, RS, x, K, K, B, wave, c, q, [&](uint32_t base, int tau, int t, f4 v) {
 			h4 o;
 #pragma unroll
-			for (int r = 0; r < 4; ++r) o[r] = (_Float16)act_fwd_rt(act, v[r]);
+			for (int r = 0; r < 4; ++r) o[r] = (_Float16)act_fwd_sel<decltype(A)::value>(act, v[r]);
 			*(h4*)(y + (size_t)(base + 16 * tau + c) * N + 16 * t + 4 * q) = o;
-		});
-	}
+		}, [](uint32_t) {});
+	});
 }
 
 // dX[i][k] = act'(H[i][k]) * sum_n dY[i][n] W[n][k]; H == nullptr -> no transfer. K = 16 NT.
 template <int NT, int KS>
-__global__ __launch_bounds__(256) void k_layer_bwd(uint32_t B, uint32_t N, const _Float16* __restrict__ w,
+__global__ __launch_bounds__(256, 2) void k_layer_bwd(uint32_t B, uint32_t N, const _Float16* __restrict__ w,
                                                     const _Float16* __restrict__ dy, const _Float16* __restrict__ h,
                                                     _Float16* __restrict__ dx, int act) {
 	constexpr int K = 16 * NT, RS = 32 * KS + 8;
@@ -146,35 +227,46 @@ __global__ __launch_bounds__(256) void k_layer_bwd(uint32_t B, uint32_t N, const
 	const int c = lane & 15, q = lane >> 4;
 	stage_matrix<true>(sWT, w, N, K, RS, 32 * KS, tid, 256);
 	__syncthreads();
-	const uint32_t n_slices = B / 32;
-	for (uint32_t sl = blockIdx.x * 4 + wave; sl < n_slices; sl += gridDim.x * 4) {
-		const uint32_t base = sl * 32;
-		layer_slice<NT, KS>(sWT, RS, dy, N, N, base, c, q, [&](int tau, int t, f4 v) {
+	with_act(h ? act : ACT_NONE, [&](auto A) {
+		constexpr bool TRANSFER = decltype(A)::value != ACT_NONE;
+		h4 hv[2][NT];
+		layer_slices<NT, KS>(sWT, RS, dy, N, N, B, wave, c, q, [&](uint32_t base, int tau, int t, f4 v) {
 			const size_t o = (size_t)(base + 16 * tau + c) * K + 16 * t + 4 * q;
 			h4 r4;
-			if (h) {
-				const h4 hv = *(const h4*)(h + o);
+			if constexpr (TRANSFER) {
 #pragma unroll
-				for (int r = 0; r < 4; ++r) r4[r] = (_Float16)act_bwd_rt(act, v[r], (float)hv[r]);
+				for (int r = 0; r < 4; ++r) r4[r] = (_Float16)act_bwd_sel<decltype(A)::value>(act, v[r], (float)hv[tau][t][r]);
 			} else {
 #pragma unroll
 				for (int r = 0; r < 4; ++r) r4[r] = (_Float16)v[r];
 			}
 			*(h4*)(dx + o) = r4;
+		}, [&](uint32_t base) {
+			if constexpr (TRANSFER) {
+#pragma unroll
+				for (int tau = 0; tau < 2; ++tau)
+#pragma unroll
+					for (int t = 0; t < NT; ++t) hv[tau][t] = *(const h4*)(h + (size_t)(base + 16 * tau + c) * K + 16 * t + 4 * q);
+			}
 		});
-	}
+	});
 }
 
 // Weight-gradient partial of one sample chunk: P[n][k] = sum_{i in chunk} dY[i][n] X[i][k].
-// The workgroup stages 32 samples of dY and X in LDS; wave w owns output tiles w, w+4, ...
-// (MT x KT tiles of 16x16), fp32 accumulators in registers for the whole chunk.
+// 8 waves stage 64 samples of dY and X per step in LDS (double-buffered: the next step's rows are
+// loaded into registers before this step's MFMAs and written to the other buffer after them, so
+// the HBM latency overlaps the math); wave w owns output tiles w, w+8, ... (MT x KT tiles of
+// 16x16) with fp32 accumulators for the whole chunk.
+constexpr int WG_WAVES = 8, WG_STEP = 64;
 template <int MT, int KT>
-__global__ __launch_bounds__(256) void k_wgrad(uint32_t B, uint32_t pts_per_chunk, const _Float16* __restrict__ dy,
-                                                const _Float16* __restrict__ x, float* __restrict__ partial) {
-	constexpr int N = 16 * MT, K = 16 * KT, RSD = N + 8, RSX = K + 8;
-	constexpr int TILES = MT * KT, TPW = (TILES + 3) / 4;
-	__shared__ __attribute__((aligned(16))) _Float16 sD[2][32 * RSD];
-	__shared__ __attribute__((aligned(16))) _Float16 sX[2][32 * RSX];
+__global__ __launch_bounds__(WG_WAVES * 64) void k_wgrad(uint32_t B, uint32_t pts_per_chunk, const _Float16* __restrict__ dy,
+                                                         const _Float16* __restrict__ x, float* __restrict__ partial) {
+	constexpr int N = 16 * MT, K = 16 * KT, RSD = N + 8, RSX = K + 8, NTHR = WG_WAVES * 64;
+	constexpr int TILES = MT * KT, TPW = (TILES + WG_WAVES - 1) / WG_WAVES;
+	constexpr int VD = WG_STEP * N / 8, VX = WG_STEP * K / 8;  // 16-byte vectors per step
+	constexpr int PD = (VD + NTHR - 1) / NTHR, PX = (VX + NTHR - 1) / NTHR;
+	__shared__ __attribute__((aligned(16))) _Float16 sD[2][WG_STEP * RSD];
+	__shared__ __attribute__((aligned(16))) _Float16 sX[2][WG_STEP * RSX];
 	const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 	const int c = lane & 15, q = lane >> 4;
 	const f4 fz = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -183,36 +275,63 @@ __global__ __launch_bounds__(256) void k_wgrad(uint32_t B, uint32_t pts_per_chun
 	for (int m = 0; m < TPW; ++m) acc[m] = fz;
 	const uint32_t i0 = blockIdx.x * pts_per_chunk;
 	const uint32_t i1 = min(B, i0 + pts_per_chunk);
-	auto stage = [&](int buf, uint32_t b0) {
-		for (int idx = tid; idx < 32 * N / 8; idx += 256) {
+	h8 rd[PD], rx[PX];
+	auto load = [&](uint32_t b0) {
+#pragma unroll
+		for (int j = 0; j < PD; ++j) {
+			const int idx = tid + j * NTHR;
 			const int r = idx / (N / 8), c8 = idx % (N / 8);
-			*(uint4*)(&sD[buf][r * RSD + 8 * c8]) = *(const uint4*)(dy + (size_t)(b0 + r) * N + 8 * c8);
+			rd[j] = (idx < VD && b0 + r < i1) ? *(const h8*)(dy + (size_t)(b0 + r) * N + 8 * c8) : h8{0, 0, 0, 0, 0, 0, 0, 0};
 		}
-		for (int idx = tid; idx < 32 * K / 8; idx += 256) {
+#pragma unroll
+		for (int j = 0; j < PX; ++j) {
+			const int idx = tid + j * NTHR;
 			const int r = idx / (K / 8), c8 = idx % (K / 8);
-			*(uint4*)(&sX[buf][r * RSX + 8 * c8]) = *(const uint4*)(x + (size_t)(b0 + r) * K + 8 * c8);
+			rx[j] = (idx < VX && b0 + r < i1) ? *(const h8*)(x + (size_t)(b0 + r) * K + 8 * c8) : h8{0, 0, 0, 0, 0, 0, 0, 0};
+		}
+	};
+	auto store = [&](int buf) {
+#pragma unroll
+		for (int j = 0; j < PD; ++j) {
+			const int idx = tid + j * NTHR;
+			if (idx < VD) *(h8*)(&sD[buf][(idx / (N / 8)) * RSD + 8 * (idx % (N / 8))]) = rd[j];
+		}
+#pragma unroll
+		for (int j = 0; j < PX; ++j) {
+			const int idx = tid + j * NTHR;
+			if (idx < VX) *(h8*)(&sX[buf][(idx / (K / 8)) * RSX + 8 * (idx % (K / 8))]) = rx[j];
 		}
 	};
 	int buf = 0;
-	if (i0 < i1) stage(0, i0);
+	if (i0 < i1) {
+		load(i0);
+		store(0);
+	}
 	__syncthreads();
-	for (uint32_t b0 = i0; b0 < i1; b0 += 32) {
-		if (b0 + 32 < i1) stage(buf ^ 1, b0 + 32);  // next slice lands while this one is consumed
+	for (uint32_t b0 = i0; b0 < i1; b0 += WG_STEP) {
+		const bool more = b0 + WG_STEP < i1;
+		if (more) load(b0 + WG_STEP);
 #pragma unroll
-		for (int m = 0; m < TPW; ++m) {
-			const int j = wave + 4 * m;
-			if (j < TILES) {
-				const int mt = j / KT, kt = j % KT;
-				acc[m] = mfma16(lds_trfrag(sD[buf], RSD, q, c, mt), lds_trfrag(sX[buf], RSX, q, c, kt), acc[m]);
+		for (int h = 0; h < WG_STEP / 32; ++h) {
+			const _Float16* dD = sD[buf] + 32 * h * RSD;
+			const _Float16* dX = sX[buf] + 32 * h * RSX;
+#pragma unroll
+			for (int m = 0; m < TPW; ++m) {
+				const int j = wave + WG_WAVES * m;
+				if (j < TILES) {
+					const int mt = j / KT, kt = j % KT;
+					acc[m] = mfma16(lds_trfrag(dD, RSD, q, c, mt), lds_trfrag(dX, RSX, q, c, kt), acc[m]);
+				}
 			}
 		}
+		if (more) store(buf ^ 1);
 		__syncthreads();
 		buf ^= 1;
 	}
 	float* dst = partial + (size_t)blockIdx.x * N * K;
 #pragma unroll
 	for (int m = 0; m < TPW; ++m) {
-		const int j = wave + 4 * m;
+		const int j = wave + WG_WAVES * m;
 		if (j < TILES) {
 			const int mt = j / KT, kt = j % KT;
 #pragma unroll
@@ -227,7 +346,8 @@ static uint32_t pow2_ceil_steps(uint32_t k) {  // 32-wide K steps, rounded up to
 	return s <= 1 ? 1 : s <= 2 ? 2 : s <= 4 ? 4 : 0;
 }
 
-static uint32_t layer_blocks(uint32_t B) { return std::max(1u, std::min(div_round_up(B / 32, 4), 1024u)); }
+// persistent: two workgroups per CU (the weights are staged once per workgroup)
+static uint32_t layer_blocks(uint32_t B) { return std::max(1u, std::min(div_round_up(B / 32, 4), 512u)); }
 
 // CutlassMLP widths (reference cutlass_mlp.h:115-121, REQUIRED_ALIGNMENT 16): any multiple of 16 up
 // to 128 (output tiles 1..8; K zero-filled up to 32, 64 or 128).
@@ -282,7 +402,7 @@ void launch_wgrad(hipStream_t st, uint32_t B, uint32_t N, uint32_t K, const void
 	bool ok = true;
 	const dim3 g(nc);
 	// MT = N / 16 (output tiles), KT = K / 16 (input tiles): both 1..8
-#define WG(mt, kt) hipLaunchKernelGGL((k_wgrad<mt, kt>), g, dim3(256), 0, st, B, ppc, (const _Float16*)dy16, (const _Float16*)x16, partial)
+#define WG(mt, kt) hipLaunchKernelGGL((k_wgrad<mt, kt>), g, dim3(WG_WAVES * 64), 0, st, B, ppc, (const _Float16*)dy16, (const _Float16*)x16, partial)
 #define WGK(mt)                                                                          \
 	switch (K / 16) {                                                                    \
 		case 1: WG(mt, 1); break; case 2: WG(mt, 2); break; case 3: WG(mt, 3); break;    \
