@@ -253,12 +253,13 @@ tcnn_module* tcnn_create_encoding(uint32_t n_in, const char* enc, int precision)
 void tcnn_module_destroy(tcnn_module* m) { delete m; }
 
 int tcnn_module_inference(tcnn_module* m, void* stream, uint32_t n, const float* in, void* out, const void* params) {
+	if (n == 0) return 0;  // empty batch: nothing to do (every kernel would be a zero-size launch)
 	return guard([&] { m->m->inference((hipStream_t)stream, n, in, out, params); });
 }
 
 tcnn_context* tcnn_module_forward(tcnn_module* m, void* stream, uint32_t n, const float* in, void* out, const void* params, int prep) {
 	return guard_ptr<tcnn_context>([&] {
-		m->m->forward((hipStream_t)stream, n, in, out, params, prep != 0);
+		if (n) m->m->forward((hipStream_t)stream, n, in, out, params, prep != 0);
 		auto* c = new tcnn_context;
 		c->n = n;
 		return c;
@@ -269,6 +270,10 @@ int tcnn_module_backward(tcnn_module* m, void* stream, const tcnn_context* ctx, 
                          void* dL_dparams, const float* in, const void* out, const void* params) {
 	return guard([&] {
 		TCNN_CHECK(ctx != nullptr, "backward: null context");
+		if (n == 0) {  // empty batch: Overwrite-mode gradients are all zero
+			if (dL_dparams) TCNN_HIP_CHECK(hipMemsetAsync(dL_dparams, 0, m->m->n_params() * 2, (hipStream_t)stream));
+			return;
+		}
 		m->m->backward((hipStream_t)stream, n, dL_din, dL_dout, dL_dparams, in, out, params);
 	});
 }
@@ -278,6 +283,10 @@ int tcnn_module_backward_backward_input(tcnn_module* m, void* stream, const tcnn
                                         const void* params) {
 	return guard([&] {
 		TCNN_CHECK(ctx != nullptr, "backward_backward_input: null context");
+		if (n == 0) {
+			if (dL_dparams) TCNN_HIP_CHECK(hipMemsetAsync(dL_dparams, 0, m->m->n_params() * 2, (hipStream_t)stream));
+			return;
+		}
 		m->m->backward_backward_input((hipStream_t)stream, n, dL_ddLdin, in, dL_dout, dL_dparams, dL_ddLdout, dL_din, params);
 	});
 }
@@ -326,7 +335,10 @@ tcnn_trainer* tcnn_trainer_create(uint32_t n_in, uint32_t n_out, const char* cfg
 }
 void tcnn_trainer_destroy(tcnn_trainer* t) { delete t; }
 int tcnn_trainer_training_step(tcnn_trainer* t, void* stream, uint32_t n, const float* in, const float* target, int run_opt) {
-	return guard([&] { t->t->training_step((hipStream_t)stream, n, in, target, run_opt != 0); });
+	return guard([&] {
+		TCNN_CHECK(n > 0, "training_step: empty batch");
+		t->t->training_step((hipStream_t)stream, n, in, target, run_opt != 0);
+	});
 }
 int tcnn_trainer_optimizer_step(tcnn_trainer* t, void* stream) {
 	return guard([&] { t->t->optimizer_step((hipStream_t)stream); });
@@ -338,7 +350,9 @@ float tcnn_trainer_loss(tcnn_trainer* t, void* stream) {
 }
 const float* tcnn_trainer_loss_device(tcnn_trainer* t) { return t->t->d_loss.as<float>(); }
 int tcnn_trainer_inference(tcnn_trainer* t, void* stream, uint32_t n, const float* in, float* out) {
-	return guard([&] { t->t->inference((hipStream_t)stream, n, in, out); });
+	return guard([&] {
+		if (n) t->t->inference((hipStream_t)stream, n, in, out);
+	});
 }
 uint64_t tcnn_trainer_n_params(const tcnn_trainer* t) { return t->t->n_params; }
 uint64_t tcnn_trainer_n_network_params(const tcnn_trainer* t) { return t->t->n_mlp; }
