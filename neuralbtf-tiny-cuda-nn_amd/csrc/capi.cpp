@@ -105,12 +105,12 @@ struct ModuleNWIE : ModuleBase {
 	std::string name() const override { return "NetworkWithInputEncoding"; }
 };
 
-// Parameter-free encodings (OneBlob, Identity) as a module (cpp_api.cu:145-149).
+// Parameter-free encodings (OneBlob, Identity) as a module (cpp_api.cu:145-149). Encoding modules take
+// any batch size (per-point kernels with bounds checks, like the reference); networks keep the 256 rule.
 struct ModuleEncoding : ModuleBase {
 	EncodingHost enc;
 	ModuleEncoding(uint32_t n_in, const json& j) : enc(n_in, j) {}
 	void inference(hipStream_t st, uint32_t n, const float* in, void* out, const void* params) override {
-		check_batch(n);
 		enc.forward_aos(st, n, in, params, out);
 	}
 	void forward(hipStream_t st, uint32_t n, const float* in, void* out, const void* params, bool) override {
@@ -118,7 +118,6 @@ struct ModuleEncoding : ModuleBase {
 	}
 	void backward(hipStream_t st, uint32_t n, float* dL_din, const void* dL_dout, void*, const float* in, const void*,
 	              const void*) override {
-		check_batch(n);
 		if (dL_din) enc.backward_input(st, n, in, dL_dout, dL_din);
 	}
 	uint32_t n_input_dims() const override { return enc.n_dims; }
@@ -134,7 +133,6 @@ struct ModuleGrid : ModuleBase {
 	DevBuf partial, grad32;
 	ModuleGrid(uint32_t n_in, const json& enc) : grid(n_in, enc) {}
 	void inference(hipStream_t st, uint32_t n, const float* in, void* out, const void* params) override {
-		check_batch(n);
 		const uint32_t W = grid.padded_output_width();
 		if (grid.n_to_pad) TCNN_HIP_CHECK(hipMemsetAsync(out, 0, (size_t)n * W * 2, st));
 		launch_grid_fwd(st, grid.desc.n_pos_dims, grid.desc.n_features_per_level, grid.desc.hash_type, n, grid.desc.n_levels,
@@ -146,7 +144,6 @@ struct ModuleGrid : ModuleBase {
 	}
 	void backward(hipStream_t st, uint32_t n, float* dL_din, const void* dL_dout, void* dL_dparams, const float* in,
 	              const void*, const void* params) override {
-		check_batch(n);
 		if (dL_din)
 			launch_grid_bwd_input(st, grid.desc.n_pos_dims, grid.desc.n_features_per_level, grid.desc.hash_type, n, grid.desc.n_levels, in,
 			                      grid.desc.n_pos_dims, params, dL_dout, 2, grid.padded_output_width(), dL_din, grid.desc.n_pos_dims,
@@ -164,7 +161,6 @@ struct ModuleGrid : ModuleBase {
 	}
 	void backward_backward_input(hipStream_t st, uint32_t n, const float* dL_ddLdin, const float* in, const void* dL_dout,
 	                             void* dL_dparams, void* dL_ddLdout, float* dL_din, const void* params) override {
-		check_batch(n);
 		if (!dL_ddLdout && !dL_dparams) return;  // grid.h:913-915
 		TCNN_CHECK(params, "backward_backward_input needs the grid parameters");
 		if (dL_dparams) {

@@ -17,6 +17,36 @@ PRECISION_FP32 = 0
 PRECISION_FP16 = 1
 
 
+class _C:
+    """Stand-in for the reference's compiled `tinycudann._C` module-level functions
+    (bindings.cpp:285-336), so scripts written against it (e.g. scripts/test_grid_bwdbwd.py,
+    which imports `_C` from tinycudann.modules) run unchanged. Everything goes to the C-ABI."""
+
+    class Precision:
+        Fp32 = PRECISION_FP32
+        Fp16 = PRECISION_FP16
+
+    @staticmethod
+    def preferred_precision():
+        return L.lib().tcnn_preferred_precision()
+
+    @staticmethod
+    def batch_size_granularity():
+        return L.lib().tcnn_batch_size_granularity()
+
+    @staticmethod
+    def default_loss_scale(precision):
+        return L.lib().tcnn_default_loss_scale(precision)
+
+    @staticmethod
+    def free_temporary_memory():
+        L.lib().tcnn_free_temporary_memory()
+
+    @staticmethod
+    def has_networks():
+        return bool(L.lib().tcnn_has_networks())
+
+
 def _torch_precision(p):
     return torch.half if p == PRECISION_FP16 else torch.float
 
