@@ -58,6 +58,7 @@ struct GridOpts {
 	uint32_t stochastic = 0;
 	uint32_t n_features = 0;  // n_levels * F (num_grid_features)
 	uint32_t active = 0;      // any option in effect (uniform fast-path test)
+	uint32_t n_levels = 0;    // set by the forward launcher (AoS lane mapping)
 };
 
 struct GridDesc {

@@ -24,10 +24,19 @@ template <uint32_t D, uint32_t F, HashType H>
 __global__ __launch_bounds__(256) void k_grid_fwd(uint32_t B, const float* __restrict__ pos, uint32_t pstride,
                                                   const _Float16* __restrict__ table, _Float16* __restrict__ out,
                                                   uint32_t soa, uint32_t out_stride, const LevelInfo* __restrict__ levels,
-                                                  uint32_t hash_grid, uint32_t interp_u, const GridOpts o) {
-	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+                                                  uint32_t hash_grid, uint32_t interp_u, const GridOpts o, uint32_t L) {
+	// SoA output: lanes = consecutive points of one level (blockIdx.y); AoS rows: lanes = the levels of
+	// consecutive points, so one store instruction writes whole rows
+	uint32_t i, level;
+	if (soa) {
+		i = blockIdx.x * blockDim.x + threadIdx.x;
+		level = blockIdx.y;
+	} else {
+		const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+		i = t / L;
+		level = t % L;
+	}
 	if (i >= B) return;
-	const uint32_t level = blockIdx.y;
 	const LevelInfo li = levels[level];
 	const Interp interp = (Interp)interp_u;
 	float p[D];
@@ -88,10 +97,11 @@ __global__ __launch_bounds__(256) void k_grid_fwd(uint32_t B, const float* __res
 template <uint32_t D, uint32_t F>
 static void grid_fwd_h(hipStream_t st, HashType h, dim3 g, uint32_t B, const float* pos, uint32_t ps, const _Float16* t,
                        _Float16* o, uint32_t soa, uint32_t os, const LevelInfo* lv, uint32_t hg, uint32_t in, const GridOpts& go) {
+	const uint32_t L = soa ? g.y : go.n_levels;
 	switch (h) {
-		case HashType::Prime: hipLaunchKernelGGL((k_grid_fwd<D, F, HashType::Prime>), g, dim3(256), 0, st, B, pos, ps, t, o, soa, os, lv, hg, in, go); break;
-		case HashType::ReversedPrime: hipLaunchKernelGGL((k_grid_fwd<D, F, HashType::ReversedPrime>), g, dim3(256), 0, st, B, pos, ps, t, o, soa, os, lv, hg, in, go); break;
-		default: hipLaunchKernelGGL((k_grid_fwd<D, F, HashType::CoherentPrime>), g, dim3(256), 0, st, B, pos, ps, t, o, soa, os, lv, hg, in, go); break;
+		case HashType::Prime: hipLaunchKernelGGL((k_grid_fwd<D, F, HashType::Prime>), g, dim3(256), 0, st, B, pos, ps, t, o, soa, os, lv, hg, in, go, L); break;
+		case HashType::ReversedPrime: hipLaunchKernelGGL((k_grid_fwd<D, F, HashType::ReversedPrime>), g, dim3(256), 0, st, B, pos, ps, t, o, soa, os, lv, hg, in, go, L); break;
+		default: hipLaunchKernelGGL((k_grid_fwd<D, F, HashType::CoherentPrime>), g, dim3(256), 0, st, B, pos, ps, t, o, soa, os, lv, hg, in, go, L); break;
 	}
 }
 
@@ -112,13 +122,15 @@ void launch_grid_fwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_
                      const float* pos, uint32_t pos_stride, const void* table16, void* out16, bool soa,
                      uint32_t out_stride, const LevelInfo* levels, bool hash_grid, Interp interp, const GridOpts& go) {
 	if (B == 0) return;
-	dim3 g(div_round_up(B, 256), L);
+	const dim3 g = soa ? dim3(div_round_up(B, 256), L) : dim3(div_round_up(B * L, 256), 1);
+	GridOpts gol = go;
+	gol.n_levels = L;  // carries L to the AoS mapping
 	const _Float16* t = (const _Float16*)table16;
 	_Float16* o = (_Float16*)out16;
 	switch (D) {
-		case 2: grid_fwd_f<2>(st, F, h, g, B, pos, pos_stride, t, o, soa, out_stride, levels, hash_grid, (uint32_t)interp, go); break;
-		case 3: grid_fwd_f<3>(st, F, h, g, B, pos, pos_stride, t, o, soa, out_stride, levels, hash_grid, (uint32_t)interp, go); break;
-		case 4: grid_fwd_f<4>(st, F, h, g, B, pos, pos_stride, t, o, soa, out_stride, levels, hash_grid, (uint32_t)interp, go); break;
+		case 2: grid_fwd_f<2>(st, F, h, g, B, pos, pos_stride, t, o, soa, out_stride, levels, hash_grid, (uint32_t)interp, gol); break;
+		case 3: grid_fwd_f<3>(st, F, h, g, B, pos, pos_stride, t, o, soa, out_stride, levels, hash_grid, (uint32_t)interp, gol); break;
+		case 4: grid_fwd_f<4>(st, F, h, g, B, pos, pos_stride, t, o, soa, out_stride, levels, hash_grid, (uint32_t)interp, gol); break;
 		default: throw std::runtime_error("GridEncoding: number of input dims must be 2, 3 or 4");
 	}
 	TCNN_HIP_CHECK(hipGetLastError());

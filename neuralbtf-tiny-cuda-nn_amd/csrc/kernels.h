@@ -179,8 +179,9 @@ bool layered_width_supported(uint32_t w);
 // y[B][N] = act(x[B][K] w^T), w row-major [N][K]
 void launch_layer_fwd(hipStream_t st, uint32_t B, uint32_t N, uint32_t K, const void* w16, const void* x16, void* y16, int act);
 // dx[B][K] = act'(h) * (dy[B][N] w); h == nullptr: no transfer
+// pairs = true (no transfer only): dX written as level-major fp16 pairs [K/2][B] (grid F = 2 encodings)
 void launch_layer_bwd(hipStream_t st, uint32_t B, uint32_t N, uint32_t K, const void* w16, const void* dy16, const void* h16,
-                      void* dx16, int act);
+                      void* dx16, int act, bool pairs = false);
 // in-place output-activation transfer: g[i] = act'(y[i]) g[i] over n elements
 void launch_act_bwd_inplace(hipStream_t st, uint32_t n, int act, const void* y16, void* g16);
 // partial[chunk][N][K] = sum over the chunk's samples of dy[i][n] x[i][k]

@@ -220,7 +220,7 @@ __global__ __launch_bounds__(256, 2) void k_layer_fwd(uint32_t B, uint32_t K, co
 template <int NT, int KS>
 __global__ __launch_bounds__(256, 2) void k_layer_bwd(uint32_t B, uint32_t N, const _Float16* __restrict__ w,
                                                     const _Float16* __restrict__ dy, const _Float16* __restrict__ h,
-                                                    _Float16* __restrict__ dx, int act) {
+                                                    _Float16* __restrict__ dx, int act, uint32_t pairs) {
 	constexpr int K = 16 * NT, RS = 32 * KS + 8;
 	__shared__ __attribute__((aligned(16))) _Float16 sWT[K * RS];
 	const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -239,6 +239,13 @@ __global__ __launch_bounds__(256, 2) void k_layer_bwd(uint32_t B, uint32_t N, co
 			} else {
 #pragma unroll
 				for (int r = 0; r < 4; ++r) r4[r] = (_Float16)v[r];
+				if (pairs) {  // grid dL/d(encoding) as level-major feature pairs [K/2][B] (the fused kernel's layout)
+					const uint32_t lv = 8 * t + 2 * q, i = base + 16 * tau + c;
+					uint32_t* d2 = (uint32_t*)dx;
+					d2[(size_t)lv * B + i] = __builtin_bit_cast(uint32_t, h2{r4[0], r4[1]});
+					d2[(size_t)(lv + 1) * B + i] = __builtin_bit_cast(uint32_t, h2{r4[2], r4[3]});
+					return;
+				}
 			}
 			*(h4*)(dx + o) = r4;
 		}, [&](uint32_t base) {
@@ -377,12 +384,13 @@ void launch_layer_fwd(hipStream_t st, uint32_t B, uint32_t N, uint32_t K, const 
 }
 
 void launch_layer_bwd(hipStream_t st, uint32_t B, uint32_t N, uint32_t K, const void* w16, const void* dy16, const void* h16,
-                      void* dx16, int act) {
+                      void* dx16, int act, bool pairs) {
+	TCNN_CHECK(!pairs || !h16, "layer_bwd: the pairs layout is for the untransferred encoding gradient");
 	TCNN_CHECK(B % 32 == 0 && N % 16 == 0 && K % 16 == 0, "layer_bwd: B % 32, N % 16, K % 16 must be 0");
 	if (B == 0) return;
 	bool ok = true;
 	const dim3 g(layer_blocks(B));
-#define CALL(nt, ks) hipLaunchKernelGGL((k_layer_bwd<nt, ks>), g, dim3(256), 0, st, B, N, (const _Float16*)w16, (const _Float16*)dy16, (const _Float16*)h16, (_Float16*)dx16, act)
+#define CALL(nt, ks) hipLaunchKernelGGL((k_layer_bwd<nt, ks>), g, dim3(256), 0, st, B, N, (const _Float16*)w16, (const _Float16*)dy16, (const _Float16*)h16, (_Float16*)dx16, act, pairs ? 1u : 0u)
 	TCNN_LAYER_DISPATCH(K / 16, pow2_ceil_steps(N), CALL)
 #undef CALL
 	TCNN_CHECK(ok, "layer_bwd: unsupported shape N=" + std::to_string(N) + " K=" + std::to_string(K));

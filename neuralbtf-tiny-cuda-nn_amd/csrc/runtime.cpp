@@ -375,7 +375,8 @@ void EncodingHost::forward_aos(hipStream_t st, uint32_t B, const float* x, const
 	}
 }
 
-void EncodingHost::backward_input(hipStream_t st, uint32_t B, const float* x, const void* dy16, float* dx, const void* params16) const {
+void EncodingHost::backward_input(hipStream_t st, uint32_t B, const float* x, const void* dy16, float* dx, const void* params16,
+                                  int dy_layout) const {
 	const uint32_t W = padded_output_width();
 	switch (kind) {
 		case EncKind::OneBlob: launch_oneblob_bwd(st, B, n_dims, n_bins, x, n_dims, dy16, W, dx, n_dims); break;
@@ -383,7 +384,7 @@ void EncodingHost::backward_input(hipStream_t st, uint32_t B, const float* x, co
 		default:
 			TCNN_CHECK(params16, "grid backward_input needs the grid parameters");
 			launch_grid_bwd_input(st, grid->desc.n_pos_dims, grid->desc.n_features_per_level, grid->desc.hash_type, B, grid->desc.n_levels,
-			                      x, grid->desc.n_pos_dims, params16, dy16, 2, W, dx, n_dims, grid->dev_levels(), grid->hash_grid(),
+			                      x, grid->desc.n_pos_dims, params16, dy16, dy_layout, W, dx, n_dims, grid->dev_levels(), grid->hash_grid(),
 			                      grid->desc.interp, grid->opts());
 	}
 }
@@ -583,17 +584,21 @@ void NetworkHost::fwd_bwd_layered(hipStream_t st, StepWorkspace& ws, uint32_t B,
 	wgrad(W, IN, dcur, ws.enc16.p, 0);
 	if (mark) mark(1);
 	const bool enc_grad = enc->n_params() > 0 || dL_dinput;
+	// a grid with feature pairs and no padding takes dL/d(encoding) as level-major pairs [L][B], the
+	// layout its backward reads coalesced (AoS rows would cost one 64-byte line per 4-byte read)
+	const bool pairs = grid && grid->desc.n_features_per_level == 2 && grid->n_to_pad == 0;
+	const int dy_layout = pairs ? 0 : 2;
 	if (enc_grad) {
-		// dL/d(encoding) = W0^T delta_0 (no transfer), AoS [B][IN]
-		launch_layer_bwd(st, B, W, IN, p16, dcur, nullptr, dnext, ACT_NONE);
-		if (dL_dinput) enc->backward_input(st, B, pos, dnext, dL_dinput, eparams);
+		// dL/d(encoding) = W0^T delta_0 (no transfer), AoS [B][IN] or level-major pairs
+		launch_layer_bwd(st, B, W, IN, p16, dcur, nullptr, dnext, ACT_NONE, pairs);
+		if (dL_dinput) enc->backward_input(st, B, pos, dnext, dL_dinput, eparams, dy_layout);
 	}
 	if (grid) {
 		const uint32_t n_chunks = grid->bwd_chunks(B);
 		ws.n_grid_chunks = n_chunks;
 		ws.grid_partial.reserve((size_t)n_chunks * grid->n_params * 4);
 		launch_grid_bwd(st, grid->desc.n_pos_dims, grid->desc.n_features_per_level, grid->desc.hash_type, B, pos,
-		                grid->desc.n_pos_dims, dnext, 2, IN, grid->d_slices.as<GridSlice>(), (uint32_t)grid->slices.size(), n_chunks,
+		                grid->desc.n_pos_dims, dnext, dy_layout, IN, grid->d_slices.as<GridSlice>(), (uint32_t)grid->slices.size(), n_chunks,
 		                ws.grid_partial.as<float>(), grid->n_params, grid->dev_levels(), grid->hash_grid(), grid->desc.interp, nullptr,
 		                grid->opts());
 		launch_grid_slab_reduce(st, ws.grid_partial.as<float>(), n_chunks, grid->n_params, grid->n_params, grad32 + n_mlp,

@@ -135,7 +135,9 @@ struct EncodingHost {
 	// encoded output AoS fp16 [B][padded_output_width()] (padding: grid 0, OneBlob / Identity 1)
 	void forward_aos(hipStream_t st, uint32_t B, const float* x, const void* params16, void* out16) const;
 	// dL/dx fp32 [B][n_dims] from dL/d(encoding) fp16 AoS; params16 = the encoding's parameters (grid)
-	void backward_input(hipStream_t st, uint32_t B, const float* x, const void* dy16, float* dx, const void* params16 = nullptr) const;
+	// dy16: AoS [B][padded width]; grid encodings also take dy_layout 0 (level-major pairs [L][B])
+	void backward_input(hipStream_t st, uint32_t B, const float* x, const void* dy16, float* dx, const void* params16 = nullptr,
+	                    int dy_layout = 2) const;
 };
 
 // Workspace for one fwd/bwd over a batch of B (sizes grow only).
