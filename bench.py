@@ -94,6 +94,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch-log2", type=int, default=18)
     ap.add_argument("--config", default=os.path.join(REPO, "tests", "golden", "config_hash.json"))
+    ap.add_argument("--log2-hashmap-size", type=int, default=None, help="override encoding.log2_hashmap_size")
+    ap.add_argument("--per-level-scale", type=float, default=None, help="override encoding.per_level_scale")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (rehearsal)")
@@ -121,6 +123,10 @@ def main():
     from tinycudann import _lib as L
 
     cfg = json.load(open(args.config))
+    if args.log2_hashmap_size is not None:
+        cfg["encoding"]["log2_hashmap_size"] = args.log2_hashmap_size
+    if args.per_level_scale is not None:
+        cfg["encoding"]["per_level_scale"] = args.per_level_scale
     B = 1 << args.batch_log2
     trainer = Trainer(2, 3, cfg, seed=1337)
     g = torch.Generator(device="cuda")

@@ -16,7 +16,7 @@ __device__ __forceinline__ float adam_bias_factor(const AdamArgs& a, uint32_t st
 // parameter is skipped (reference adam.h:75-82: frozen class, or a zero non-matrix gradient).
 __device__ __forceinline__ bool adam_core(const AdamArgs& a, uint32_t i, float gsum, _Float16& g16, float& w, float& m1, float& m2,
                                           uint32_t& step) {
-	g16 = (_Float16)(gsum * a.grad_scale);
+	g16 = f16_rn(gsum * a.grad_scale);
 	// x / 2^k is exact, so a power-of-two loss scale (128) becomes a multiply
 	float gradient = a.inv_loss_scale != 0.0f ? (float)g16 * a.inv_loss_scale : (float)g16 / a.loss_scale;
 	if (i >= a.n_matrix) {
@@ -53,7 +53,7 @@ __device__ __forceinline__ _Float16 adam_update(const AdamArgs& a, const AdamBuf
 	s.m1[i] = m1;
 	s.m2[i] = m2;
 	s.steps[i] = step;
-	const _Float16 h = (_Float16)w;
+	const _Float16 h = f16_rn(w);
 	s.w16[i] = h;
 	return h;
 }

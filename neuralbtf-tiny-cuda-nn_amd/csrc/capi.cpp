@@ -130,7 +130,8 @@ struct ModuleEncoding : ModuleBase {
 
 struct ModuleGrid : ModuleBase {
 	GridEncodingHost grid;
-	DevBuf partial, grad32;
+	GridBwdBufs gbw;
+	DevBuf grad32;
 	ModuleGrid(uint32_t n_in, const json& enc) : grid(n_in, enc) {}
 	void inference(hipStream_t st, uint32_t n, const float* in, void* out, const void* params) override {
 		const uint32_t W = grid.padded_output_width();
@@ -149,14 +150,8 @@ struct ModuleGrid : ModuleBase {
 			                      grid.desc.n_pos_dims, params, dL_dout, 2, grid.padded_output_width(), dL_din, grid.desc.n_pos_dims,
 			                      grid.dev_levels(), grid.hash_grid(), grid.desc.interp, grid.opts());
 		if (!dL_dparams) return;
-		const uint32_t n_slices = (uint32_t)grid.slices.size();
-		const uint32_t n_chunks = grid.bwd_chunks(n);
-		partial.reserve((size_t)n_chunks * grid.n_params * 4);
 		grad32.reserve((size_t)grid.n_params * 4);
-		launch_grid_bwd(st, grid.desc.n_pos_dims, grid.desc.n_features_per_level, grid.desc.hash_type, n, in, grid.desc.n_pos_dims,
-		                dL_dout, 2, grid.padded_output_width(), grid.d_slices.as<GridSlice>(), n_slices, n_chunks,
-		                partial.as<float>(), grid.n_params, grid.dev_levels(), grid.hash_grid(), grid.desc.interp, nullptr, grid.opts());
-		launch_grid_slab_reduce(st, partial.as<float>(), n_chunks, grid.n_params, grid.n_params, grad32.as<float>(), grid.slab_map());
+		grid.backward(st, gbw, n, in, grid.desc.n_pos_dims, dL_dout, 2, grid.padded_output_width(), grad32.as<float>());
 		launch_cast_f32_f16(st, grad32.as<float>(), dL_dparams, grid.n_params);
 	}
 	void backward_backward_input(hipStream_t st, uint32_t n, const float* dL_ddLdin, const float* in, const void* dL_dout,

@@ -73,6 +73,16 @@ struct GridDesc {
 	Interp interp;
 };
 
+// fp32 -> fp16 of an fp32 RESULT, rounded once from the fp32 value (the reference's __float2half of
+// an fp32 expression). The empty asm pins the fp32 value: without it hipcc folds the producing
+// multiply / FMA / subtraction and the conversion into one v_fma_mix{lo,hi}_f16, which rounds the
+// exact result straight to fp16 -- different from fp32-then-fp16 whenever the fp32 rounding lands
+// on an fp16 tie (~1e-5 of the grid's corner weights; found by tests/test_gpu_grid_large.py).
+__device__ __forceinline__ _Float16 f16_rn(float x) {
+	asm("" : "+v"(x));
+	return (_Float16)x;
+}
+
 inline uint32_t div_round_up(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
 // Grow-only scratch allocation owned by a launcher (not stream-ordered: callers on one stream).

@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void k_oneblob_fwd(uint32_t B, uint32_t D, uin
 			float right;
 			if (j + 1 < S) right = wrapped_cdf(scalbnf((float)(b + 1), -(int)log2_bins), xv, nb);
 			else right = first + (b == n_bins - 1 ? 1.0f : 0.0f);
-			o[b] = (_Float16)(right - left);
+			o[b] = f16_rn(right - left);
 			left = right;
 		}
 	}
@@ -87,7 +87,7 @@ __global__ __launch_bounds__(256) void k_oneblob_fwd8(uint32_t B, uint32_t D, ui
 		float right;
 		if (b - g + 1 < S) right = wrapped_cdf(scalbnf((float)(b + 1), -(int)log2_bins), xv, nb);
 		else right = wrapped_cdf(scalbnf((float)g, -(int)log2_bins), xv, nb) + (b == n_bins - 1 ? 1.0f : 0.0f);
-		o[j] = (_Float16)(right - left);
+		o[j] = f16_rn(right - left);
 		left = right;
 	}
 	*(h8*)(out + (size_t)i * out_stride + d * n_bins + b0) = o;
@@ -172,7 +172,7 @@ __global__ __launch_bounds__(256) void k_identity_bwd(uint32_t B, uint32_t D, fl
 	const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
 	if (t >= B * D) return;
 	const uint32_t i = t / D, j = t % D;
-	dx[(size_t)i * dx_stride + j] = (float)(_Float16)((float)dy[(size_t)i * dy_stride + j] * scale);
+	dx[(size_t)i * dx_stride + j] = (float)f16_rn((float)dy[(size_t)i * dy_stride + j] * scale);
 }
 
 void launch_identity_fwd(hipStream_t st, uint32_t B, uint32_t D, float scale, float offset, const float* x, uint32_t x_stride,

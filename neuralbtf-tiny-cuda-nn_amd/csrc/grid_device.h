@@ -134,7 +134,7 @@ __device__ __forceinline__ void level_corners(const LevelInfo& li, bool hash_gri
 			if ((c & (1u << d)) == 0) { w *= 1.0f - pos[d]; local[d] = pg[d]; }
 			else { w *= pos[d]; local[d] = pg[d] + 1; }
 		}
-		w16[c] = (_Float16)w;
+		w16[c] = f16_rn(w);
 		idx[c] = li.offset + grid_index<D, H>(hash_grid, li.size, li.res, local);
 	}
 }
@@ -165,7 +165,7 @@ __device__ __forceinline__ h2 encode_level_f2(const uint32_t* __restrict__ table
 			if ((c & (1u << d)) == 0) { w *= 1.0f - pos[d]; local[d] = pg[d]; }
 			else { w *= pos[d]; local[d] = pg[d] + 1; }
 		}
-		w16[c] = (_Float16)w;
+		w16[c] = f16_rn(w);
 		v[c] = table_u32[li.offset + grid_index<D, H>(hash_grid, li.size, li.res, local)];
 	}
 	h2 r = {(_Float16)0.0f, (_Float16)0.0f};
@@ -175,6 +175,29 @@ __device__ __forceinline__ h2 encode_level_f2(const uint32_t* __restrict__ table
 		r = pk_fma_f16(wv, __builtin_bit_cast(h2, v[c]), r);
 	}
 	return r;
+}
+
+// F fp16 features of one table entry / one point-level
+template <uint32_t F>
+struct HVec { _Float16 v[F]; };
+
+// dL/dy of point i, level `level` (F features) in one of the grid backward's layouts:
+// 0 = level-major feature pairs [l][i][F], 1 = SoA [(l*F+f)*B + i] (reference RM), 2 = AoS
+// [i*stride + l*F + f] (reference CM)
+template <uint32_t F>
+__device__ __forceinline__ void load_dy(int layout, const _Float16* __restrict__ dLdy, uint32_t dy_stride, uint32_t level, uint32_t B,
+                                        uint32_t i, float* dy) {
+	if (layout == 0) {  // level-major feature pairs [l][i][F]
+		const HVec<F> v = ((const HVec<F>*)dLdy)[(size_t)level * B + i];
+#pragma unroll
+		for (uint32_t f = 0; f < F; ++f) dy[f] = (float)v.v[f];
+	} else if (layout == 1) {  // SoA [(l*F+f)*B + i] (reference RM layout)
+#pragma unroll
+		for (uint32_t f = 0; f < F; ++f) dy[f] = (float)dLdy[(size_t)(level * F + f) * B + i];
+	} else {  // AoS [i*stride + l*F + f] (reference CM layout)
+#pragma unroll
+		for (uint32_t f = 0; f < F; ++f) dy[f] = (float)dLdy[(size_t)i * dy_stride + level * F + f];
+	}
 }
 
 }  // namespace tcnn_amd

@@ -17,6 +17,30 @@ struct GridSlice {
 	uint32_t nf;
 };
 
+// Binned backward of the grid levels whose accumulators do not fit the LDS (grid_bin.hip): the
+// level's entries are cut into slices of 2^slice_log2 entries; every (point, corner) update is
+// counting-sorted by slice into per-chunk record runs, then one workgroup per slice ("bucket")
+// accumulates its records in LDS and writes (or applies Adam to) the slice's gradient.
+struct GridBinLevel {
+	uint32_t level;
+	uint32_t slice_log2;
+	uint32_t n_slices;
+	uint32_t bucket_base;  // first global bucket of the level
+};
+
+struct GridBinArgs {
+	const GridBinLevel* lv;  // [n_slots]
+	uint32_t n_slots, n_buckets;
+	uint32_t n_chunks, pts_per_chunk;  // point chunks of the bin pass (pts_per_chunk = GRID_BIN_RECS >> D)
+	uint32_t acc_lds_bytes;            // accumulator bytes of the largest slice
+	uint2* recs;     // [n_slots][n_chunks][GRID_BIN_RECS] {(w16 << 16) | entry-in-slice, dL/dy bits or point index}
+	uint2* dir;      // [n_buckets][n_chunks] {first record of the bucket's run in the chunk, count}
+	float* dysum;    // [n_slots][n_chunks][F] sum of |dL/dy| (fixed-point range of the level)
+};
+constexpr uint32_t GRID_BIN_RECS = 4096;        // records per (level, chunk) run
+constexpr uint32_t GRID_BIN_MAX_SLICES = 2048;  // slices per level
+constexpr uint32_t GRID_ACC_LDS_BYTES = 64 * 1024;  // accumulator budget of one slice
+
 // Runtime activation codes of the layer-wise engine (reference Activation, common.h:126-136).
 enum : int {
 	ACT_NONE = 0, ACT_RELU = 1, ACT_LEAKY_RELU = 2, ACT_EXPONENTIAL = 3, ACT_SINE = 4, ACT_SIGMOID = 5,
@@ -136,6 +160,22 @@ void launch_grid_bwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_
                      uint32_t n_slices, uint32_t n_chunks, float* partial, uint32_t partial_stride,
                      const LevelInfo* levels, bool hash_grid, Interp interp, const GridBwdEpilogue* ep = nullptr,
                      const GridOpts& opts = GridOpts{});
+// Binned backward, pass 1: counting-sort the updates of the binned levels by slice (GridBinArgs).
+void launch_grid_bin(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_t B, const float* pos, uint32_t pos_stride,
+                     const void* dLdy16, int dy_layout, uint32_t dy_stride, const LevelInfo* levels, bool hash_grid, Interp interp,
+                     const GridBinArgs& a, const GridOpts& opts = GridOpts{});
+// Binned backward, pass 2: one workgroup per slice sums its records in LDS (int32 fixed point scaled
+// by the level's sum of |dL/dy|) and writes the fp32 gradient of grid parameter p to grad32[p] (grid
+// parameter order) or, with adam != nullptr, applies Adam to parameter param_base + p.
+struct GridAccAdam {
+	AdamArgs a;
+	AdamBuffers buf;
+	uint32_t param_base;
+	int write_grad32;  // also store the fp32 sum into buf.g32
+};
+void launch_grid_acc(hipStream_t st, uint32_t D, uint32_t F, uint32_t B, const void* dLdy16, int dy_layout, uint32_t dy_stride,
+                     const LevelInfo* levels, const GridBinArgs& a, float* grad32, const GridAccAdam* adam);
+
 // dL/dx fp32 [B][dx_stride] through the grid (reference grid.h:171-211 + 322-349), dy_dx recomputed
 // from the table; dLdy in the launch_grid_bwd layouts.
 void launch_grid_bwd_input(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_t B, uint32_t L, const float* pos,

@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256) void k_relative_l2(uint32_t n_elements, uint32
 	const float d = p - target[inter * dims + intra];
 	if (values) values[i] = d * d / pse / n_total;
 	const float gr = 2.0f * d / pse;
-	grads[i] = (_Float16)(loss_scale * gr / n_total);
+	grads[i] = f16_rn(loss_scale * gr / n_total);
 }
 
 void launch_relative_l2(hipStream_t st, uint32_t B, uint32_t stride, uint32_t dims, float loss_scale,

@@ -288,7 +288,7 @@ __device__ __forceinline__ void slice_fwd_loss(const FusedTrainArgs& a, uint32_t
 					const float d = p - target(tau, o);
 					loss += d * d / pse / a.n_total;
 					const float gr = 2.0f * d / pse;
-					g[r] = (_Float16)(a.loss_scale * gr / a.n_total);
+					g[r] = f16_rn(a.loss_scale * gr / a.n_total);
 				}
 			}
 			G[tau] = g;

@@ -53,7 +53,7 @@ __device__ __forceinline__ float act_bwd_rt(int a, float g, float y) {
 		case ACT_RELU: return y > 0.0f ? g : 0.0f;
 		case ACT_LEAKY_RELU: f = y > 0.0f ? 1.0f : 0.01f; break;
 		case ACT_EXPONENTIAL: f = y; break;
-		case ACT_SIGMOID: f = y * (float)(_Float16)(1.0f - y); break;
+		case ACT_SIGMOID: f = y * (float)f16_rn(1.0f - y); break;
 		case ACT_SQUAREPLUS: {
 			const float t = y * K_ACT;
 			f = t * t / (t * t + 1.0f);
@@ -63,7 +63,7 @@ __device__ __forceinline__ float act_bwd_rt(int a, float g, float y) {
 		case ACT_TANH: f = 1.0f - y * y; break;
 		default: return g;
 	}
-	return (float)(_Float16)g * (float)(_Float16)f;
+	return (float)f16_rn(g) * (float)f16_rn(f);
 }
 
 // Stage a row-major [rows][cols] fp16 matrix into LDS with row stride rs, zero-filling columns
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(256, 2) void k_layer_fwd(uint32_t B, uint32_t K, co
 		layer_slices<NT, KS>(sW, RS, x, K, K, B, wave, c, q, [&](uint32_t base, int tau, int t, f4 v) {
 			h4 o;
 #pragma unroll
-			for (int r = 0; r < 4; ++r) o[r] = (_Float16)act_fwd_sel<decltype(A)::value>(act, v[r]);
+			for (int r = 0; r < 4; ++r) o[r] = f16_rn(act_fwd_sel<decltype(A)::value>(act, v[r]));
 			*(h4*)(y + (size_t)(base + 16 * tau + c) * N + 16 * t + 4 * q) = o;
 		}, [](uint32_t) {});
 	});
@@ -235,7 +235,7 @@ __global__ __launch_bounds__(256, 2) void k_layer_bwd(uint32_t B, uint32_t N, co
 			h4 r4;
 			if constexpr (TRANSFER) {
 #pragma unroll
-				for (int r = 0; r < 4; ++r) r4[r] = (_Float16)act_bwd_sel<decltype(A)::value>(act, v[r], (float)hv[tau][t][r]);
+				for (int r = 0; r < 4; ++r) r4[r] = f16_rn(act_bwd_sel<decltype(A)::value>(act, v[r], (float)hv[tau][t][r]));
 			} else {
 #pragma unroll
 				for (int r = 0; r < 4; ++r) r4[r] = (_Float16)v[r];
@@ -446,7 +446,7 @@ __global__ __launch_bounds__(256) void k_relative_l2_partial(uint32_t n_elements
 		const float d = p - target[inter * dims + intra];
 		s += d * d / pse / n_total;
 		const float gr = 2.0f * d / pse;
-		grads[i] = (_Float16)(loss_scale * gr / n_total);
+		grads[i] = f16_rn(loss_scale * gr / n_total);
 	}
 #pragma unroll
 	for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
@@ -468,7 +468,7 @@ void launch_relative_l2_partial(hipStream_t st, uint32_t B, uint32_t stride, uin
 
 __global__ __launch_bounds__(256) void k_act_bwd_inplace(uint32_t n, int act, const _Float16* __restrict__ y, _Float16* __restrict__ g) {
 	const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-	if (i < n) g[i] = (_Float16)act_bwd_rt(act, (float)g[i], (float)y[i]);
+	if (i < n) g[i] = f16_rn(act_bwd_rt(act, (float)g[i], (float)y[i]));
 }
 
 void launch_act_bwd_inplace(hipStream_t st, uint32_t n, int act, const void* y16, void* g16) {

@@ -177,15 +177,25 @@ GridEncodingHost::GridEncodingHost(uint32_t n_dims, const json& enc) {
 	}
 	n_params = offset * F;
 
-	// LDS-privatised backward plan: a level whose F features fit the LDS budget is one item; else
-	// one item per feature group (as many features as fit), else entry slices of one feature.
-	// Items with all features (2 atomics per corner for F = 2) go first: they are the heaviest.
+	// Backward plan. A level whose F features fit the LDS budget is one LDS item; else, when one
+	// feature fits, one item per feature group (config_hash's 2^15-entry hashed levels: two items);
+	// levels with even one feature over the budget -- and every level after them, so the binned
+	// levels are a suffix of the parameter vector -- go through the binned backward (grid_bin.hip).
+	// TCNN_GRID_BIN=all bins every level that does not fit whole (tuning switch).
 	const uint32_t S = grid_bwd_slot_budget();
+	const char* bin_env = std::getenv("TCNN_GRID_BIN");
+	const bool bin_all = bin_env && std::string(bin_env) == "all";
+	first_binned = L;
+	for (uint32_t l = 0; l < L; ++l) {
+		const uint64_t need = bin_all ? (uint64_t)levels[l].size * F : (uint64_t)levels[l].size;
+		if (need > S) { first_binned = l; break; }
+	}
+	n_lds_params = (first_binned < L ? levels[first_binned].offset : offset) * F;
 	std::vector<GridSlice> single;
 	GridSlabMap map{};
-	map.n_levels = L;
+	map.n_levels = std::max(1u, first_binned);
 	while ((1u << map.log2F) < F) ++map.log2F;
-	for (uint32_t l = 0; l < L; ++l) {
+	for (uint32_t l = 0; l < first_binned; ++l) {
 		const uint32_t size = levels[l].size;
 		map.pbase[l] = levels[l].offset * F;
 		map.size[l] = size;
@@ -197,14 +207,34 @@ GridEncodingHost::GridEncodingHost(uint32_t n_dims, const json& enc) {
 		uint32_t nf = F;
 		while (nf > 1 && ((uint64_t)size * nf > S || F % nf)) --nf;
 		map.nf[l] = nf;
-		const uint32_t SL = size <= S / nf ? size : S / nf;
-		for (uint32_t f = 0; f < F; f += nf)
-			for (uint32_t b = 0; b < size; b += SL) single.push_back(GridSlice{l, b, std::min(size, b + SL), f, nf});
+		for (uint32_t f = 0; f < F; f += nf) single.push_back(GridSlice{l, 0, size, f, nf});
 	}
 	slices.insert(slices.end(), single.begin(), single.end());
-	map.pbase[L] = n_params;
+	map.pbase[first_binned] = n_lds_params;
 	d_slab_map.reserve(sizeof(GridSlabMap));
 	TCNN_HIP_CHECK(hipMemcpy(d_slab_map.p, &map, sizeof(GridSlabMap), hipMemcpyHostToDevice));
+
+	// binned levels: slices of 2^s entries, ~128 per level (one workgroup each in the accumulate
+	// pass), within the accumulator budget and GRID_BIN_MAX_SLICES
+	const uint32_t max_entries = GRID_ACC_LDS_BYTES / 4 / F;
+	for (uint32_t l = first_binned; l < L; ++l) {
+		const uint32_t size = levels[l].size;
+		uint32_t lg = 0;
+		while ((1ull << lg) < size) ++lg;
+		uint32_t s = lg > 7 ? lg - 7 : 0;
+		s = std::max(s, 9u);
+		while ((1u << s) > max_entries) --s;
+		TCNN_CHECK(div_round_up(size, 1u << s) <= GRID_BIN_MAX_SLICES,
+		           "GridEncoding: level of " + std::to_string(size) + " entries exceeds the binned backward's capacity");
+		GridBinLevel b{l, s, div_round_up(size, 1u << s), n_buckets};
+		n_buckets += b.n_slices;
+		acc_lds_bytes = std::max(acc_lds_bytes, (1u << s) * F * 4);
+		bin_levels.push_back(b);
+	}
+	if (!bin_levels.empty()) {
+		d_bin_levels.reserve(bin_levels.size() * sizeof(GridBinLevel));
+		TCNN_HIP_CHECK(hipMemcpy(d_bin_levels.p, bin_levels.data(), bin_levels.size() * sizeof(GridBinLevel), hipMemcpyHostToDevice));
+	}
 
 	d_levels.reserve(levels.size() * sizeof(LevelInfo));
 	TCNN_HIP_CHECK(hipMemcpy(d_levels.p, levels.data(), levels.size() * sizeof(LevelInfo), hipMemcpyHostToDevice));
@@ -214,6 +244,67 @@ GridEncodingHost::GridEncodingHost(uint32_t n_dims, const json& enc) {
 
 void GridEncodingHost::initialize_params(Pcg32& rng, float* out, float scale) const {
 	strided_uniform(rng, n_params, out, -1e-4f * scale, 1e-4f * scale);
+}
+
+GridBinArgs GridEncodingHost::bin_args(GridBwdBufs& w, uint32_t B) const {
+	GridBinArgs a{};
+	a.lv = d_bin_levels.as<GridBinLevel>();
+	a.n_slots = (uint32_t)bin_levels.size();
+	a.n_buckets = n_buckets;
+	a.pts_per_chunk = GRID_BIN_RECS >> desc.n_pos_dims;
+	a.n_chunks = div_round_up(std::max(B, 1u), a.pts_per_chunk);
+	a.acc_lds_bytes = acc_lds_bytes;
+	if (a.n_slots) {
+		w.recs.reserve((size_t)a.n_slots * a.n_chunks * GRID_BIN_RECS * sizeof(uint2));
+		w.dir.reserve((size_t)a.n_buckets * a.n_chunks * sizeof(uint2));
+		w.dysum.reserve((size_t)a.n_slots * a.n_chunks * desc.n_features_per_level * sizeof(float));
+	}
+	a.recs = w.recs.as<uint2>();
+	a.dir = w.dir.as<uint2>();
+	a.dysum = w.dysum.as<float>();
+	return a;
+}
+
+void GridEncodingHost::backward_items(hipStream_t st, GridBwdBufs& w, uint32_t B, const float* pos, uint32_t pstride, const void* dy,
+                                      int layout, uint32_t dy_stride, const GridBwdEpilogue* ep, uint32_t reserved) const {
+	const uint32_t n_chunks = bwd_chunks(B, reserved);
+	w.n_chunks = n_chunks;
+	if (!slices.empty()) w.partial.reserve((size_t)n_chunks * n_lds_params * 4);
+	launch_grid_bwd(st, desc.n_pos_dims, desc.n_features_per_level, desc.hash_type, B, pos, pstride, dy, layout, dy_stride,
+	                d_slices.as<GridSlice>(), (uint32_t)slices.size(), n_chunks, w.partial.as<float>(), n_lds_params, dev_levels(),
+	                hash_grid(), desc.interp, ep, opts());
+}
+
+void GridEncodingHost::backward_bin(hipStream_t st, GridBwdBufs& w, uint32_t B, const float* pos, uint32_t pstride, const void* dy,
+                                    int layout, uint32_t dy_stride) const {
+	if (bin_levels.empty() || B == 0) return;
+	const GridBinArgs a = bin_args(w, B);
+	launch_grid_bin(st, desc.n_pos_dims, desc.n_features_per_level, desc.hash_type, B, pos, pstride, dy, layout, dy_stride, dev_levels(),
+	                hash_grid(), desc.interp, a, opts());
+}
+
+void GridEncodingHost::backward_acc(hipStream_t st, GridBwdBufs& w, uint32_t B, const void* dy, int layout, uint32_t dy_stride,
+                                    float* grad32, const GridAccAdam* adam) const {
+	if (bin_levels.empty()) return;
+	if (B == 0) {  // no points: zero gradient (Overwrite)
+		if (!adam) TCNN_HIP_CHECK(hipMemsetAsync(grad32 + n_lds_params, 0, (size_t)(n_params - n_lds_params) * 4, st));
+		return;
+	}
+	const GridBinArgs a = bin_args(w, B);
+	launch_grid_acc(st, desc.n_pos_dims, desc.n_features_per_level, B, dy, layout, dy_stride, dev_levels(), a, grad32, adam);
+}
+
+void GridEncodingHost::reduce_items(hipStream_t st, GridBwdBufs& w, float* grad32) const {
+	if (slices.empty()) return;
+	launch_grid_slab_reduce(st, w.partial.as<float>(), w.n_chunks, n_lds_params, n_lds_params, grad32, slab_map());
+}
+
+void GridEncodingHost::backward(hipStream_t st, GridBwdBufs& w, uint32_t B, const float* pos, uint32_t pstride, const void* dy,
+                                int layout, uint32_t dy_stride, float* grad32) const {
+	backward_items(st, w, B, pos, pstride, dy, layout, dy_stride);
+	backward_bin(st, w, B, pos, pstride, dy, layout, dy_stride);
+	backward_acc(st, w, B, dy, layout, dy_stride, grad32);
+	reduce_items(st, w, grad32);
 }
 
 static const char* grid_type_str(GridType t) { return t == GridType::Hash ? "Hash" : t == GridType::Dense ? "Dense" : "Tiled"; }
@@ -493,10 +584,6 @@ void NetworkHost::fused_kernel(hipStream_t st, StepWorkspace& ws, uint32_t B, co
 }
 
 void NetworkHost::grid_backward(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, GridBwdEpilogue* ep) {
-	const uint32_t n_slices = (uint32_t)grid->slices.size();
-	const uint32_t n_chunks = grid->bwd_chunks(B, ep ? ep->n_mlp_groups : 0u);
-	ws.n_grid_chunks = n_chunks;
-	ws.grid_partial.reserve((size_t)n_chunks * grid->n_params * 4);
 	if (ep) {
 		ep->wimage = ws.wimage.as<_Float16>();
 		ep->W = mlp.width;
@@ -507,9 +594,8 @@ void NetworkHost::grid_backward(hipStream_t st, StepWorkspace& ws, uint32_t B, c
 		ep->n_wparts = ws.n_fused_blocks;
 		ep->lpart = ws.loss_partial.as<float>();
 	}
-	launch_grid_bwd(st, grid->desc.n_pos_dims, grid->desc.n_features_per_level, grid->desc.hash_type, B, pos, grid->desc.n_pos_dims,
-	                ws.dLdenc.p, 0, 0, grid->d_slices.as<GridSlice>(), n_slices, n_chunks, ws.grid_partial.as<float>(),
-	                grid->n_params, grid->dev_levels(), grid->hash_grid(), grid->desc.interp, ep);
+	grid->backward_items(st, ws.gbw, B, pos, grid->desc.n_pos_dims, ws.dLdenc.p, 0, 0, ep, ep ? ep->n_mlp_groups : 0u);
+	grid->backward_bin(st, ws.gbw, B, pos, grid->desc.n_pos_dims, ws.dLdenc.p, 0, 0);
 	if (ep && ep->apply_adam) ws.wimage_valid = true;  // the epilogue wrote the image of the updated weights
 }
 
@@ -520,10 +606,10 @@ void NetworkHost::fwd_bwd_fused(hipStream_t st, StepWorkspace& ws, uint32_t B, c
 	fused_kernel(st, ws, B, pos, target, dims, loss_scale, params16, true, dout16, out16);
 	if (mark) mark(1);
 	grid_backward(st, ws, B, pos);
+	grid->backward_acc(st, ws.gbw, B, ws.dLdenc.p, 0, 0, grad32 + n_mlp);
 	if (mark) mark(2);
 	launch_column_sums(st, ws.wgrad_partial.as<float>(), ws.n_fused_blocks, n_mlp, grad32);
-	launch_grid_slab_reduce(st, ws.grid_partial.as<float>(), ws.n_grid_chunks, grid->n_params, grid->n_params, grad32 + n_mlp,
-	                        grid->slab_map());
+	grid->reduce_items(st, ws.gbw, grad32 + n_mlp);
 	if (mark) mark(3);
 }
 
@@ -594,15 +680,7 @@ void NetworkHost::fwd_bwd_layered(hipStream_t st, StepWorkspace& ws, uint32_t B,
 		if (dL_dinput) enc->backward_input(st, B, pos, dnext, dL_dinput, eparams, dy_layout);
 	}
 	if (grid) {
-		const uint32_t n_chunks = grid->bwd_chunks(B);
-		ws.n_grid_chunks = n_chunks;
-		ws.grid_partial.reserve((size_t)n_chunks * grid->n_params * 4);
-		launch_grid_bwd(st, grid->desc.n_pos_dims, grid->desc.n_features_per_level, grid->desc.hash_type, B, pos,
-		                grid->desc.n_pos_dims, dnext, dy_layout, IN, grid->d_slices.as<GridSlice>(), (uint32_t)grid->slices.size(), n_chunks,
-		                ws.grid_partial.as<float>(), grid->n_params, grid->dev_levels(), grid->hash_grid(), grid->desc.interp, nullptr,
-		                grid->opts());
-		launch_grid_slab_reduce(st, ws.grid_partial.as<float>(), n_chunks, grid->n_params, grid->n_params, grad32 + n_mlp,
-		                        grid->slab_map());
+		grid->backward(st, ws.gbw, B, pos, grid->desc.n_pos_dims, dnext, dy_layout, IN, grad32 + n_mlp);
 	}
 	if (mark) mark(2);
 	if (mark) mark(3);
@@ -714,20 +792,33 @@ void TrainerHost::training_step_overlapped(hipStream_t st, uint32_t B, const flo
 	ep.factor_step = adam_step;  // parameters updated every step have step count == adam_step
 	TCNN_CHECK(n_mlp % 4 == 0, "network parameter count must be a multiple of 4");
 	m.grid_backward(st, ws, B, input, &ep);
-	mark(st, 2);
+	GridEncodingHost& g = *m.grid;
 	if (run_optimizer) {
+		// binned levels: Adam applied by the accumulate pass; LDS levels: Adam summing their slabs
+		GridAccAdam ga{};
+		ga.a = adam_args();
+		ga.a.cached_factor = d_factor.as<float>();
+		ga.a.cached_step = adam_step;
+		ga.buf = ep.buf;
+		ga.param_base = (uint32_t)n_mlp;
+		ga.write_grad32 = 1;
+		g.backward_acc(st, ws.gbw, B, ws.dLdenc.p, 0, 0, g32.as<float>() + n_mlp, &ga);
+		mark(st, 2);
 		AdamArgs ag = adam_args();
+		ag.n = (uint32_t)n_mlp + g.n_lds_params;
 		ag.begin = (uint32_t)n_mlp;
-		ag.part = ws.grid_partial.as<float>();
-		ag.n_parts = ws.n_grid_chunks;
-		ag.part_stride = m.grid->n_params;
-		ag.part_map = m.grid->slab_map();
+		ag.part = ws.gbw.partial.as<float>();
+		ag.n_parts = ws.gbw.n_chunks;
+		ag.part_stride = g.n_lds_params;
+		ag.part_map = g.slab_map();
 		ag.cached_factor = d_factor.as<float>();
 		ag.cached_step = adam_step;
-		launch_adam(st, ag, w32.as<float>(), w16.p, g32.as<float>(), g16.p, m1.as<float>(), m2.as<float>(), steps.as<uint32_t>());
+		if (!g.slices.empty())
+			launch_adam(st, ag, w32.as<float>(), w16.p, g32.as<float>(), g16.p, m1.as<float>(), m2.as<float>(), steps.as<uint32_t>());
 	} else {
-		launch_grid_slab_reduce(st, ws.grid_partial.as<float>(), ws.n_grid_chunks, m.grid->n_params, m.grid->n_params,
-		                        g32.as<float>() + n_mlp, m.grid->slab_map());
+		g.backward_acc(st, ws.gbw, B, ws.dLdenc.p, 0, 0, g32.as<float>() + n_mlp);
+		mark(st, 2);
+		g.reduce_items(st, ws.gbw, g32.as<float>() + n_mlp);
 	}
 	mark(st, 3);
 	last_B = B;

@@ -46,6 +46,12 @@ struct DevBuf {
 
 bool ieq(const std::string& a, const std::string& b);
 
+// Scratch of one grid backward (grow-only).
+struct GridBwdBufs {
+	DevBuf partial, recs, dir, dysum;
+	uint32_t n_chunks = 0;  // LDS items: point chunks = slabs in `partial`
+};
+
 // ---- multiresolution grid (reference encodings/grid.h:652-1208) ----
 struct GridEncodingHost {
 	GridDesc desc{};
@@ -56,8 +62,14 @@ struct GridEncodingHost {
 	float max_level = 1000.0f;              // GridEncoding::set_max_level (grid_interface.h:101-107)
 	const float* max_level_gpu = nullptr;   // set_max_level_gpu: [B] per point (grid_interface.h:109-123)
 	std::vector<LevelInfo> levels;
+	// backward plan: levels [0, first_binned) are LDS work items (`slices`, per-chunk slabs), levels
+	// [first_binned, L) go through the binned backward (grid_bin.hip), one slot each
 	std::vector<GridSlice> slices;
-	DevBuf d_levels, d_slices, d_slab_map;
+	uint32_t first_binned = 0;
+	uint32_t n_lds_params = 0;  // offset[first_binned] * F
+	std::vector<GridBinLevel> bin_levels;
+	uint32_t n_buckets = 0, acc_lds_bytes = 0;
+	DevBuf d_levels, d_slices, d_slab_map, d_bin_levels;
 
 	GridEncodingHost(uint32_t n_dims_to_encode, const json& enc);
 	uint32_t padded_output_width() const { return n_features + n_to_pad; }
@@ -83,13 +95,32 @@ struct GridEncodingHost {
 	// slack (config_hash, 26 items + 16 tail workgroups: 7 / 8 / 9 / 10 chunks -> 68.8 / 65.8 /
 	// 67.5 / 109 us, the last spilling into a second round); >= 4096 points each
 	uint32_t bwd_chunks(uint32_t B, uint32_t reserved = 0) const {
+		if (slices.empty()) return 1;
 		const uint32_t n_cu = 256;
 		const uint32_t fit = (n_cu > reserved ? n_cu - reserved : 1u) / (uint32_t)slices.size();
 		uint32_t c = std::max(1u, fit > 2 ? fit - 1 : fit);
 		if (const char* e = std::getenv("TCNN_GRID_BWD_CHUNKS"))  // tuning override
 			if (std::atoi(e) > 0) c = (uint32_t)std::atoi(e);
-		return std::max(1u, std::min(c, B / 4096));
+		return std::max(1u, std::min(std::min(c, 32u), B / 4096));
 	}
+	// bin-pass geometry for B points (reserves the record / directory buffers in w)
+	GridBinArgs bin_args(GridBwdBufs& w, uint32_t B) const;
+	// The backward pieces. dy: dL/d(encoding) fp16 in launch_grid_bwd layout `layout` (stride for AoS).
+	//   backward_items  LDS items -> per-chunk slabs in w.partial (+ the trainer's epilogue workgroups)
+	//   backward_bin    bin pass of the binned levels
+	//   backward_acc    accumulate pass: fp32 gradient of the binned levels into grad32 (grid
+	//                   parameter order, whole grid vector) or Adam on them (adam != nullptr)
+	//   reduce_items    fixed-order slab sums of the LDS levels into grad32[0, n_lds_params)
+	// backward() = all four: the fp32 gradient of every grid parameter into grad32 [n_params].
+	void backward_items(hipStream_t st, GridBwdBufs& w, uint32_t B, const float* pos, uint32_t pstride, const void* dy, int layout,
+	                    uint32_t dy_stride, const GridBwdEpilogue* ep = nullptr, uint32_t reserved = 0) const;
+	void backward_bin(hipStream_t st, GridBwdBufs& w, uint32_t B, const float* pos, uint32_t pstride, const void* dy, int layout,
+	                  uint32_t dy_stride) const;
+	void backward_acc(hipStream_t st, GridBwdBufs& w, uint32_t B, const void* dy, int layout, uint32_t dy_stride, float* grad32,
+	                  const GridAccAdam* adam = nullptr) const;
+	void reduce_items(hipStream_t st, GridBwdBufs& w, float* grad32) const;
+	void backward(hipStream_t st, GridBwdBufs& w, uint32_t B, const float* pos, uint32_t pstride, const void* dy, int layout,
+	              uint32_t dy_stride, float* grad32) const;
 };
 
 // ---- fully fused MLP shape (reference networks/fully_fused_mlp.h) ----
@@ -142,9 +173,10 @@ struct EncodingHost {
 
 // Workspace for one fwd/bwd over a batch of B (sizes grow only).
 struct StepWorkspace {
-	DevBuf dLdenc, wgrad_partial, loss_partial, grid_partial, grad32_tmp, out16, enc16, wimage;
+	DevBuf dLdenc, wgrad_partial, loss_partial, grad32_tmp, out16, enc16, wimage;
+	GridBwdBufs gbw;
 	DevBuf acts, delta0, delta1, dout16;  // layer-wise engine
-	uint32_t n_fused_blocks = 0, n_grid_chunks = 0, n_loss_partials = 0;
+	uint32_t n_fused_blocks = 0, n_loss_partials = 0;
 	bool wimage_valid = false;  // fused weight image matches the current fp16 params (trainer fast path)
 };
 

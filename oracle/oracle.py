@@ -82,6 +82,8 @@ def lib():
         _lib.orc_coherent_prime_hash.argtypes = [ctypes.c_uint32, ctypes.c_void_p]
         _lib.orc_grid_fwd.argtypes = [ctypes.POINTER(GridCfg), ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         _lib.orc_grid_bwd.argtypes = [ctypes.POINTER(GridCfg), ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        _lib.orc_grid_bwd_stats.argtypes = [ctypes.POINTER(GridCfg), ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_void_p]
         _lib.orc_grid_bwd_input.argtypes = [ctypes.POINTER(GridCfg), ctypes.c_uint32] + [ctypes.c_void_p] * 4
         _lib.orc_grid_bwd_bwd.argtypes = [ctypes.POINTER(GridCfg), ctypes.c_uint32] + [ctypes.c_void_p] * 7
         _lib.orc_mlp_n_params.restype = ctypes.c_uint32
@@ -230,6 +232,38 @@ def grid_bwd(g, pos, dL_dy16):
     grad = np.zeros(g.n_params, dtype=np.float32)
     lib().orc_grid_bwd(ctypes.byref(g), B, _p(pos), _p(dL_dy16), _p(grad))
     return grad
+
+
+def grid_bwd_stats(g, pos, dL_dy16):
+    """per grid parameter: (sum of |update|, number of updates) of the backward over pos"""
+    pos = np.ascontiguousarray(pos, dtype=np.float32)
+    B = pos.shape[0]
+    dL_dy16 = np.ascontiguousarray(dL_dy16, dtype=np.uint16)
+    absum = np.zeros(g.n_params, dtype=np.float32)
+    count = np.zeros(g.n_params, dtype=np.uint32)
+    lib().orc_grid_bwd_stats(ctypes.byref(g), B, _p(pos), _p(dL_dy16), _p(absum), _p(count))
+    return absum, count
+
+
+def grid_grad_tolerance(g, pos, dL_dy16, ref_grad):
+    """Per-element bound |gpu - oracle| of a grid gradient (fp32 [n_params]).
+
+    The GPU sums the exact fp32 products w16 * dL/dy as int32 fixed point with step
+    2^-e <= 2^-29.9 * sum_i max_f |dL/dy_i,f| (level sum over at most all B points, grid.hip /
+    grid_bin.hip), so each update is off by at most half a step: count * 2^-30.9 * S_level. The
+    oracle sums the same products sequentially in fp32: (count - 1) * 2^-24 * sum |update|; the final
+    int32 -> fp32 conversion rounds once more (2^-24 relative)."""
+    B = pos.shape[0]
+    L, F = g.n_levels, g.n_features_per_level
+    absum, count = grid_bwd_stats(g, pos, dL_dy16)
+    dy = np.abs(h2f(np.asarray(dL_dy16, dtype=np.uint16)).reshape(L, F, B).astype(np.float64))
+    S = dy.max(axis=1).sum(axis=1)  # per level
+    tol = np.zeros(g.n_params, dtype=np.float64)
+    for l in range(L):
+        a, b = g.offsets[l] * F, g.offsets[l + 1] * F
+        tol[a:b] = count[a:b] * S[l] * 2.0 ** -29.9
+    tol += count * 2.0 ** -24 * absum.astype(np.float64) + 2.0 ** -23 * np.abs(np.asarray(ref_grad, dtype=np.float64))
+    return tol
 
 
 def grid_bwd_input(g, pos, table16, dL_dy16):

@@ -351,10 +351,15 @@ void orc_grid_fwd(const orc_grid* g, uint32_t B, const float* pos_in, const uint
 }
 
 /* kernel_grid_backward, grid.h:214-320, ideal precision (fp32 sums of exact products). */
-void orc_grid_bwd(const orc_grid* g, uint32_t B, const float* pos_in, const uint16_t* dL_dy, float* grad) {
+/* ADD: one update of grid parameter (level base + p): the gradient sum, or (stats mode) the sum of
+ * |update| and the number of updates per parameter -- the per-element tolerance of the GPU tests */
+#define ADD(p, v) do { const float v_ = (v); if (grad) grad[base + (p)] += v_; \
+	if (abssum) { abssum[base + (p)] += fabsf(v_); count[base + (p)] += 1; } } while (0)
+static void grid_bwd_impl(const orc_grid* g, uint32_t B, const float* pos_in, const uint16_t* dL_dy, float* grad, float* abssum,
+                          uint32_t* count) {
 	const uint32_t D = g->n_pos_dims, F = g->n_features_per_level, L = g->n_levels;
 	for (uint32_t l = 0; l < L; ++l) {
-		float* gg = grad + (size_t)g->offsets[l] * F;
+		const size_t base = (size_t)g->offsets[l] * F;
 		const float scale = g->scales[l];
 		for (uint32_t i = 0; i < B; ++i) {
 			float pos[8], dy[8];
@@ -364,14 +369,14 @@ void orc_grid_bwd(const orc_grid* g, uint32_t B, const float* pos_in, const uint
 			if (orc_masked_bwd(g, l, i)) continue;
 			if (g->interpolation == ORC_INTERP_NEAREST) {
 				uint32_t idx = orc_grid_index(g, l, pg) * F;
-				for (uint32_t f = 0; f < F; ++f) gg[idx + f] += dy[f];
+				for (uint32_t f = 0; f < F; ++f) ADD(idx + f, dy[f]);
 				continue;
 			}
 			if (g->opts && g->stochastic) { /* grid.h:284-298 */
 				const float sample = orc_random_val(1337u, i + l * B);
 				for (uint32_t d = 0; d < D; ++d) local[d] = sample >= pos[d] ? pg[d] : pg[d] + 1;
 				uint32_t idx = orc_grid_index(g, l, local) * F;
-				for (uint32_t f = 0; f < F; ++f) gg[idx + f] += dy[f];
+				for (uint32_t f = 0; f < F; ++f) ADD(idx + f, dy[f]);
 				continue;
 			}
 			for (uint32_t c = 0; c < (1u << D); ++c) {
@@ -382,10 +387,20 @@ void orc_grid_bwd(const orc_grid* g, uint32_t B, const float* pos_in, const uint
 				}
 				float wh = orc_h2f(orc_f2h(w));
 				uint32_t idx = orc_grid_index(g, l, local) * F;
-				for (uint32_t f = 0; f < F; ++f) gg[idx + f] += wh * dy[f];
+				for (uint32_t f = 0; f < F; ++f) ADD(idx + f, wh * dy[f]);
 			}
 		}
 	}
+}
+
+#undef ADD
+
+void orc_grid_bwd(const orc_grid* g, uint32_t B, const float* pos_in, const uint16_t* dL_dy, float* grad) {
+	grid_bwd_impl(g, B, pos_in, dL_dy, grad, NULL, NULL);
+}
+
+void orc_grid_bwd_stats(const orc_grid* g, uint32_t B, const float* pos_in, const uint16_t* dL_dy, float* abssum, uint32_t* count) {
+	grid_bwd_impl(g, B, pos_in, dL_dy, NULL, abssum, count);
 }
 
 /* kernel_grid dy_dx branch (grid.h:171-211) + kernel_grid_backward_input (grid.h:322-349):

@@ -79,6 +79,8 @@ void orc_grid_fwd(const orc_grid* g, uint32_t B, const float* pos, const uint16_
 /* kernel_grid_backward (grid.h:214-320) in ideal precision: grad[p] += float(half(w))*float(dLdy);
  * dL_dy SoA fp16 [(l*F+f)*B + i]; grad fp32 [n_params] is accumulated into (caller zeroes). */
 void orc_grid_bwd(const orc_grid* g, uint32_t B, const float* pos, const uint16_t* dL_dy, float* grad);
+/* same loop: per grid parameter, the sum of |update| and the number of updates (accumulated into) */
+void orc_grid_bwd_stats(const orc_grid* g, uint32_t B, const float* pos, const uint16_t* dL_dy, float* abssum, uint32_t* count);
 /* dL/dx fp32 [B][D] through the grid (grid.h:171-211 dy_dx + 322-349 backward_input);
  * dL_dy SoA fp16 [(l*F+f)*B + i] (F <= 4, D <= 8) */
 void orc_grid_bwd_input(const orc_grid* g, uint32_t B, const float* pos, const uint16_t* table, const uint16_t* dL_dy,
