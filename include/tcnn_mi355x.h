@@ -46,6 +46,11 @@ void tcnn_free_temporary_memory(void);            /* cpp::free_temporary_memory(
 int tcnn_has_networks(void);                      /* cpp::has_networks() */
 float tcnn_default_loss_scale(int precision);     /* cpp::default_loss_scale() */
 int tcnn_preferred_precision(void);               /* cpp::preferred_precision() */
+/* cpp::set_log_callback(fn) (cpp_api.h:70, src/cpp_api.cu:61-63; common_host.h:46-66): severity is
+ * the reference's LogSeverity order (0 Info, 1 Debug, 2 Warning, 3 Error, 4 Success); NULL removes
+ * the callback. Called synchronously from whichever thread logs. */
+typedef void (*tcnn_log_callback_t)(int severity, const char* message, void* user);
+void tcnn_set_log_callback(tcnn_log_callback_t callback, void* user);
 
 /* ---- runtime module FFI (cpp_api.h:86-117) ---- */
 /* cpp::create_network_with_input_encoding(n_input_dims, n_output_dims, encoding, network) */
@@ -130,7 +135,8 @@ int tcnn_trainer_set_params_full_precision(tcnn_trainer* t, const float* host_pa
 /* Snapshot in the reference's format: the msgpack bytes of Trainer::serialize(with_optimizer)
  * (trainer.h:275-315, adam.h:278-299). Call with buf == NULL to get the size. */
 int tcnn_trainer_serialize(tcnn_trainer* t, int with_optimizer, void* buf, uint64_t capacity, uint64_t* size);
-/* Trainer::deserialize: params_type "__half" or "float", optional optimizer state. */
+/* Trainer::deserialize: msgpack bytes (or the JSON text of the same object, binaries as {"bytes": [...]},
+ * gpu_memory_json.h:52-71); params_type "__half" or "float", optional optimizer state. */
 int tcnn_trainer_deserialize(tcnn_trainer* t, const void* buf, uint64_t size);
 uint32_t tcnn_trainer_optimizer_step_count(const tcnn_trainer* t);
 /* Engine diagnostics: name of the path the trainer runs ("fused" / "layered" / "unsupported"). */

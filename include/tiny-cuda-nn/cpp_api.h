@@ -66,8 +66,21 @@ inline float default_loss_scale(Precision p) {
 inline Precision preferred_precision() {
 	return tcnn_preferred_precision() == TCNN_PRECISION_FP16 ? Precision::Fp16 : Precision::Fp32;
 }
-// The engine emits no log messages; the callback is accepted for source compatibility.
-inline void set_log_callback(const std::function<void(LogSeverity, const std::string&)>&) {}
+// cpp_api.cu:61-63: the engine's log messages (grid level table, trainer init, engine fallbacks)
+// reach `callback`; an empty function removes it.
+namespace detail {
+inline std::function<void(LogSeverity, const std::string&)>& log_fn() {
+	static std::function<void(LogSeverity, const std::string&)> f;
+	return f;
+}
+inline void log_trampoline(int severity, const char* msg, void*) {
+	if (log_fn()) log_fn()((LogSeverity)severity, msg);
+}
+}  // namespace detail
+inline void set_log_callback(const std::function<void(LogSeverity, const std::string&)>& callback) {
+	detail::log_fn() = callback;
+	tcnn_set_log_callback(callback ? &detail::log_trampoline : nullptr, nullptr);
+}
 
 struct Context {  // cpp_api.h:82-84
 	std::unique_ptr<tcnn::Context> ctx;

@@ -32,7 +32,7 @@ __device__ __forceinline__ bool adam_core(const AdamArgs& a, uint32_t i, float g
 	float lr = a.lr;
 	if (i >= a.n_matrix) lr *= a.nonmat_lr_factor;
 	const uint32_t st = ++step;
-	lr *= (a.cached_factor && st == a.cached_step) ? *a.cached_factor : adam_bias_factor(a, st);
+	lr *= (st - 1u < a.factor_n) ? a.factor_table[st - 1u] : adam_bias_factor(a, st);
 	const float eff = fminf(fmaxf(lr / (sqrtf(m2) + a.eps), a.lower_lr_bound), a.upper_lr_bound);
 	const float decayed = __builtin_fmaf(1.0f - a.rel_decay * lr, wfp, -copysignf(a.abs_decay * lr, wfp));
 	float nw = __builtin_fmaf(-eff, m1, decayed);
@@ -56,6 +56,49 @@ __device__ __forceinline__ _Float16 adam_update(const AdamArgs& a, const AdamBuf
 	const _Float16 h = f16_rn(w);
 	s.w16[i] = h;
 	return h;
+}
+
+// Adam state of 4 consecutive parameters (i % 4 == 0): one 16-byte load per state array, so a
+// thread keeps 5 independent HBM round trips in flight instead of a chain of scalar ones.
+struct AdamState4 {
+	f4 w, m1, m2;
+	uint4 st;
+	h4 w16;
+};
+
+__device__ __forceinline__ AdamState4 adam_load4(const AdamBuffers& s, uint32_t i) {
+	AdamState4 v;
+	v.w = *(const f4*)(s.w32 + i);
+	v.m1 = *(const f4*)(s.m1 + i);
+	v.m2 = *(const f4*)(s.m2 + i);
+	v.st = *(const uint4*)(s.steps + i);
+	v.w16 = *(const h4*)(s.w16 + i);
+	return v;
+}
+
+// adam_update on parameters i .. i+3 from their loaded state; same per-parameter arithmetic and
+// skip rule. A group with no updated parameter writes nothing back (like the scalar path); otherwise
+// skipped parameters are rewritten with their unchanged values.
+__device__ __forceinline__ void adam_store4(const AdamArgs& a, const AdamBuffers& s, uint32_t i, const float (&gsum)[4], AdamState4 v) {
+	float w[4] = {v.w.x, v.w.y, v.w.z, v.w.w}, m1[4] = {v.m1.x, v.m1.y, v.m1.z, v.m1.w}, m2[4] = {v.m2.x, v.m2.y, v.m2.z, v.m2.w};
+	uint32_t st[4] = {v.st.x, v.st.y, v.st.z, v.st.w};
+	h4 g16, h = v.w16;
+	bool any = false;
+#pragma unroll
+	for (int r = 0; r < 4; ++r) {
+		_Float16 gr;
+		const bool upd = adam_core(a, i + r, gsum[r], gr, w[r], m1[r], m2[r], st[r]);
+		g16[r] = gr;
+		if (upd) h[r] = f16_rn(w[r]);
+		any = any || upd;
+	}
+	if (s.g16) *(h4*)(s.g16 + i) = g16;
+	if (!any) return;
+	*(f4*)(s.w32 + i) = f4{w[0], w[1], w[2], w[3]};
+	*(f4*)(s.m1 + i) = f4{m1[0], m1[1], m1[2], m1[3]};
+	*(f4*)(s.m2 + i) = f4{m2[0], m2[1], m2[2], m2[3]};
+	*(uint4*)(s.steps + i) = make_uint4(st[0], st[1], st[2], st[3]);
+	*(h4*)(s.w16 + i) = h;
 }
 
 // Fixed-order sum of n slab values src[j * stride], j = 0 .. n-1, with the loads issued 8 at a time

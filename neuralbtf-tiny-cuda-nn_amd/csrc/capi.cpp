@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <mutex>
 
 #include "runtime.h"
 
@@ -12,6 +13,10 @@ using namespace tcnn_amd;
 namespace {
 thread_local std::string g_last_error;
 thread_local std::string g_str;
+
+std::mutex g_log_mutex;
+tcnn_log_callback_t g_log_cb = nullptr;
+void* g_log_user = nullptr;
 
 template <typename F>
 int guard(F&& f) {
@@ -208,6 +213,12 @@ int tcnn_set_cuda_device(int device) {
 }
 void tcnn_free_temporary_memory(void) {}
 int tcnn_has_networks(void) { return 1; }
+
+void tcnn_set_log_callback(tcnn_log_callback_t cb, void* user) {
+	std::lock_guard<std::mutex> lk(g_log_mutex);
+	g_log_cb = cb;
+	g_log_user = user;
+}
 float tcnn_default_loss_scale(int precision) { return precision == TCNN_PRECISION_FP32 ? 1.0f : 128.0f; }
 int tcnn_preferred_precision(void) { return TCNN_PRECISION_FP16; }
 
@@ -431,3 +442,10 @@ int tcnn_debug_probe(void* stream, float* mfma_out, int16_t* tr_out) {
 }
 
 }  // extern "C"
+
+namespace tcnn_amd {
+void log_msg(LogSeverity s, const std::string& msg) {
+	std::lock_guard<std::mutex> lk(g_log_mutex);
+	if (g_log_cb) g_log_cb((int)s, msg.c_str(), g_log_user);
+}
+}  // namespace tcnn_amd

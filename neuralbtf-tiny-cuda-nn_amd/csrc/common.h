@@ -83,6 +83,15 @@ __device__ __forceinline__ _Float16 f16_rn(float x) {
 	return (_Float16)x;
 }
 
+// Engine log (reference common_host.h:46-66: LogSeverity, log_callback, log_info/debug/warning).
+// Messages go to the callback installed through tcnn_set_log_callback (capi.cpp); without one they
+// are dropped (the reference's default prints to stdout; a library embedded in a torch process should
+// not). Severity values are the reference's enum order.
+enum class LogSeverity : int { Info = 0, Debug = 1, Warning = 2, Error = 3, Success = 4 };
+void log_msg(LogSeverity s, const std::string& msg);
+inline void log_debug(const std::string& m) { log_msg(LogSeverity::Debug, m); }
+inline void log_warning(const std::string& m) { log_msg(LogSeverity::Warning, m); }
+
 inline uint32_t div_round_up(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
 // Grow-only scratch allocation owned by a launcher (not stream-ordered: callers on one stream).

@@ -117,9 +117,10 @@ void launch_fused_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, ui
                         uint32_t B, uint32_t dims, float loss_scale, const void* params16, const void* table16,
                         const float* pos, const float* target, void* out16, void* dLdenc_pairs,
                         float* wgrad_partial, float* loss_partial, const LevelInfo* levels, bool hash_grid,
-                        Interp interp, uint32_t n_blocks, const void* dout16, const void* wimage) {
+                        Interp interp, uint32_t n_blocks, const void* dout16, const void* wimage, uint32_t loss_l2) {
 	TCNN_CHECK(B % 32 == 0, "fused train: batch must be a multiple of 32");
 	FusedTrainArgs a;
+	a.loss_l2 = loss_l2;
 	a.wimage = (const _Float16*)wimage;
 	a.dout = (const _Float16*)dout16;
 	a.B = B;

@@ -299,23 +299,43 @@ __global__ __launch_bounds__(ACC_THREADS) void k_grid_acc(int layout, uint32_t B
 	// write out: grid parameter p = (offset + e0 + entry) * F + f
 	const float inv = finite ? ldexpf(1.0f, -e) : __builtin_nanf("");
 	const uint32_t p0 = (li.offset + e0) * F;
-	for (uint32_t j = threadIdx.x; j < ne * F; j += ACC_THREADS) {
-		float g;
+	auto grad_of = [&](uint32_t j) -> float {
 		if constexpr (F == 2) {
 			const long long t64 = ((const long long*)acc)[j >> 1];
 			const int lo = (int)(uint32_t)(unsigned long long)t64;
 			const int hi = (int)((t64 - (long long)lo) >> 32);
-			g = (float)((j & 1) ? hi : lo) * inv;
+			return (float)((j & 1) ? hi : lo) * inv;
 		} else {
-			g = (float)acc[j] * inv;
+			return (float)acc[j] * inv;
 		}
-		const uint32_t p = p0 + j;
-		if (apply_adam) {
-			const uint32_t i = ad.param_base + p;
-			if (ad.write_grad32) ad.buf.g32[i] = g;
-			adam_update(ad.a, ad.buf, i, g);
-		} else {
-			grad32[p] = g;
+	};
+	if (!apply_adam) {
+		for (uint32_t j = threadIdx.x; j < ne * F; j += ACC_THREADS) grad32[p0 + j] = grad_of(j);
+		return;
+	}
+	// Adam on groups of 4 parameters (ne * F and the parameter base are multiples of 4: level offsets
+	// are multiples of 8 entries, the network block of 16); two groups per thread have their state
+	// loads in flight together
+	const uint32_t n4 = ne * F / 4;
+	for (uint32_t q0 = threadIdx.x; q0 < n4; q0 += 2 * ACC_THREADS) {
+		AdamState4 sv[2];
+		float g[2][4];
+#pragma unroll
+		for (uint32_t u = 0; u < 2; ++u) {
+			const uint32_t q = q0 + u * ACC_THREADS;
+			if (q < n4) {
+				sv[u] = adam_load4(ad.buf, ad.param_base + p0 + 4 * q);
+#pragma unroll
+				for (uint32_t r = 0; r < 4; ++r) g[u][r] = grad_of(4 * q + r);
+			}
+		}
+#pragma unroll
+		for (uint32_t u = 0; u < 2; ++u) {
+			const uint32_t q = q0 + u * ACC_THREADS;
+			if (q >= n4) break;
+			const uint32_t i = ad.param_base + p0 + 4 * q;
+			if (ad.write_grad32) *(f4*)(ad.buf.g32 + i) = f4{g[u][0], g[u][1], g[u][2], g[u][3]};
+			adam_store4(ad.a, ad.buf, i, g[u], sv[u]);
 		}
 	}
 }
@@ -379,6 +399,8 @@ static void grid_acc_t(hipStream_t st, int layout, uint32_t dys, uint32_t B, con
 	GridAccAdam adv{};
 	if (ad) adv = *ad;
 	TCNN_CHECK(a.acc_lds_bytes <= GRID_ACC_LDS_BYTES, "grid acc: slice exceeds the LDS budget");
+	TCNN_CHECK(!ad || (ad->param_base % 4 == 0 && ((uintptr_t)ad->buf.w32 & 15) == 0 && ((uintptr_t)ad->buf.w16 & 7) == 0),
+	           "grid acc: Adam buffers must be 16-byte aligned with a parameter base that is a multiple of 4");
 	hipLaunchKernelGGL((k_grid_acc<NC, F>), dim3(a.n_buckets), dim3(ACC_THREADS), a.acc_lds_bytes, st, layout, B, dy, dys, lv, a, grad32, adv,
 	                   ad ? 1 : 0);
 }

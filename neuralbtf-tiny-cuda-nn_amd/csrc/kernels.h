@@ -81,10 +81,12 @@ struct AdamArgs {
 	uint32_t begin;
 	const float* part;
 	uint32_t n_parts, part_stride;
-	// bias-correction factor sqrt(1 - beta2^t) / (1 - beta1^t) precomputed on the device for
-	// t == cached_step (nullptr: always computed per parameter; same device arithmetic either way)
-	const float* cached_factor;
-	uint32_t cached_step;
+	// bias-correction factors sqrt(1 - beta2^t) / (1 - beta1^t) precomputed on the device by the
+	// same adam_bias_factor for t = 1 .. factor_n (factor_table[t - 1]); other t are computed per
+	// parameter. Parameters carry their own step counts (adam.h:110-113), so without the table every
+	// grid entry paid two powf -- the Adam epilogue of the binned backward was VALU-bound on them.
+	const float* factor_table;
+	uint32_t factor_n;
 	// grid slabs: parameter i reads slab element grid_slab_index(part_map, i - begin) (nullptr: i - begin)
 	const GridSlabMap* part_map;
 };
@@ -134,7 +136,7 @@ void launch_fused_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, ui
                         uint32_t B, uint32_t dims, float loss_scale, const void* params16, const void* table16,
                         const float* pos, const float* target, void* out16, void* dLdenc_pairs,
                         float* wgrad_partial, float* loss_partial, const LevelInfo* levels, bool hash_grid,
-                        Interp interp, uint32_t n_blocks, const void* dout16, const void* wimage);
+                        Interp interp, uint32_t n_blocks, const void* dout16, const void* wimage, uint32_t loss_l2 = 0);
 // LDS weight image of the fused kernels, built once per parameter update.
 size_t fused_weight_image_bytes(uint32_t W, uint32_t IN, uint32_t NH);
 void launch_pack_weights(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, const void* params16, void* image);
@@ -198,10 +200,15 @@ constexpr uint32_t MLP_TAIL_GROUPS = 16;
 // out[p] = sum_j in[j*stride + grid_slab_index(map, p)] (the grid backward's slabs, fixed order)
 void launch_grid_slab_reduce(hipStream_t st, const float* in, uint32_t n_parts, uint32_t stride, uint32_t n, float* out,
                              const GridSlabMap* map);
-// out[p] = sum_j in[j*stride + p] (p < n), optional fp16 copy
+// out[p] = sum_j in[j*stride + p] (p < n). tmp: caller-owned device scratch of
+// reduce_partials_tmp_floats(n_parts, n) floats (per workspace, so concurrent modules / streams /
+// devices never share it)
+size_t reduce_partials_tmp_floats(uint32_t n_parts, uint32_t n);
 void launch_reduce_partials(hipStream_t st, const float* in, uint32_t n_parts, uint32_t stride, uint32_t n,
-                            float* out);
+                            float* out, float* tmp);
 
+// factor_table[t - 1] = adam_bias_factor(a, t) for t in (lo, hi]
+void launch_fill_bias_factors(hipStream_t st, const AdamArgs& a, float* table, uint32_t lo, uint32_t hi);
 void launch_adam(hipStream_t st, const AdamArgs& a, float* w32, void* w16, const float* grad32, void* grad16,
                  float* m1, float* m2, uint32_t* steps);
 
@@ -230,7 +237,7 @@ void launch_wgrad(hipStream_t st, uint32_t B, uint32_t N, uint32_t K, const void
                   uint32_t n_chunks);
 uint32_t relative_l2_n_blocks(uint32_t B, uint32_t stride);
 void launch_relative_l2_partial(hipStream_t st, uint32_t B, uint32_t stride, uint32_t dims, float loss_scale, const void* pred16,
-                                const float* target, void* grads16, float* loss_partial);
+                                const float* target, void* grads16, float* loss_partial, uint32_t loss_l2 = 0);
 
 // ---- OneBlob / Identity encodings (encodings.hip); output AoS fp16 [B][out_stride], padding = 1 ----
 void launch_oneblob_fwd(hipStream_t st, uint32_t B, uint32_t D, uint32_t n_bins, const float* x, uint32_t x_stride, void* out16,

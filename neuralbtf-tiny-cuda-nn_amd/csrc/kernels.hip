@@ -73,9 +73,14 @@ void launch_column_sums(hipStream_t st, const float* in, uint32_t n_parts, uint3
 	TCNN_HIP_CHECK(hipGetLastError());
 }
 
-static DevBufLite g_red_tmp;
+size_t reduce_partials_tmp_floats(uint32_t n_parts, uint32_t n) {
+	constexpr uint32_t MAXG = 16;
+	if (n_parts <= MAXG) return 0;
+	const uint32_t group = div_round_up(n_parts, MAXG);
+	return (size_t)div_round_up(n_parts, group) * ((n + 3) / 4 * 4);
+}
 
-void launch_reduce_partials(hipStream_t st, const float* in, uint32_t n_parts, uint32_t stride, uint32_t n, float* out) {
+void launch_reduce_partials(hipStream_t st, const float* in, uint32_t n_parts, uint32_t stride, uint32_t n, float* out, float* tmp) {
 	if (n == 0) return;
 	constexpr uint32_t MAXG = 16;
 	const uint32_t bx = div_round_up(div_round_up(n, 4), 256);
@@ -85,11 +90,22 @@ void launch_reduce_partials(hipStream_t st, const float* in, uint32_t n_parts, u
 		const uint32_t group = div_round_up(n_parts, MAXG);
 		const uint32_t G = div_round_up(n_parts, group);
 		const uint32_t ostride = (n + 3) / 4 * 4;
-		float* tmp = (float*)g_red_tmp.get((size_t)G * ostride * 4);
+		TCNN_CHECK(tmp != nullptr, "reduce partials: scratch missing");
 		hipLaunchKernelGGL(k_reduce_groups, dim3(bx, G), dim3(256), 0, st, in, n_parts, group, stride, n, tmp, ostride);
 		TCNN_HIP_CHECK(hipGetLastError());
 		hipLaunchKernelGGL(k_reduce_groups, dim3(bx, 1), dim3(256), 0, st, tmp, G, G, ostride, n, out, 0u);
 	}
+	TCNN_HIP_CHECK(hipGetLastError());
+}
+
+__global__ __launch_bounds__(256) void k_fill_bias_factors(const AdamArgs a, float* __restrict__ table, uint32_t lo, uint32_t hi) {
+	const uint32_t t = lo + 1 + blockIdx.x * blockDim.x + threadIdx.x;
+	if (t <= hi) table[t - 1] = adam_bias_factor(a, t);
+}
+
+void launch_fill_bias_factors(hipStream_t st, const AdamArgs& a, float* table, uint32_t lo, uint32_t hi) {
+	if (hi <= lo) return;
+	hipLaunchKernelGGL(k_fill_bias_factors, dim3(div_round_up(hi - lo, 256)), dim3(256), 0, st, a, table, lo, hi);
 	TCNN_HIP_CHECK(hipGetLastError());
 }
 

@@ -164,6 +164,7 @@ struct FusedTrainArgs {
 	uint32_t dims;          // target width (n_output_dims)
 	float loss_scale;
 	float n_total;          // (float)(B * dims) as in relative_l2.h:64
+	uint32_t loss_l2;       // 0: RelativeL2 (relative_l2.h:40-76), 1: L2 (l2.h:40-76)
 	const _Float16* params; // MLP weights fp16 [W0 | hidden | Wout]
 	const uint32_t* table;  // grid params as half2 entries (F == 2)
 	const float* pos;       // [B][D]
@@ -284,7 +285,7 @@ __device__ __forceinline__ void slice_fwd_loss(const FusedTrainArgs& a, uint32_t
 				const uint32_t o = 4 * q + r;
 				if (o < a.dims) {
 					const float p = (float)y[r];
-					const float pse = __builtin_fmaf(p, p, 0.01f);
+					const float pse = a.loss_l2 ? 1.0f : __builtin_fmaf(p, p, 0.01f);  // L2: pdf = 1
 					const float d = p - target(tau, o);
 					loss += d * d / pse / a.n_total;
 					const float gr = 2.0f * d / pse;

@@ -428,8 +428,9 @@ void launch_wgrad(hipStream_t st, uint32_t B, uint32_t N, uint32_t K, const void
 	TCNN_HIP_CHECK(hipGetLastError());
 }
 
-// RelativeL2 (losses/relative_l2.h:40-76) over pred fp16 [B][stride]; per-workgroup loss sums.
-__global__ __launch_bounds__(256) void k_relative_l2_partial(uint32_t n_elements, uint32_t stride, uint32_t dims, float loss_scale,
+// RelativeL2 (losses/relative_l2.h:40-76) or L2 (losses/l2.h:40-76, l2 != 0) over pred fp16
+// [B][stride]; per-workgroup loss sums.
+__global__ __launch_bounds__(256) void k_relative_l2_partial(uint32_t l2, uint32_t n_elements, uint32_t stride, uint32_t dims, float loss_scale,
                                                               float n_total, const _Float16* __restrict__ pred,
                                                               const float* __restrict__ target, _Float16* __restrict__ grads,
                                                               float* __restrict__ loss_partial) {
@@ -442,7 +443,7 @@ __global__ __launch_bounds__(256) void k_relative_l2_partial(uint32_t n_elements
 			continue;
 		}
 		const float p = (float)pred[i];
-		const float pse = __builtin_fmaf(p, p, 0.01f);
+		const float pse = l2 ? 1.0f : __builtin_fmaf(p, p, 0.01f);
 		const float d = p - target[inter * dims + intra];
 		s += d * d / pse / n_total;
 		const float gr = 2.0f * d / pse;
@@ -458,10 +459,10 @@ __global__ __launch_bounds__(256) void k_relative_l2_partial(uint32_t n_elements
 uint32_t relative_l2_n_blocks(uint32_t B, uint32_t stride) { return std::max(1u, std::min(div_round_up((uint64_t)B * stride, 256), 1024u)); }
 
 void launch_relative_l2_partial(hipStream_t st, uint32_t B, uint32_t stride, uint32_t dims, float loss_scale, const void* pred16,
-                                const float* target, void* grads16, float* loss_partial) {
+                                const float* target, void* grads16, float* loss_partial, uint32_t loss_l2) {
 	const uint32_t n = B * stride;
 	if (!n) return;
-	hipLaunchKernelGGL(k_relative_l2_partial, dim3(relative_l2_n_blocks(B, stride)), dim3(256), 0, st, n, stride, dims, loss_scale,
+	hipLaunchKernelGGL(k_relative_l2_partial, dim3(relative_l2_n_blocks(B, stride)), dim3(256), 0, st, loss_l2, n, stride, dims, loss_scale,
 	                   (float)((uint64_t)B * dims), (const _Float16*)pred16, target, (_Float16*)grads16, loss_partial);
 	TCNN_HIP_CHECK(hipGetLastError());
 }

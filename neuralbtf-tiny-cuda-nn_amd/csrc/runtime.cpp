@@ -173,6 +173,8 @@ GridEncodingHost::GridEncodingHost(uint32_t n_dims, const json& enc) {
 		if (gt == GridType::Tiled) params = std::min(params, powi_u32(base, n_dims));
 		else if (gt == GridType::Hash) params = std::min(params, 1u << desc.log2_hashmap_size);
 		levels[l] = LevelInfo{scale, res, offset, params};
+		log_debug("GridEncoding at level " + std::to_string(l) + ": resolution=" + std::to_string(res) +
+		          " params_in_level=" + std::to_string(params));  // grid.h:717
 		offset += params;
 	}
 	n_params = offset * F;
@@ -490,6 +492,8 @@ NetworkHost::NetworkHost(uint32_t n_in, uint32_t n_out, const json& e, const jso
 	mlp = MlpHost(enc->padded_output_width(), n_out, net);
 	TCNN_CHECK(fused_ok() || layered_ok(), "network shape (n_neurons = " + std::to_string(mlp.width) + ", input width " +
 	                                           std::to_string(mlp.n_input) + ") is not supported by the MI355X engine");
+	log_debug(std::string("NetworkWithInputEncoding: ") + mlp.otype + " (n_neurons=" + std::to_string(mlp.width) +
+	          ", n_hidden_layers=" + std::to_string(mlp.n_hidden_layers) + ") runs on the " + engine() + " engine");
 }
 
 bool NetworkHost::fused_ok() const {
@@ -580,7 +584,7 @@ void NetworkHost::fused_kernel(hipStream_t st, StepWorkspace& ws, uint32_t B, co
 	launch_fused_train(st, mlp.width, mlp.n_input, mlp.n_hidden_layers, grid->desc.n_pos_dims, grid->desc.hash_type,
 	                   mlp.activation, B, dims, loss_scale, params16, table, pos, target, out16, ws.dLdenc.p,
 	                   ws.wgrad_partial.as<float>(), ws.loss_partial.as<float>(), grid->dev_levels(), grid->hash_grid(),
-	                   grid->desc.interp, nb, dout16, ws.wimage.p);
+	                   grid->desc.interp, nb, dout16, ws.wimage.p, loss_l2);
 }
 
 void NetworkHost::grid_backward(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, GridBwdEpilogue* ep) {
@@ -646,7 +650,7 @@ void NetworkHost::fwd_bwd_layered(hipStream_t st, StepWorkspace& ws, uint32_t B,
 	} else {
 		const uint32_t nl = relative_l2_n_blocks(B, OUTP);
 		ws.loss_partial.reserve((size_t)nl * 4);
-		launch_relative_l2_partial(st, B, OUTP, dims, loss_scale, out, target, ws.dout16.p, ws.loss_partial.as<float>());
+		launch_relative_l2_partial(st, B, OUTP, dims, loss_scale, out, target, ws.dout16.p, ws.loss_partial.as<float>(), loss_l2);
 		ws.n_loss_partials = nl;
 	}
 	launch_act_bwd_inplace(st, B * OUTP, mlp.output_activation, out, ws.dout16.p);
@@ -655,7 +659,9 @@ void NetworkHost::fwd_bwd_layered(hipStream_t st, StepWorkspace& ws, uint32_t B,
 	auto w_off = [&](uint32_t j) -> size_t { return j == 0 ? 0 : (size_t)W * IN + (size_t)(j - 1) * W * W; };
 	auto wgrad = [&](uint32_t N, uint32_t K, const void* dy, const void* x, size_t off) {
 		launch_wgrad(st, B, N, K, dy, x, ws.wgrad_partial.as<float>(), nck);
-		launch_reduce_partials(st, ws.wgrad_partial.as<float>(), nck, N * K, N * K, grad32 + off);
+		const size_t tf = reduce_partials_tmp_floats(nck, N * K);
+		if (tf) ws.red_tmp.reserve(tf * 4);
+		launch_reduce_partials(st, ws.wgrad_partial.as<float>(), nck, N * K, N * K, grad32 + off, ws.red_tmp.as<float>());
 	};
 	_Float16* dcur = ws.delta0.as<_Float16>();
 	_Float16* dnext = ws.delta1.as<_Float16>();
@@ -696,17 +702,20 @@ TrainerHost::TrainerHost(uint32_t n_in, uint32_t n_out, const json& cfg, uint32_
 	const json opt = jhas(cfg, "optimizer") ? cfg["optimizer"] : json::object();
 	const json los = jhas(cfg, "loss") ? cfg["loss"] : json::object();
 	loss_otype = jval<std::string>(los, "otype", "RelativeL2");
-	TCNN_CHECK(ieq(loss_otype, "RelativeL2"), "Loss '" + loss_otype + "' is not implemented by the MI355X engine yet");
+	TCNN_CHECK(ieq(loss_otype, "RelativeL2") || ieq(loss_otype, "L2"),
+	           "Loss '" + loss_otype + "' is not implemented by the MI355X engine (RelativeL2, L2)");
 	const std::string oo = jval<std::string>(opt, "otype", "Adam");
 	TCNN_CHECK(ieq(oo, "Adam"), "Optimizer '" + oo + "' is not implemented by the MI355X engine yet");
 	adam.update(opt);
 	model = std::make_unique<NetworkHost>(n_in, n_out, enc, net);
+	model->loss_l2 = ieq(loss_otype, "L2") ? 1u : 0u;
 	n_params = model->n_params();
 	n_mlp = model->mlp.n_params();
 	initialize_params(seed);
 }
 
 void TrainerHost::initialize_params(uint32_t seed) {
+	log_debug("Trainer: initializing " + std::to_string(n_params) + " params and resetting training.");  // trainer.h:70
 	// trainer.h:52-55: pcg32{seed_seq{seed}.generate()[0]}
 	std::seed_seq seq{seed};
 	std::vector<uint32_t> seeds(2);
@@ -737,6 +746,7 @@ void TrainerHost::initialize_params(uint32_t seed) {
 
 void TrainerHost::set_params_full_precision(const float* host, uint64_t n) {
 	TCNN_CHECK(n == n_params, "Can't set fp params because buffer has the wrong size.");
+	TCNN_HIP_CHECK(hipDeviceSynchronize());  // queued training work must not race the upload
 	TCNN_HIP_CHECK(hipMemcpy(w32.p, host, n * 4, hipMemcpyHostToDevice));
 	launch_cast_f32_f16(nullptr, w32.as<float>(), w16.p, n_params);
 	ws.wimage_valid = false;
@@ -780,39 +790,37 @@ void TrainerHost::training_step_overlapped(hipStream_t st, uint32_t B, const flo
 	GridBwdEpilogue ep{};
 	ep.enabled = 1;
 	ep.apply_adam = run_optimizer ? 1 : 0;
-	ep.adam_mlp = adam_args();
+	// bias factors of earlier steps from the table; this step's entry is written by the launch's
+	// workgroup 0 (grid_bwd_mlp_tail) for the Adam launches that follow
+	ep.adam_mlp = run_optimizer ? adam_args_table(st, adam_step - 1, adam_step) : adam_args();
 	ep.adam_mlp.n = (uint32_t)n_mlp;
 	ep.buf = AdamBuffers{w32.as<float>(), w16.as<_Float16>(), g32.as<float>(), g16.as<_Float16>(), m1.as<float>(), m2.as<float>(),
 	                     steps.as<uint32_t>()};
 	ep.n_mlp_groups = MLP_TAIL_GROUPS;
 	ep.n_mlp = (uint32_t)n_mlp;
 	ep.d_loss = d_loss.as<float>();
-	d_factor.reserve(4);
-	ep.factor_out = d_factor.as<float>();
-	ep.factor_step = adam_step;  // parameters updated every step have step count == adam_step
+	ep.factor_out = run_optimizer ? d_ftable.as<float>() + (adam_step - 1) : nullptr;
+	ep.factor_step = adam_step;
 	TCNN_CHECK(n_mlp % 4 == 0, "network parameter count must be a multiple of 4");
 	m.grid_backward(st, ws, B, input, &ep);
+	if (run_optimizer) ftable_valid = adam_step;
 	GridEncodingHost& g = *m.grid;
 	if (run_optimizer) {
 		// binned levels: Adam applied by the accumulate pass; LDS levels: Adam summing their slabs
 		GridAccAdam ga{};
-		ga.a = adam_args();
-		ga.a.cached_factor = d_factor.as<float>();
-		ga.a.cached_step = adam_step;
+		ga.a = adam_args_table(st, adam_step);
 		ga.buf = ep.buf;
 		ga.param_base = (uint32_t)n_mlp;
-		ga.write_grad32 = 1;
+		ga.write_grad32 = 0;  // the fp16 gradients (reference m_param_gradients) are written; the fp32 sums are not needed
 		g.backward_acc(st, ws.gbw, B, ws.dLdenc.p, 0, 0, g32.as<float>() + n_mlp, &ga);
 		mark(st, 2);
-		AdamArgs ag = adam_args();
+		AdamArgs ag = adam_args_table(st, adam_step);
 		ag.n = (uint32_t)n_mlp + g.n_lds_params;
 		ag.begin = (uint32_t)n_mlp;
 		ag.part = ws.gbw.partial.as<float>();
 		ag.n_parts = ws.gbw.n_chunks;
 		ag.part_stride = g.n_lds_params;
 		ag.part_map = g.slab_map();
-		ag.cached_factor = d_factor.as<float>();
-		ag.cached_step = adam_step;
 		if (!g.slices.empty())
 			launch_adam(st, ag, w32.as<float>(), w16.p, g32.as<float>(), g16.p, m1.as<float>(), m2.as<float>(), steps.as<uint32_t>());
 	} else {
@@ -893,9 +901,31 @@ AdamArgs TrainerHost::adam_args() const {
 	return a;
 }
 
+AdamArgs TrainerHost::adam_args_table(hipStream_t st, uint32_t upto, uint32_t reserve) {
+	AdamArgs a = adam_args();
+	if (ftable_b1 != adam.beta1 || ftable_b2 != adam.beta2) {  // hyper-parameters changed: recompute all
+		ftable_valid = 0;
+		ftable_b1 = adam.beta1;
+		ftable_b2 = adam.beta2;
+	}
+	if (std::max(upto, reserve) > ftable_cap) {
+		ftable_cap = std::max(std::max(upto, reserve), std::max(1024u, 2 * ftable_cap));
+		TCNN_HIP_CHECK(hipStreamSynchronize(st));  // the old table may still be read by queued work
+		d_ftable.reserve((size_t)ftable_cap * 4);
+		ftable_valid = 0;
+	}
+	if (upto > ftable_valid) {
+		launch_fill_bias_factors(st, a, d_ftable.as<float>(), ftable_valid, upto);
+		ftable_valid = upto;
+	}
+	a.factor_table = d_ftable.as<float>();
+	a.factor_n = ftable_valid;
+	return a;
+}
+
 void TrainerHost::optimizer_step(hipStream_t st) {  // AdamOptimizer::step, adam.h:150-188
 	++adam_step;
-	const AdamArgs a = adam_args();
+	const AdamArgs a = adam_args_table(st, adam_step);
 	launch_adam(st, a, w32.as<float>(), w16.p, g32.as<float>(), g16.p, m1.as<float>(), m2.as<float>(), steps.as<uint32_t>());
 	ws.wimage_valid = false;
 }

@@ -175,7 +175,7 @@ struct EncodingHost {
 struct StepWorkspace {
 	DevBuf dLdenc, wgrad_partial, loss_partial, grad32_tmp, out16, enc16, wimage;
 	GridBwdBufs gbw;
-	DevBuf acts, delta0, delta1, dout16;  // layer-wise engine
+	DevBuf acts, delta0, delta1, dout16, red_tmp;  // layer-wise engine
 	uint32_t n_fused_blocks = 0, n_loss_partials = 0;
 	bool wimage_valid = false;  // fused weight image matches the current fp16 params (trainer fast path)
 };
@@ -190,6 +190,7 @@ struct NetworkHost {
 	GridEncodingHost* grid = nullptr;  // enc->grid when the encoding is a grid
 	MlpHost mlp;
 	uint32_t n_input_dims = 0, n_output_dims = 0;
+	uint32_t loss_l2 = 0;  // training loss: 0 RelativeL2 (relative_l2.h), 1 L2 (l2.h)
 	NetworkHost(uint32_t n_in, uint32_t n_out, const json& enc, const json& net);
 	uint64_t n_params() const { return (uint64_t)mlp.n_params() + enc->n_params(); }
 	bool fused_ok() const;
@@ -250,7 +251,16 @@ struct TrainerHost {
 	AdamHost adam;
 	std::string loss_otype;
 	uint64_t n_params = 0, n_mlp = 0;
-	DevBuf w32, w16, g16, g32, m1, m2, steps, d_loss, d_factor;
+	DevBuf w32, w16, g16, g32, m1, m2, steps, d_loss;
+	// Adam bias-correction factors of steps 1 .. ftable_valid (AdamArgs::factor_table), for the betas
+	// they were computed with; grown by doubling
+	DevBuf d_ftable;
+	uint32_t ftable_cap = 0, ftable_valid = 0;
+	float ftable_b1 = 0.0f, ftable_b2 = 0.0f;
+	// makes the table cover steps 1 .. upto (launching the fill kernel for what is missing) and
+	// returns args with factor_table / factor_n set
+	// (capacity for at least `reserve` entries)
+	AdamArgs adam_args_table(hipStream_t st, uint32_t upto, uint32_t reserve = 0);
 	StepWorkspace ws;
 	uint32_t adam_step = 0;
 	float grad_scale = 1.0f;

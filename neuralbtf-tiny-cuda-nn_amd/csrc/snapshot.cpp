@@ -175,10 +175,49 @@ std::vector<uint8_t> d2h(const DevBuf& b, size_t bytes) {
 	return h;
 }
 
-const std::string& bin_of(const MsgValue& v, size_t bytes, const char* what) {
-	TCNN_CHECK(v.kind == MsgValue::Bin, std::string("snapshot: '") + what + "' must be a binary");
-	TCNN_CHECK(v.s.size() == bytes, std::string("snapshot: '") + what + "' has the wrong size");
-	return v.s;
+// from_json(json, GPUMemory<T>&) (gpu_memory_json.h:52-71): a binary, or its JSON image
+// {"bytes": [u8, ...], "subtype": ...} (nlohmann's binary-as-JSON form)
+std::string bin_of(const MsgValue& v, size_t bytes, const char* what) {
+	std::string out;
+	if (v.kind == MsgValue::Bin) {
+		out = v.s;
+	} else if (v.kind == MsgValue::Map && v.has("bytes") && v.at("bytes").kind == MsgValue::Arr) {
+		const auto& arr = v.at("bytes").a;
+		out.resize(arr.size());
+		for (size_t i = 0; i < arr.size(); ++i) out[i] = (char)(uint8_t)arr[i].number();
+	} else {
+		throw std::runtime_error(std::string("snapshot: '") + what + "': Invalid json type: must be either binary or object");
+	}
+	TCNN_CHECK(out.size() == bytes, std::string("snapshot: '") + what + "' has the wrong size");
+	return out;
+}
+
+// JSON text snapshot (json::dump of Trainer::serialize, binaries in their {"bytes": [...]} form)
+MsgValue from_json_text(const json& j) {
+	MsgValue v;
+	if (j.is_object()) {
+		v.kind = MsgValue::Map;
+		for (auto it = j.begin(); it != j.end(); ++it) v.m[it.key()] = from_json_text(it.value());
+	} else if (j.is_array()) {
+		v.kind = MsgValue::Arr;
+		for (const auto& e : j) v.a.push_back(from_json_text(e));
+	} else if (j.is_string()) {
+		v.kind = MsgValue::Str;
+		v.s = j.get<std::string>();
+	} else if (j.is_boolean()) {
+		v.kind = MsgValue::Bool;
+		v.u = j.get<bool>() ? 1 : 0;
+	} else if (j.is_number_unsigned()) {
+		v.kind = MsgValue::UInt;
+		v.u = j.get<uint64_t>();
+	} else if (j.is_number_integer()) {
+		v.kind = MsgValue::Int;
+		v.i = j.get<int64_t>();
+	} else if (j.is_number_float()) {
+		v.kind = MsgValue::Float;
+		v.f = j.get<double>();
+	}
+	return v;
 }
 
 }  // namespace
@@ -214,19 +253,26 @@ std::vector<uint8_t> TrainerHost::serialize(bool with_optimizer) {
 }
 
 void TrainerHost::deserialize(const void* data, size_t size) {
-	MsgReader r{(const uint8_t*)data, (const uint8_t*)data + size};
-	const MsgValue root = r.value();
+	// training steps may still be queued on the caller's (possibly non-blocking) stream
+	TCNN_HIP_CHECK(hipDeviceSynchronize());
+	MsgValue root;
+	if (size > 0 && ((const char*)data)[0] == '{') {  // JSON text
+		root = from_json_text(json::parse(std::string((const char*)data, size)));
+	} else {
+		MsgReader r{(const uint8_t*)data, (const uint8_t*)data + size};
+		root = r.value();
+	}
 	TCNN_CHECK(root.kind == MsgValue::Map, "snapshot: top level must be a map");
 	const size_t n = n_params;
 	const std::string type = root.has("params_type") ? root.at("params_type").s : "__half";
 	const MsgValue& pb = root.at("params_binary");
 	if (type == "float") {  // trainer.h:292-294: fp32 params -> full precision + fp16 copy
-		const std::string& b = bin_of(pb, n * 4, "params_binary");
+		const std::string b = bin_of(pb, n * 4, "params_binary");
 		std::vector<float> host(n);
 		std::memcpy(host.data(), b.data(), n * 4);
 		set_params_full_precision(host.data(), n);
 	} else if (type == "__half") {  // trainer.h:295-304: fp16 params; full precision = (float)half
-		const std::string& b = bin_of(pb, n * 2, "params_binary");
+		const std::string b = bin_of(pb, n * 2, "params_binary");
 		TCNN_HIP_CHECK(hipMemcpy(w16.p, b.data(), n * 2, hipMemcpyHostToDevice));
 		launch_cast_f16_f32(nullptr, w16.p, w32.as<float>(), n);
 		TCNN_HIP_CHECK(hipDeviceSynchronize());

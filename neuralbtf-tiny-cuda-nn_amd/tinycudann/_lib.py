@@ -14,6 +14,9 @@ _lib = None
 c_void_p, c_float, c_int, c_uint32, c_uint64, c_char_p = (
     ctypes.c_void_p, ctypes.c_float, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_char_p)
 
+# void (*)(int severity, const char* message, void* user) -- tcnn_set_log_callback
+LOG_CALLBACK = ctypes.CFUNCTYPE(None, c_int, c_char_p, c_void_p)
+
 _SIGS = {
     "tcnn_last_error": (c_char_p, []),
     "tcnn_version": (c_char_p, []),
@@ -24,6 +27,7 @@ _SIGS = {
     "tcnn_has_networks": (c_int, []),
     "tcnn_default_loss_scale": (c_float, [c_int]),
     "tcnn_preferred_precision": (c_int, []),
+    "tcnn_set_log_callback": (None, [LOG_CALLBACK, c_void_p]),
     "tcnn_create_network_with_input_encoding": (c_void_p, [c_uint32, c_uint32, c_char_p, c_char_p]),
     "tcnn_create_network": (c_void_p, [c_uint32, c_uint32, c_char_p]),
     "tcnn_create_encoding": (c_void_p, [c_uint32, c_char_p, c_int]),

@@ -1,6 +1,12 @@
 """torch.nn front-end mirroring reference bindings/torch/tinycudann/modules.py:91-329 on top of the
 C-ABI runtime module (include/tcnn_mi355x.h, which replaces reference src/cpp_api.cu +
-bindings/torch/tinycudann/bindings.cpp)."""
+bindings/torch/tinycudann/bindings.cpp).
+
+Provenance: the autograd plumbing below (null-tensor conventions, `_module_function`,
+`_module_function_backward`, `Module.forward`'s batch padding and the pickling hooks) follows the
+reference's modules.py:81-204 (tiny-cuda-nn, Copyright (c) 2020-2022 NVIDIA CORPORATION, BSD-3-Clause)
+closely on purpose: it is the plugin API whose exact behaviour -- loss-scale multiply/divide order,
+null-tensor conventions, output slicing -- callers such as NeuralBTF depend on."""
 import ctypes
 import gc
 import json
@@ -69,10 +75,16 @@ class _NativeModule:
 
     def __init__(self, handle):
         self.h = L.check_ptr(handle)
-        lib = L.lib()
-        self.n_input_dims = lib.tcnn_module_n_input_dims(self.h)
-        self.n_output_dims = lib.tcnn_module_n_output_dims(self.h)
-        self.n_params = lib.tcnn_module_n_params(self.h)
+
+    # bindings.cpp:306-313: sizes are methods on the native module, as in the reference
+    def n_input_dims(self):
+        return L.lib().tcnn_module_n_input_dims(self.h)
+
+    def n_output_dims(self):
+        return L.lib().tcnn_module_n_output_dims(self.h)
+
+    def n_params(self):
+        return L.lib().tcnn_module_n_params(self.h)
 
     def __del__(self):
         try:
@@ -93,16 +105,16 @@ class _NativeModule:
         return L.lib().tcnn_module_name(self.h).decode()
 
     def initial_params(self, seed):
-        p = torch.zeros(self.n_params, dtype=torch.float32, device="cuda")
+        p = torch.zeros(self.n_params(), dtype=torch.float32, device="cuda")
         torch.cuda.synchronize()
         L.check(L.lib().tcnn_module_initialize_params(self.h, seed, _ptr(p), 1.0))
         return p
 
     def fwd(self, input, params):
-        assert input.dtype == torch.float32 and input.is_contiguous() and input.shape[1] == self.n_input_dims
-        assert params.dtype == _torch_precision(self.param_precision()) and params.numel() == self.n_params
+        assert input.dtype == torch.float32 and input.is_contiguous() and input.shape[1] == self.n_input_dims()
+        assert params.dtype == _torch_precision(self.param_precision()) and params.numel() == self.n_params()
         B = input.shape[0]
-        out = torch.empty(B, self.n_output_dims, dtype=_torch_precision(self.output_precision()), device=input.device)
+        out = torch.empty(B, self.n_output_dims(), dtype=_torch_precision(self.output_precision()), device=input.device)
         if not (input.requires_grad or params.requires_grad):
             L.check(L.lib().tcnn_module_inference(self.h, _stream(), B, _ptr(input), _ptr(out), _ptr(params)))
             return None, out
@@ -113,7 +125,7 @@ class _NativeModule:
     def bwd(self, ctx, input, params, output, dL_doutput):
         B = input.shape[0]
         dL_dinput = torch.empty_like(input) if input.requires_grad else None
-        dL_dparams = torch.empty(self.n_params, dtype=_torch_precision(self.param_precision()), device=input.device) if params.requires_grad else None
+        dL_dparams = torch.empty(self.n_params(), dtype=_torch_precision(self.param_precision()), device=input.device) if params.requires_grad else None
         dL_doutput = dL_doutput.to(_torch_precision(self.output_precision())).contiguous()
         L.check(L.lib().tcnn_module_backward(self.h, _stream(), ctx.h, B, _ptr(dL_dinput), _ptr(dL_doutput),
                                              _ptr(dL_dparams), _ptr(input), _ptr(output), _ptr(params)))
@@ -123,11 +135,11 @@ class _NativeModule:
         """bindings.cpp:185-239: second-order gradients from dL/d(dL/dinput)."""
         B = input.shape[0]
         dev = input.device
-        dL_ddLdoutput = (torch.zeros(B, self.n_output_dims, dtype=_torch_precision(self.output_precision()), device=dev)
+        dL_ddLdoutput = (torch.zeros(B, self.n_output_dims(), dtype=_torch_precision(self.output_precision()), device=dev)
                          if dL_doutput.requires_grad else None)
-        dL_dparams = (torch.zeros(self.n_params, dtype=_torch_precision(self.param_precision()), device=dev)
+        dL_dparams = (torch.zeros(self.n_params(), dtype=_torch_precision(self.param_precision()), device=dev)
                       if params.requires_grad else None)
-        dL_dinput = torch.zeros(B, self.n_input_dims, dtype=torch.float32, device=dev) if input.requires_grad else None
+        dL_dinput = torch.zeros(B, self.n_input_dims(), dtype=torch.float32, device=dev) if input.requires_grad else None
         if dL_doutput.requires_grad or params.requires_grad:
             dL_ddLdinput = dL_ddLdinput.to(torch.float32).contiguous()
             dout = dL_doutput.detach().to(_torch_precision(self.output_precision())).contiguous()
@@ -239,6 +251,17 @@ class Module(torch.nn.Module):
         )
         return output[:batch_size, :self.n_output_dims]
 
+    def __getstate__(self):
+        """modules.py:194-199: pickle everything except the native module (a C-ABI handle)."""
+        state = self.__dict__.copy()
+        del state["native_tcnn_module"]
+        return state
+
+    def __setstate__(self, state):
+        """modules.py:201-204: rebuild the native module from the stored configuration."""
+        self.__dict__.update(state)
+        self.native_tcnn_module = self._native_tcnn_module()
+
     def extra_repr(self):
         return (f"n_input_dims={self.n_input_dims}, n_output_dims={self.n_output_dims}, seed={self.seed}, "
                 f"dtype={self.dtype}, hyperparams={self.native_tcnn_module.hyperparams()}")
@@ -246,6 +269,8 @@ class Module(torch.nn.Module):
 
 class NetworkWithInputEncoding(Module):
     def __init__(self, n_input_dims, n_output_dims, encoding_config, network_config, seed=1337):
+        if not _C.has_networks():
+            raise RuntimeError("Cannot create `NetworkWithInputEncoding` because tiny-cuda-nn was not compiled with neural network support.")
         self.n_input_dims = n_input_dims
         self.n_output_dims = n_output_dims
         self.encoding_config = encoding_config
@@ -260,6 +285,8 @@ class NetworkWithInputEncoding(Module):
 
 class Network(Module):
     def __init__(self, n_input_dims, n_output_dims, network_config, seed=1337):
+        if not _C.has_networks():
+            raise RuntimeError("Cannot create `Network` because tiny-cuda-nn was not compiled with neural network support.")
         self.n_input_dims = n_input_dims
         self.n_output_dims = n_output_dims
         self.network_config = network_config
@@ -274,14 +301,16 @@ class Encoding(Module):
     def __init__(self, n_input_dims, encoding_config, seed=1337, dtype=None):
         self.n_input_dims = n_input_dims
         self.encoding_config = encoding_config
-        if dtype is None or dtype == torch.float16:
+        if dtype is None:
+            self.precision = _C.preferred_precision()
+        elif dtype == torch.float16:
             self.precision = PRECISION_FP16
         elif dtype == torch.float32:
             self.precision = PRECISION_FP32
         else:
             raise ValueError(f"Encoding only supports fp32 or fp16 precision, but got {dtype}")
         super().__init__(seed=seed)
-        self.n_output_dims = self.native_tcnn_module.n_output_dims
+        self.n_output_dims = self.native_tcnn_module.n_output_dims()
 
     def _native_tcnn_module(self):
         return _NativeModule(L.lib().tcnn_create_encoding(self.n_input_dims, json.dumps(self.encoding_config).encode(),

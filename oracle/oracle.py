@@ -51,7 +51,7 @@ class Model(ctypes.Structure):
         ("m1", ctypes.POINTER(ctypes.c_float)), ("m2", ctypes.POINTER(ctypes.c_float)),
         ("steps", ctypes.POINTER(ctypes.c_uint32)),
         ("enc_type", ctypes.c_uint32), ("n_dims", ctypes.c_uint32), ("n_bins", ctypes.c_uint32), ("IN", ctypes.c_uint32),
-        ("enc_scale", ctypes.c_float), ("enc_offset", ctypes.c_float),
+        ("enc_scale", ctypes.c_float), ("enc_offset", ctypes.c_float), ("loss_type", ctypes.c_uint32),
     ]
 
 
@@ -94,6 +94,8 @@ def lib():
         _lib.orc_relative_l2.restype = ctypes.c_double
         _lib.orc_relative_l2.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_float,
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        _lib.orc_l2.restype = ctypes.c_double
+        _lib.orc_l2.argtypes = _lib.orc_relative_l2.argtypes
         _lib.orc_adam_step.argtypes = [ctypes.POINTER(AdamCfg), ctypes.c_uint32, ctypes.c_uint32, ctypes.c_float, ctypes.c_uint32] + [ctypes.c_void_p] * 6
         _lib.orc_model_init.argtypes = [ctypes.POINTER(Model), ctypes.c_uint32]
         _lib.orc_model_free.argtypes = [ctypes.POINTER(Model)]
@@ -392,6 +394,8 @@ class OracleModel:
         act = net.get("activation", "ReLU").lower()
         self.m.activation = {"none": 0, "relu": 1}[act]
         self.m.adam = adam_cfg(opt)
+        lo = config.get("loss", {}).get("otype", "RelativeL2").lower()
+        self.m.loss_type = {"relativel2": 0, "l2": 1}[lo]
         assert lib().orc_model_init(ctypes.byref(self.m), seed) == 0
         self.n_params = self.m.n_params
         self.n_mlp_params = self.m.n_mlp_params
@@ -431,3 +435,16 @@ class OracleModel:
         out = np.empty((pos.shape[0], self.m.OUTP), dtype=np.uint16)
         lib().orc_model_inference(ctypes.byref(self.m), pos.shape[0], _p(pos), _p(out), n_threads)
         return out
+
+
+def l2(pred16, target, loss_scale=128.0, want_values=False):
+    """L2 loss (losses/l2.h:40-76); same layouts as relative_l2"""
+    pred16 = np.ascontiguousarray(pred16, dtype=np.uint16)
+    target = np.ascontiguousarray(target, dtype=np.float32)
+    B, stride = pred16.shape
+    dims = target.shape[1]
+    grads = np.empty_like(pred16)
+    values = np.empty((B, stride), dtype=np.float32) if want_values else None
+    s = lib().orc_l2(B, stride, dims, loss_scale, _p(pred16), _p(target),
+                     _p(values) if values is not None else None, _p(grads))
+    return s, grads, values

@@ -891,6 +891,30 @@ double orc_relative_l2(uint32_t B, uint32_t stride, uint32_t dims, float loss_sc
 	return sum;
 }
 
+/* L2 -- losses/l2.h:40-76 (data_pdf = 1) */
+double orc_l2(uint32_t B, uint32_t stride, uint32_t dims, float loss_scale,
+              const uint16_t* pred, const float* target, float* values, uint16_t* grads) {
+	const uint32_t n_elements = B * stride;
+	const uint32_t n_total = n_elements / stride * dims;
+	double sum = 0.0;
+	for (uint32_t i = 0; i < n_elements; ++i) {
+		uint32_t intra = i % stride, inter = i / stride;
+		if (intra >= dims) {
+			if (values) values[i] = 0.0f;
+			grads[i] = 0;
+			continue;
+		}
+		uint32_t ti = inter * dims + intra;
+		float d = orc_h2f(pred[i]) - target[ti];
+		float val = d * d / 1.0f / (float)n_total;
+		float gr = 2.0f * d / 1.0f;
+		if (values) values[i] = val;
+		sum += val;
+		grads[i] = orc_f2h(loss_scale * gr / (float)n_total);
+	}
+	return sum;
+}
+
 /* ------------------------------------------------------------------------------------------ */
 /* Adam -- optimizers/adam.h:47-188                                                            */
 /* ------------------------------------------------------------------------------------------ */
@@ -1009,7 +1033,8 @@ double orc_train_step(orc_model* m, uint32_t B, const float* pos, const float* t
 	uint16_t* denc = (uint16_t*)malloc((size_t)IN * B * 2);
 	const int soa = model_encode(m, B, pos, enc);
 	orc_mlp_fwd(m->W, IN, m->NH, m->OUTP, m->activation, m->w16, B, enc, soa, out, hidden, n_threads);
-	double loss = orc_relative_l2(B, m->OUTP, m->n_output_dims, loss_scale, out, target, NULL, dout);
+	double loss = m->loss_type == 1 ? orc_l2(B, m->OUTP, m->n_output_dims, loss_scale, out, target, NULL, dout)
+	                                : orc_relative_l2(B, m->OUTP, m->n_output_dims, loss_scale, out, target, NULL, dout);
 	orc_mlp_bwd(m->W, IN, m->NH, m->OUTP, m->activation, m->w16, B, enc, soa, hidden, dout, m->grad32,
 	            m->enc_type == 0 ? denc : NULL, n_threads);
 	if (m->enc_type == 0) {

@@ -124,6 +124,9 @@ void orc_identity_fwd(uint32_t B, uint32_t D, float scale, float offset, const f
  * grads fp16 CM [stride][B]. Returns sum of values (in double). */
 double orc_relative_l2(uint32_t B, uint32_t stride, uint32_t dims, float loss_scale,
                        const uint16_t* pred, const float* target, float* values, uint16_t* grads);
+/* ---- L2 loss (losses/l2.h:40-76), same layouts ---- */
+double orc_l2(uint32_t B, uint32_t stride, uint32_t dims, float loss_scale,
+              const uint16_t* pred, const float* target, float* values, uint16_t* grads);
 
 /* ---- Adam (optimizers/adam.h:47-188) ---- */
 typedef struct {
@@ -151,6 +154,7 @@ typedef struct {
 	 * caller for OneBlob / Identity: n_dims * n_bins or n_dims, rounded up to 16) */
 	uint32_t enc_type, n_dims, n_bins, IN;
 	float enc_scale, enc_offset;
+	uint32_t loss_type; /* 0 = RelativeL2, 1 = L2 */
 } orc_model;
 int orc_model_init(orc_model* m, uint32_t seed); /* allocate + Trainer::initialize_params */
 void orc_model_free(orc_model* m);
