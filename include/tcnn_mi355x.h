@@ -52,6 +52,12 @@ int tcnn_preferred_precision(void);               /* cpp::preferred_precision() 
 typedef void (*tcnn_log_callback_t)(int severity, const char* message, void* user);
 void tcnn_set_log_callback(tcnn_log_callback_t callback, void* user);
 
+/* generate_random_uniform<float>(stream, rng, n, out, lower, upper) (random.h:57-70): n floats in the
+ * reference's strided order (4 per thread, thread i jumps 4i) from the pcg32 stream {*rng_state,
+ * *rng_inc} (dependencies/pcg32/pcg32.h); the state is advanced by n on return, as rng.advance(n). */
+int tcnn_generate_random_uniform(void* stream, uint64_t* rng_state, uint64_t* rng_inc, uint64_t n, float* out, float lower,
+                                 float upper);
+
 /* ---- runtime module FFI (cpp_api.h:86-117) ---- */
 /* cpp::create_network_with_input_encoding(n_input_dims, n_output_dims, encoding, network) */
 tcnn_module* tcnn_create_network_with_input_encoding(uint32_t n_input_dims, uint32_t n_output_dims,
@@ -139,6 +145,14 @@ int tcnn_trainer_serialize(tcnn_trainer* t, int with_optimizer, void* buf, uint6
  * gpu_memory_json.h:52-71); params_type "__half" or "float", optional optimizer state. */
 int tcnn_trainer_deserialize(tcnn_trainer* t, const void* buf, uint64_t size);
 uint32_t tcnn_trainer_optimizer_step_count(const tcnn_trainer* t);
+/* Trainer::update_hyperparams(json) (trainer.h:213-216): {"optimizer": {...}} fields update Adam
+ * (adam.h:235-283: learning_rate, betas, epsilon, l2_reg, ...). */
+int tcnn_trainer_update_hyperparams(tcnn_trainer* t, const char* params_json);
+/* {"optimizer": Adam hyperparams, "loss": {"otype"}} as JSON; valid until the next call on this thread. */
+const char* tcnn_trainer_hyperparams(tcnn_trainer* t);
+/* Trainer::initialize_params (trainer.h:68-87): re-seed pcg32{seed_seq{seed}[0]}, re-initialise every
+ * parameter, zero the optimizer state and its step counter. */
+int tcnn_trainer_initialize_params(tcnn_trainer* t, uint32_t seed);
 /* Engine diagnostics: name of the path the trainer runs ("fused" / "layered" / "unsupported"). */
 const char* tcnn_trainer_engine(const tcnn_trainer* t);
 /* set_max_level on the trainer model's grid encoding (see tcnn_module_set_max_level) */

@@ -15,20 +15,7 @@
 #include <stdexcept>
 #include <string>
 
-#include <json.hpp>  // nlohmann::json (the reference includes it as <json/json.hpp>)
-
-#include "../tcnn_mi355x.h"
-
-namespace tcnn {
-struct Context {  // cpp_api.h:40-47
-	Context() = default;
-	virtual ~Context() {}
-	Context(const Context&) = delete;
-	Context& operator=(const Context&) = delete;
-	Context(Context&&) = delete;
-	Context& operator=(Context&&) = delete;
-};
-}  // namespace tcnn
+#include "common.h"  // tcnn::Context, json, the C-ABI
 
 namespace tcnn { namespace cpp {
 

@@ -1,0 +1,172 @@
+// tiny-cuda-nn/trainer.h -- Trainer<T, PARAMS_T, COMPUTE_T> (reference
+// include/tiny-cuda-nn/trainer.h:47-361) for the MI355X engine.
+//
+// The engine runs forward, loss, backward and (optionally) the optimizer of one training step as
+// three launches on the caller's stream (neuralbtf-tiny-cuda-nn_amd/csrc/runtime.cpp,
+// TrainerHost::training_step_overlapped), so training_step() is one C-ABI call. The ForwardContext it
+// returns identifies the step; loss(ctx) reads that step's loss sum (trainer.h:205-211 reduces the
+// context's loss values). The separate forward()/backward() of the reference, data_pdf, external
+// dL/dy, dL/dinput and Accumulate gradients are not part of this engine's training step and throw.
+#pragma once
+
+#include <memory>
+#include <vector>
+
+#include "network_with_input_encoding.h"
+#include "optimizer.h"
+
+namespace tcnn {
+
+template <typename T, typename PARAMS_T, typename COMPUTE_T = T>
+class Trainer {
+public:
+	using Model = NetworkWithInputEncoding<PARAMS_T>;
+
+	// trainer.h:50-57: the trainer owns the parameters (seeded pcg32{seed_seq{seed}[0]})
+	Trainer(std::shared_ptr<Model> model, std::shared_ptr<Optimizer<PARAMS_T>> optimizer, std::shared_ptr<Loss<COMPUTE_T>> loss,
+	        uint32_t seed = 1337, float perturbation_sigma = 0)
+	    : m_model{std::move(model)}, m_optimizer{std::move(optimizer)}, m_loss{std::move(loss)}, m_seed{seed} {
+		static_assert(std::is_same<T, float>::value, "Trainer: inputs are fp32 (Trainer<float, __half, __half>)");
+		if (perturbation_sigma != 0) throw std::runtime_error{"Trainer: output perturbation is not supported by the MI355X engine"};
+		// (keyed assignment: brace-initialising with json values would wrap them in arrays)
+		json cfg = json::object();
+		cfg["loss"] = m_loss->config();
+		cfg["optimizer"] = m_optimizer->config();
+		cfg["encoding"] = m_model->encoding_config();
+		cfg["network"] = m_model->network_config();
+		m_h = detail::check_handle(tcnn_trainer_create(m_model->input_width(), m_model->output_width(), cfg.dump().c_str(), seed));
+		m_model->attach(m_h);
+		m_optimizer->attach(m_h);
+	}
+	virtual ~Trainer() {
+		if (m_model->trainer_handle() == m_h) m_model->attach(nullptr);
+		m_optimizer->attach(nullptr);
+		tcnn_trainer_destroy(m_h);
+	}
+	Trainer(const Trainer&) = delete;
+	Trainer& operator=(const Trainer&) = delete;
+
+	// trainer.h:89-95
+	struct ForwardContext : public Context {
+		const Trainer* owner = nullptr;
+		uint64_t step = 0;
+	};
+
+	// trainer.h:68-87
+	void initialize_params() {
+		detail::check_rc(tcnn_trainer_initialize_params(m_h, m_seed));
+		++m_n_steps;  // contexts of earlier steps no longer describe the parameters
+	}
+
+	// trainer.h:163-203
+	std::unique_ptr<ForwardContext> training_step(hipStream_t stream, const GPUMatrixDynamic<T>& input, const GPUMatrixDynamic<float>& target,
+	                                              const GPUMatrixDynamic<float>* data_pdf = nullptr, bool run_optimizer = true,
+	                                              GPUMatrixDynamic<T>* dL_dinput = nullptr, bool use_inference_params = false,
+	                                              GradientMode param_gradients_mode = GradientMode::Overwrite,
+	                                              const GPUMatrixDynamic<COMPUTE_T>* external_dL_dy = nullptr) {
+		(void)use_inference_params;
+		CHECK_THROW(input.m() == m_model->input_width());
+		CHECK_THROW(target.m() == m_model->output_width());
+		CHECK_THROW(input.n() == target.n());
+		CHECK_THROW(input.n() % BATCH_SIZE_GRANULARITY == 0);
+		CHECK_THROW(input.layout() == CM && input.is_contiguous() && target.layout() == CM && target.is_contiguous());
+		if (data_pdf || dL_dinput || external_dL_dy || param_gradients_mode != GradientMode::Overwrite)
+			throw std::runtime_error{"Trainer::training_step: data_pdf / dL_dinput / external dL/dy / non-Overwrite gradients are not supported"};
+		detail::check_rc(tcnn_trainer_training_step(m_h, stream, input.n(), input.data(), target.data(), run_optimizer ? 1 : 0));
+		auto ctx = std::make_unique<ForwardContext>();
+		ctx->owner = this;
+		ctx->step = ++m_n_steps;
+		return ctx;
+	}
+	std::unique_ptr<ForwardContext> training_step(const GPUMatrixDynamic<T>& input, const GPUMatrixDynamic<float>& target,
+	                                              const GPUMatrixDynamic<float>* data_pdf = nullptr, bool run_optimizer = true,
+	                                              GPUMatrixDynamic<T>* dL_dinput = nullptr, bool use_inference_params = false,
+	                                              GradientMode param_gradients_mode = GradientMode::Overwrite,
+	                                              const GPUMatrixDynamic<COMPUTE_T>* external_dL_dy = nullptr) {
+		return training_step(nullptr, input, target, data_pdf, run_optimizer, dL_dinput, use_inference_params, param_gradients_mode,
+		                     external_dL_dy);
+	}
+
+	// trainer.h:205-211: synchronises `stream`
+	float loss(hipStream_t stream, const ForwardContext& ctx) const {
+		if (ctx.owner != this || ctx.step != m_n_steps)
+			throw std::runtime_error{"Trainer::loss: only the loss of this trainer's most recent training step is retained"};
+		const float v = tcnn_trainer_loss(m_h, stream);
+		if (v < 0.0f) throw std::runtime_error{tcnn_last_error()};
+		return v;
+	}
+	float loss(const ForwardContext& ctx) const { return loss(nullptr, ctx); }
+
+	// trainer.h:155-161 (the loss scale is the engine's default_loss_scale<PARAMS_T>())
+	void optimizer_step(hipStream_t stream, float loss_scale) {
+		(void)loss_scale;
+		detail::check_rc(tcnn_trainer_optimizer_step(m_h, stream));
+	}
+	void optimizer_step(float loss_scale) { optimizer_step(nullptr, loss_scale); }
+
+	// trainer.h:213-224
+	void update_hyperparams(const json& params) {
+		if (params.count("optimizer")) m_optimizer->update_hyperparams(params["optimizer"]);
+		if (params.count("loss")) m_loss->update_hyperparams(params["loss"]);
+	}
+	json hyperparams() const { return json::parse(tcnn_trainer_hyperparams(m_h)); }
+
+	// parameter buffers (trainer.h:226-240, 322-336): device pointers owned by the trainer
+	float* params_full_precision() const { return tcnn_trainer_params_fp32(m_h); }
+	PARAMS_T* params() const { return (PARAMS_T*)tcnn_trainer_params(m_h); }
+	PARAMS_T* params_inference() const { return params(); }
+	PARAMS_T* param_gradients() const { return (PARAMS_T*)tcnn_trainer_param_gradients(m_h); }
+	size_t n_params() const { return (size_t)tcnn_trainer_n_params(m_h); }
+
+	// trainer.h:242-273
+	void set_params_full_precision(const float* params, size_t n_params, bool device_ptr = false) {
+		if (n_params != this->n_params()) throw std::runtime_error{"Can't set fp params because buffer has the wrong size."};
+		std::vector<float> host;
+		if (device_ptr) {
+			host.resize(n_params);
+			HIP_CHECK_THROW(hipMemcpy(host.data(), params, n_params * sizeof(float), hipMemcpyDeviceToHost));
+			params = host.data();
+		}
+		detail::check_rc(tcnn_trainer_set_params_full_precision(m_h, params, n_params));
+	}
+	void set_params(const PARAMS_T* params, size_t n_params, bool device_ptr = false) {
+		if (n_params != this->n_params()) throw std::runtime_error{"Can't set params because buffer has the wrong size."};
+		std::vector<PARAMS_T> h(n_params);
+		if (device_ptr) HIP_CHECK_THROW(hipMemcpy(h.data(), params, n_params * sizeof(PARAMS_T), hipMemcpyDeviceToHost));
+		else std::copy(params, params + n_params, h.begin());
+		std::vector<float> f(n_params);
+		for (size_t i = 0; i < n_params; ++i) f[i] = (float)h[i];
+		detail::check_rc(tcnn_trainer_set_params_full_precision(m_h, f.data(), n_params));
+	}
+
+	// trainer.h:275-315: json::to_msgpack(serialize(optimizer)) bytes and back (nlohmann 3.1.1, the
+	// json library of this toolchain, has no binary values, so the msgpack image is the interface)
+	std::vector<uint8_t> serialize_msgpack(bool serialize_optimizer = false) {
+		uint64_t n = 0;
+		detail::check_rc(tcnn_trainer_serialize(m_h, serialize_optimizer ? 1 : 0, nullptr, 0, &n));
+		std::vector<uint8_t> out(n);
+		detail::check_rc(tcnn_trainer_serialize(m_h, serialize_optimizer ? 1 : 0, out.data(), n, &n));
+		out.resize(n);
+		return out;
+	}
+	void deserialize_msgpack(const std::vector<uint8_t>& data) {
+		detail::check_rc(tcnn_trainer_deserialize(m_h, data.data(), data.size()));
+	}
+
+	std::shared_ptr<Model> model() const { return m_model; }
+	std::shared_ptr<Optimizer<PARAMS_T>> optimizer() const { return m_optimizer; }
+	std::shared_ptr<Loss<COMPUTE_T>> loss_object() const { return m_loss; }
+	// which of the engine's paths trains this model ("fused" / "layered")
+	std::string engine() const { return tcnn_trainer_engine(m_h); }
+	tcnn_trainer* handle() const { return m_h; }
+
+private:
+	std::shared_ptr<Model> m_model;
+	std::shared_ptr<Optimizer<PARAMS_T>> m_optimizer;
+	std::shared_ptr<Loss<COMPUTE_T>> m_loss;
+	uint32_t m_seed;
+	tcnn_trainer* m_h = nullptr;
+	uint64_t m_n_steps = 0;
+};
+
+}  // namespace tcnn

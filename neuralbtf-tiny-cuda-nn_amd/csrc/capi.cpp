@@ -214,6 +214,18 @@ int tcnn_set_cuda_device(int device) {
 void tcnn_free_temporary_memory(void) {}
 int tcnn_has_networks(void) { return 1; }
 
+int tcnn_generate_random_uniform(void* stream, uint64_t* rng_state, uint64_t* rng_inc, uint64_t n, float* out, float lower, float upper) {
+	return guard([&] {
+		TCNN_CHECK(rng_state && rng_inc, "generate_random_uniform: rng state missing");
+		launch_generate_uniform((hipStream_t)stream, n, *rng_state, *rng_inc, out, lower, upper);
+		Pcg32 r;
+		r.state = *rng_state;
+		r.inc = *rng_inc;
+		r.advance((int64_t)n);  // rng.advance(n_elements), random.h:64
+		*rng_state = r.state;
+	});
+}
+
 void tcnn_set_log_callback(tcnn_log_callback_t cb, void* user) {
 	std::lock_guard<std::mutex> lk(g_log_mutex);
 	g_log_cb = cb;
@@ -383,6 +395,27 @@ int tcnn_trainer_set_params_full_precision(tcnn_trainer* t, const float* host, u
 	return guard([&] { t->t->set_params_full_precision(host, n); });
 }
 uint32_t tcnn_trainer_optimizer_step_count(const tcnn_trainer* t) { return t->t->adam_step; }
+int tcnn_trainer_update_hyperparams(tcnn_trainer* t, const char* params_json) {
+	return guard([&] {
+		const json p = json::parse(params_json);
+		if (p.count("optimizer")) t->t->adam.update(p["optimizer"]);  // Trainer::update_hyperparams, trainer.h:213-216
+	});
+}
+const char* tcnn_trainer_hyperparams(tcnn_trainer* t) {
+	g_str.clear();
+	if (guard([&] {
+		    json h = json::object();
+		    h["optimizer"] = t->t->adam.hyperparams();
+		    h["loss"] = json::object();
+		    h["loss"]["otype"] = t->t->loss_otype;
+		    g_str = h.dump();
+	    }) != 0)
+		return nullptr;
+	return g_str.c_str();
+}
+int tcnn_trainer_initialize_params(tcnn_trainer* t, uint32_t seed) {
+	return guard([&] { t->t->initialize_params(seed); });
+}
 const char* tcnn_trainer_engine(const tcnn_trainer* t) { return t->t->model->engine(); }
 int tcnn_trainer_set_max_level(tcnn_trainer* t, float max_level) {
 	return guard([&] {

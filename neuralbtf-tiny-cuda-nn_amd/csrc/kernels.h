@@ -207,6 +207,8 @@ size_t reduce_partials_tmp_floats(uint32_t n_parts, uint32_t n);
 void launch_reduce_partials(hipStream_t st, const float* in, uint32_t n_parts, uint32_t stride, uint32_t n,
                             float* out, float* tmp);
 
+// generate_random_uniform<float> (random.h:57-70) from pcg32 {state, inc} (not advanced here)
+void launch_generate_uniform(hipStream_t st, uint64_t n, uint64_t state, uint64_t inc, float* out, float lo, float hi);
 // factor_table[t - 1] = adam_bias_factor(a, t) for t in (lo, hi]
 void launch_fill_bias_factors(hipStream_t st, const AdamArgs& a, float* table, uint32_t lo, uint32_t hi);
 void launch_adam(hipStream_t st, const AdamArgs& a, float* w32, void* w16, const float* grad32, void* grad16,

@@ -98,6 +98,51 @@ void launch_reduce_partials(hipStream_t st, const float* in, uint32_t n_parts, u
 	TCNN_HIP_CHECK(hipGetLastError());
 }
 
+// pcg32 (dependencies/pcg32/pcg32.h:53-69, 139-158): jump `delta` steps ahead, then next_float
+__device__ __forceinline__ void pcg32_advance(uint64_t& state, uint64_t inc, uint64_t delta) {
+	constexpr uint64_t MULT = 0x5851f42d4c957f2dULL;
+	uint64_t cur_mult = MULT, cur_plus = inc, acc_mult = 1u, acc_plus = 0u;
+	for (; delta > 0; delta >>= 1) {
+		if (delta & 1u) {
+			acc_mult *= cur_mult;
+			acc_plus = acc_plus * cur_mult + cur_plus;
+		}
+		cur_plus = (cur_mult + 1u) * cur_plus;
+		cur_mult *= cur_mult;
+	}
+	state = acc_mult * state + acc_plus;
+}
+
+__device__ __forceinline__ float pcg32_next_float(uint64_t& state, uint64_t inc) {
+	const uint64_t old = state;
+	state = old * 0x5851f42d4c957f2dULL + inc;
+	const uint32_t xorshifted = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+	const uint32_t rot = (uint32_t)(old >> 59u);
+	const uint32_t u = ((xorshifted >> rot) | (xorshifted << ((~rot + 1u) & 31))) >> 9 | 0x3f800000u;
+	return __builtin_bit_cast(float, u) - 1.0f;
+}
+
+// generate_random_kernel<float, pcg32, 4> (random.h:39-55): thread i jumps 4 i steps and writes
+// out[i + n_threads j], j < 4; value = fma(u, upper - lower, lower) (the transform of random.h:69)
+__global__ __launch_bounds__(128) void k_generate_uniform(uint64_t n, uint64_t state, uint64_t inc, float* __restrict__ out, float lo, float range) {
+	const uint64_t i = threadIdx.x + (uint64_t)blockIdx.x * blockDim.x;
+	const uint64_t n_threads = (uint64_t)blockDim.x * gridDim.x;
+	pcg32_advance(state, inc, i * 4);
+#pragma unroll
+	for (uint32_t j = 0; j < 4; ++j) {
+		const uint64_t idx = i + n_threads * j;
+		if (idx >= n) return;
+		out[idx] = __builtin_fmaf(pcg32_next_float(state, inc), range, lo);
+	}
+}
+
+void launch_generate_uniform(hipStream_t st, uint64_t n, uint64_t state, uint64_t inc, float* out, float lo, float hi) {
+	if (n == 0) return;
+	const uint64_t n_thr = (n + 3) / 4;
+	hipLaunchKernelGGL(k_generate_uniform, dim3((uint32_t)((n_thr + 127) / 128)), dim3(128), 0, st, n, state, inc, out, lo, hi - lo);
+	TCNN_HIP_CHECK(hipGetLastError());
+}
+
 __global__ __launch_bounds__(256) void k_fill_bias_factors(const AdamArgs a, float* __restrict__ table, uint32_t lo, uint32_t hi) {
 	const uint32_t t = lo + 1 + blockIdx.x * blockDim.x + threadIdx.x;
 	if (t <= hi) table[t - 1] = adam_bias_factor(a, t);

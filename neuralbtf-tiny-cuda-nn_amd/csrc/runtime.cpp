@@ -716,6 +716,7 @@ TrainerHost::TrainerHost(uint32_t n_in, uint32_t n_out, const json& cfg, uint32_
 
 void TrainerHost::initialize_params(uint32_t seed) {
 	log_debug("Trainer: initializing " + std::to_string(n_params) + " params and resetting training.");  // trainer.h:70
+	TCNN_HIP_CHECK(hipDeviceSynchronize());  // queued steps on the caller's stream must not race the reset
 	// trainer.h:52-55: pcg32{seed_seq{seed}.generate()[0]}
 	std::seed_seq seq{seed};
 	std::vector<uint32_t> seeds(2);

@@ -28,6 +28,7 @@ _SIGS = {
     "tcnn_default_loss_scale": (c_float, [c_int]),
     "tcnn_preferred_precision": (c_int, []),
     "tcnn_set_log_callback": (None, [LOG_CALLBACK, c_void_p]),
+    "tcnn_generate_random_uniform": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_float, c_float]),
     "tcnn_create_network_with_input_encoding": (c_void_p, [c_uint32, c_uint32, c_char_p, c_char_p]),
     "tcnn_create_network": (c_void_p, [c_uint32, c_uint32, c_char_p]),
     "tcnn_create_encoding": (c_void_p, [c_uint32, c_char_p, c_int]),
@@ -65,6 +66,9 @@ _SIGS = {
     "tcnn_trainer_set_gradient_scale": (c_int, [c_void_p, c_float]),
     "tcnn_trainer_set_params_full_precision": (c_int, [c_void_p, c_void_p, c_uint64]),
     "tcnn_trainer_optimizer_step_count": (c_uint32, [c_void_p]),
+    "tcnn_trainer_update_hyperparams": (c_int, [c_void_p, c_char_p]),
+    "tcnn_trainer_hyperparams": (c_char_p, [c_void_p]),
+    "tcnn_trainer_initialize_params": (c_int, [c_void_p, c_uint32]),
     "tcnn_trainer_engine": (c_char_p, [c_void_p]),
     "tcnn_trainer_profile_begin": (c_int, [c_void_p]),
     "tcnn_trainer_profile_begin_sampled": (c_int, [c_void_p, c_uint32]),

@@ -1,0 +1,195 @@
+// A caller of the reference's C++ template API (reference include/tiny-cuda-nn/config.h:46-63,
+// trainer.h:163-211, object.h:147-179, gpu_matrix.h, gpu_memory.h, random.h, common_device.h:331),
+// built against include/tiny-cuda-nn/*.h + libtcnn_mi355x.so and run by
+// tests/test_gpu_template_api.py. Every check prints "FAIL ..." and exits nonzero on mismatch.
+#include <tiny-cuda-nn/common_device.h>
+
+#include <tiny-cuda-nn/config.h>
+
+#include <cmath>
+#include <cstdio>
+#include <fstream>
+#include <iostream>
+#include <vector>
+
+using namespace tcnn;
+
+static int g_fail = 0;
+#define EXPECT(c)                                                           \
+	do {                                                                    \
+		if (!(c)) {                                                         \
+			std::printf("FAIL %s:%d %s\n", __FILE__, __LINE__, #c);        \
+			++g_fail;                                                       \
+		}                                                                   \
+	} while (0)
+
+__global__ void field(uint32_t n, const float* __restrict__ xy, float* __restrict__ rgb) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	const float x = xy[2 * i], y = xy[2 * i + 1];
+	rgb[3 * i + 0] = 0.5f + 0.5f * sinf(9.0f * x) * cosf(7.0f * y);
+	rgb[3 * i + 1] = 0.5f + 0.4f * sinf(23.0f * x * y + 1.0f);
+	rgb[3 * i + 2] = 0.5f + 0.3f * cosf(31.0f * x) * sinf(17.0f * y);
+}
+
+int main(int argc, char** argv) {
+	if (argc < 2) {
+		std::printf("usage: %s <config_hash.json>\n", argv[0]);
+		return 2;
+	}
+	try {
+		std::ifstream f{argv[1]};
+		const json config = json::parse(std::string{std::istreambuf_iterator<char>{f}, std::istreambuf_iterator<char>{}});
+
+		// default_rng_t == pcg32: known answers of the reference's own pcg32.h compiled in the build
+		// container (tests/golden/ref_known_answers.json: pcg32_1337_next_uint / _next_float,
+		// pcg32_1337_advance_1000003_next_uint)
+		{
+			default_rng_t r{1337};
+			EXPECT(r.next_uint() == 634364130u);
+			EXPECT(r.next_float() == 0.471029401f);
+			default_rng_t a{1337};
+			a.advance(1000003);
+			EXPECT(a.next_uint() == 2652094483u);
+		}
+		// generate_random_uniform: device batch == host evaluation of the strided order, rng advanced by n
+		{
+			const uint32_t n = 1000;
+			default_rng_t rng{1337};
+			GPUMemory<float> buf(n);
+			generate_random_uniform<float>(nullptr, rng, n, buf.data(), -2.0f, 3.0f);
+			std::vector<float> got(n);
+			buf.copy_to_host(got);
+			const uint32_t n_thr = (n + 3) / 4, n_threads = (n_thr + 127) / 128 * 128;
+			default_rng_t base{1337};
+			int bad = 0;
+			for (uint32_t i = 0; i < n_thr; ++i) {
+				default_rng_t r = base;
+				r.advance(4 * i);
+				for (uint32_t j = 0; j < 4; ++j) {
+					const uint32_t idx = i + n_threads * j;
+					if (idx >= n) break;
+					if (got[idx] != std::fma(r.next_float(), 5.0f, -2.0f)) ++bad;
+				}
+			}
+			EXPECT(bad == 0);
+			default_rng_t adv{1337};
+			adv.advance(n);
+			EXPECT(rng == adv);
+		}
+		// GPUMatrix conventions (gpu_matrix.h): m = features, n = batch, CM default
+		{
+			GPUMatrix<float> a(3, 512);
+			EXPECT(a.m() == 3 && a.n() == 512 && a.layout() == CM && a.stride() == 3 && a.n_elements() == 1536);
+			GPUMatrix<float> v(a.data(), 3, 512);
+			EXPECT(v.data() == a.data());
+			auto t = a.transposed();
+			EXPECT(t.m() == 512 && t.n() == 3 && t.layout() == RM);
+		}
+		// create_from_config -> training_step / loss / inference (config.h:53-63)
+		const uint32_t B = 1 << 16;
+		TrainableModel model = create_from_config(2, 3, config);
+		EXPECT(model.trainer->n_params() == 715536);
+		EXPECT(model.network->padded_output_width() == 16 && model.network->input_width() == 2 && model.network->output_width() == 3);
+		EXPECT(model.trainer->engine() == "fused");
+
+		hipStream_t stream;
+		HIP_CHECK_THROW(hipStreamCreate(&stream));
+		default_rng_t rng{1337};
+		GPUMatrix<float> batch(2, B), target(3, B);
+		GPUMatrix<float> probe(2, 4096), probe_out(3, 4096);
+		generate_random_uniform<float>(stream, rng, probe.n_elements(), probe.data());
+		float first = 0.0f, last = 0.0f;
+		for (int i = 0; i < 200; ++i) {
+			generate_random_uniform<float>(stream, rng, batch.n_elements(), batch.data());
+			linear_kernel(field, 0, stream, B, batch.data(), target.data());
+			auto ctx = model.trainer->training_step(stream, batch, target);
+			if (i == 0) first = model.trainer->loss(stream, *ctx);
+			if (i == 199) last = model.trainer->loss(stream, *ctx);
+			if (i == 198) {
+				// a context of an earlier step is rejected by loss(), as documented
+				auto old = std::move(ctx);
+				bool threw = false;
+				auto ctx2 = model.trainer->training_step(stream, batch, target);
+				try {
+					model.trainer->loss(stream, *old);
+				} catch (const std::runtime_error&) {
+					threw = true;
+				}
+				EXPECT(threw);
+				++i;
+				last = model.trainer->loss(stream, *ctx2);
+			}
+		}
+		std::printf("loss first=%g last=%g\n", first, last);
+		EXPECT(std::isfinite(first) && last < 0.5f * first);
+		EXPECT(model.optimizer->step() == 200u);
+
+		model.network->inference(stream, probe, probe_out);
+		HIP_CHECK_THROW(hipStreamSynchronize(stream));
+		const std::vector<float> out = probe_out.to_cpu_vector();
+		bool finite = true;
+		for (float v : out) finite = finite && std::isfinite(v);
+		EXPECT(finite);
+
+		// hyper-parameters reach the engine (adam.h:200-210)
+		model.optimizer->set_learning_rate(1e-3f);
+		EXPECT(std::fabs(model.optimizer->learning_rate() - 1e-3f) < 1e-9f);
+		model.trainer->update_hyperparams({{"optimizer", {{"learning_rate", 2e-3f}}}});
+		EXPECT(std::fabs(model.trainer->hyperparams()["optimizer"]["learning_rate"].get<float>() - 2e-3f) < 1e-9f);
+
+		// parameters: set_params_full_precision round trip, snapshot round trip
+		std::vector<float> p(model.trainer->n_params());
+		HIP_CHECK_THROW(hipMemcpy(p.data(), model.trainer->params_full_precision(), p.size() * 4, hipMemcpyDeviceToHost));
+		auto snap = model.trainer->serialize_msgpack(true);
+		TrainableModel other = create_from_config(2, 3, config);
+		other.trainer->set_params_full_precision(p.data(), p.size());
+		std::vector<float> q(p.size());
+		HIP_CHECK_THROW(hipMemcpy(q.data(), other.trainer->params_full_precision(), q.size() * 4, hipMemcpyDeviceToHost));
+		EXPECT(p == q);
+		TrainableModel third = create_from_config(2, 3, config);
+		third.trainer->deserialize_msgpack(snap);
+		GPUMatrix<float> out3(3, 4096);
+		third.network->inference(stream, probe, out3);
+		HIP_CHECK_THROW(hipStreamSynchronize(stream));
+		EXPECT(out3.to_cpu_vector() == out);
+
+		// the reference's error behaviour: CHECK_THROW on a batch that is not a multiple of 256
+		{
+			GPUMatrix<float> bad_in(2, 300), bad_t(3, 300);
+			bool threw = false;
+			try {
+				model.trainer->training_step(stream, bad_in, bad_t);
+			} catch (const std::runtime_error&) {
+				threw = true;
+			}
+			EXPECT(threw);
+			threw = false;
+			try {
+				create_loss<network_precision_t>({{"otype", "Huber"}});
+			} catch (const std::runtime_error&) {
+				threw = true;
+			}
+			EXPECT(threw);
+		}
+		// a network that no Trainer owns has no parameters
+		{
+			NetworkWithInputEncoding<network_precision_t> lone(2, 3, config["encoding"], config["network"]);
+			bool threw = false;
+			try {
+				lone.inference(stream, probe, probe_out);
+			} catch (const std::runtime_error&) {
+				threw = true;
+			}
+			EXPECT(threw);
+		}
+		free_all_gpu_memory_arenas();
+		HIP_CHECK_THROW(hipStreamDestroy(stream));
+	} catch (const std::exception& e) {
+		std::printf("FAIL exception: %s\n", e.what());
+		return 1;
+	}
+	if (g_fail) return 1;
+	std::printf("template api ok\n");
+	return 0;
+}
