@@ -59,7 +59,7 @@ static void strided_uniform(Pcg32& rng, size_t n, float* out, float lo, float hi
 	const size_t n_thr = (n + n_gen - 1) / n_gen;
 	const size_t n_threads = (n_thr + 127) / 128 * 128;
 	const float range = hi - lo;
-	for (size_t i = 0; i < n_thr; ++i) {
+	for (size_t i = 0; i < n_threads; ++i) {  // all launched threads write, also those past n_thr (random.h:41-54)
 		Pcg32 r = rng;
 		r.advance((int64_t)(i * n_gen));
 		for (size_t j = 0; j < n_gen; ++j) {

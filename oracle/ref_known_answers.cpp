@@ -27,7 +27,7 @@ static std::vector<float> strided_uniform(pcg32& rng, size_t n, float lo, float 
 	size_t n_thr = (n + N_GEN - 1) / N_GEN;
 	size_t n_threads = (n_thr + 127) / 128 * 128;
 	std::vector<float> out(n);
-	for (size_t i = 0; i < n_thr; ++i) {
+	for (size_t i = 0; i < n_threads; ++i) {  // every launched thread writes (random.h:41-54)
 		pcg32 r = rng;
 		r.advance(i * N_GEN);
 		for (size_t j = 0; j < N_GEN; ++j) {

@@ -195,7 +195,9 @@ void orc_generate_uniform(orc_pcg32* r, size_t n, float* out, float lo, float hi
 	size_t n_thr_needed = (n + n_gen - 1) / n_gen;
 	size_t n_threads = ((n_thr_needed + 127) / 128) * 128;
 	float range = hi - lo;
-	for (size_t i = 0; i < n_thr_needed; ++i) {
+	/* every one of the n_threads launched threads writes (random.h:41-54): the threads past
+	 * n_thr_needed fill out[i + n_threads * j] too, from rng positions 4i.. beyond n */
+	for (size_t i = 0; i < n_threads; ++i) {
 		orc_pcg32 rr = *r;
 		orc_pcg32_advance(&rr, (int64_t)(i * n_gen));
 		for (size_t j = 0; j < n_gen; ++j) {

@@ -63,7 +63,7 @@ int main(int argc, char** argv) {
 			const uint32_t n_thr = (n + 3) / 4, n_threads = (n_thr + 127) / 128 * 128;
 			default_rng_t base{1337};
 			int bad = 0;
-			for (uint32_t i = 0; i < n_thr; ++i) {
+			for (uint32_t i = 0; i < n_threads; ++i) {  // every launched thread writes (random.h:41-54)
 				default_rng_t r = base;
 				r.advance(4 * i);
 				for (uint32_t j = 0; j < 4; ++j) {

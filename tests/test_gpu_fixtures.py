@@ -1,0 +1,146 @@
+"""The HIP path against the FROZEN fixtures F3-F7 (tests/golden, made by tools/make_fixtures.py from
+the oracle and re-checked on the CPU by tests/test_fixtures.py), so a change to the live oracle
+cannot silently move the GPU's parity target.
+
+Tolerances:
+  * F3 grid forward: bit-exact (same fp16 FMA chain and index math)
+  * F4 grid backward: per element, |gpu - ref| <= the fixture's bound (fixed-point step x updates +
+    the oracle's fp32 summation error) + fp16 rounding of the output (2^-11 relative)
+  * F5 MLP (Network module on the layer-wise engine, fp32 MFMA accumulation): output within 4 fp16
+    ulp of the output scale; weight gradients (fp16) and dL/dinput rel L2 <= 1e-3 (5e-3 for the
+    5-hidden-layer net, see tests/test_fixtures.py)
+  * F7 20 training steps of config_hash at B=4096: per-step loss within 3e-2 relative, final
+    parameter norms within 1e-2 (trajectories of fp32-MFMA vs CPU summation orders)
+"""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from helpers import CONFIG_HASH, GOLD, make_batch, trainer_arrays
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tools"))
+import make_fixtures as MF  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_mod():
+    import torch
+    assert torch.cuda.is_available()
+    return torch
+
+
+def _vp(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _load(name):
+    return dict(np.load(os.path.join(GOLD, name + ".npz")))
+
+
+def test_f3_grid_forward_bit_exact(torch_mod):
+    torch = torch_mod
+    from tinycudann import _lib as L
+    lib = L.lib()
+    g, pos, table = MF.f3_inputs()
+    m = L.check_ptr(lib.tcnn_create_encoding(2, json.dumps(CONFIG_HASH["encoding"]).encode(), 1))
+    B = pos.shape[0]
+    out = torch.empty(B, 32, dtype=torch.float16, device="cuda")
+    p16 = torch.from_numpy(table.view(np.float16)).cuda()
+    pos_d = torch.from_numpy(pos).cuda()
+    L.check(lib.tcnn_module_inference(m, None, B, _vp(pos_d), _vp(out), _vp(p16)))
+    torch.cuda.synchronize()
+    lib.tcnn_module_destroy(m)
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint16).T, _load("f3_grid_fwd")["enc"])
+
+
+def test_f4_grid_backward_per_element(torch_mod):
+    torch = torch_mod
+    from tinycudann import _lib as L
+    lib = L.lib()
+    g, pos, dy = MF.f4_inputs()
+    f = _load("f4_grid_bwd")
+    m = L.check_ptr(lib.tcnn_create_encoding(2, json.dumps(CONFIG_HASH["encoding"]).encode(), 1))
+    B = pos.shape[0]
+    n = lib.tcnn_module_n_params(m)
+    assert n == int(f["n_params"][0])
+    p16 = torch.zeros(n, dtype=torch.float16, device="cuda")
+    pos_d = torch.from_numpy(pos).cuda()
+    out = torch.empty(B, 32, dtype=torch.float16, device="cuda")
+    ctx = L.check_ptr(lib.tcnn_module_forward(m, None, B, _vp(pos_d), _vp(out), _vp(p16), 0))
+    dy_d = torch.from_numpy(np.ascontiguousarray(dy.T).view(np.float16)).cuda()  # AoS [B][32]
+    grad = torch.empty(n, dtype=torch.float16, device="cuda")
+    L.check(lib.tcnn_module_backward(m, None, ctx, B, None, _vp(dy_d), _vp(grad), _vp(pos_d), _vp(out), _vp(p16)))
+    torch.cuda.synchronize()
+    lib.tcnn_context_destroy(ctx)
+    lib.tcnn_module_destroy(m)
+    got = grad.float().cpu().numpy().astype(np.float64)
+    ref = np.zeros(n)
+    ref[f["idx"]] = f["val"]
+    tol = np.zeros(n)
+    tol[f["idx"]] = f["tol"]
+    tol = tol + 2.0 ** -11 * (np.abs(ref) + tol) + 2.0 ** -25
+    bad = np.flatnonzero(np.abs(got - ref) > tol)
+    assert bad.size == 0, (bad.size, bad[:5], got[bad[:5]], ref[bad[:5]])
+    # untouched entries are exactly zero
+    assert np.all(got[np.setdiff1d(np.arange(n), f["idx"])] == 0.0)
+
+
+@pytest.mark.parametrize("shape", MF.MLP_SHAPES)
+def test_f5_mlp_module(torch_mod, shape):
+    torch = torch_mod
+    from tinycudann import _lib as L
+    lib = L.lib()
+    W, H, IN = shape
+    params, x, dout = MF.f5_inputs(W, H, IN)
+    f = _load(f"f5_mlp_w{W}_h{H}_in{IN}")
+    net = {"otype": "FullyFusedMLP", "n_neurons": W, "n_hidden_layers": H, "activation": "ReLU", "output_activation": "None"}
+    m = L.check_ptr(lib.tcnn_create_network(IN, 16, json.dumps(net).encode()))
+    n = lib.tcnn_module_n_params(m)
+    assert n == params.size
+    B = x.shape[0]
+    xin = torch.from_numpy(x.view(np.float16).astype(np.float32)).cuda()  # fp16-exact values through Identity
+    p16 = torch.from_numpy(params.view(np.float16)).cuda()
+    out = torch.empty(B, 16, dtype=torch.float16, device="cuda")
+    ctx = L.check_ptr(lib.tcnn_module_forward(m, None, B, _vp(xin), _vp(out), _vp(p16), 1))
+    d_d = torch.from_numpy(dout.view(np.float16)).cuda()
+    grad = torch.empty(n, dtype=torch.float16, device="cuda")
+    dx = torch.empty(B, IN, dtype=torch.float32, device="cuda")
+    L.check(lib.tcnn_module_backward(m, None, ctx, B, _vp(dx), _vp(d_d), _vp(grad), _vp(xin), _vp(out), _vp(p16)))
+    torch.cuda.synchronize()
+    lib.tcnn_context_destroy(ctx)
+    lib.tcnn_module_destroy(m)
+    a = f["out"].view(np.float16).astype(np.float64)
+    b = out.cpu().numpy().astype(np.float64)
+    scale_ulp = float(np.spacing(np.float16(np.abs(a).max())))
+    assert np.max(np.abs(a - b)) <= 4 * scale_ulp, (np.max(np.abs(a - b)), scale_ulp)
+    lim = 5e-3 if H >= 5 else 1e-3
+    wg = grad.float().cpu().numpy().astype(np.float64)
+    ew = np.linalg.norm(wg - f["wgrad"]) / np.linalg.norm(f["wgrad"])
+    assert ew <= lim, ew
+    rdx = f["dinput"].view(np.float16).astype(np.float64)
+    ed = np.linalg.norm(dx.cpu().numpy() - rdx) / np.linalg.norm(rdx)
+    assert ed <= lim, ed
+
+
+def test_f7_training_trajectory(torch_mod):
+    torch = torch_mod
+    from tinycudann import Trainer
+    frozen = json.load(open(os.path.join(GOLD, "f7_train20.json")))
+    t = Trainer(2, 3, CONFIG_HASH, seed=1337)
+    losses = []
+    for s in range(20):
+        pos, tgt = make_batch(4096, step=s)
+        t.training_step(torch.from_numpy(pos).cuda(), torch.from_numpy(tgt).cuda())
+        losses.append(t.loss())
+    np.testing.assert_allclose(losses, frozen["loss"], rtol=3e-2)
+    a = trainer_arrays(t)
+    nm = t.n_network_params
+    assert abs(np.linalg.norm(a["w32"][:nm].astype(np.float64)) - frozen["mlp_l2"]) <= 1e-2 * frozen["mlp_l2"]
+    assert abs(np.linalg.norm(a["w32"][nm:].astype(np.float64)) - frozen["grid_l2"]) <= 1e-2 * frozen["grid_l2"]
