@@ -3,9 +3,12 @@ log2T15 s1.5 + FullyFusedMLP 64x2, RelativeL2, Adam) -- BASELINE.json `metric`.
 
 One step = Trainer::training_step over one 2^18-point batch resident in HBM: fused grid-encode +
 MLP fwd + loss + MLP bwd + weight gradients, grid backward, reductions, Adam (and, with N>1 ranks,
-the RCCL all-reduce of the fp32 gradient sums). Synthetic data: uniform positions, analytic RGB
-targets (no image I/O). Multi-GPU is data parallel, weak scaling: every rank trains on its own
-2^18 batch per step; `value` counts 2^18-sample training steps completed by all ranks per second.
+the RCCL all-reduce of the gradient sums, overlapped with the grid backward). Synthetic data:
+uniform positions, analytic RGB targets. Multi-GPU is data parallel:
+  --scaling strong (default; BASELINE configs[4] / SURVEY C5): the global 2^18 batch is sharded
+      2^18/N points per rank; `value` = global 2^18-sample steps per second;
+  --scaling weak: every rank trains on its own 2^18 batch; `value` = 2^18-sample steps completed by
+      all ranks per second.
 
   python bench.py [--gpus N --steps K --warmup W]
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
@@ -43,33 +46,56 @@ def rgb_field_torch(pos):
     return torch.stack([r, g, b], dim=1).float().contiguous()
 
 
-def cpu_baseline(cfg, budget_s=12.0):
-    """CPU restatement (oracle/, fp32 OpenMP) timed on the host: `port` baseline."""
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(cfg):
+    """CPU restatement (oracle/, fp32 OpenMP) timed on the host: the `port` baseline (the reference
+    has no CPU path). Bounded sample (~25 s): all threads of this box's CPU share
+    (OMP_NUM_THREADS, 16 on the GPU box) at C3 (B=2^18, the bench workload -- `value`) and C1
+    (B=2^16); one thread at C1. Each timed after one warm-up step."""
     import numpy as np
     from oracle import oracle as O
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    threads = min(threads, 16)
-    B = 1 << 16
-    om = O.OracleModel(cfg, 2, 3, seed=1337)
-    r = O.pcg32(1337)
-    pos = O.generate_uniform(r, 2 * B).reshape(B, 2)
-    tgt = np.stack([0.5 + 0.5 * np.sin(9 * pos[:, 0]), pos[:, 1], pos[:, 0] * pos[:, 1]], axis=1).astype(np.float32)
-    om.train_step(pos, tgt, n_threads=threads)  # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
-        om.train_step(pos, tgt, n_threads=threads)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or n >= 200:
-            break
-    steps_per_s_2p16 = n / el
+
+    def timed(B, n_threads, budget_s, max_steps):
+        om = O.OracleModel(cfg, 2, 3, seed=1337)
+        r = O.pcg32(1337)
+        pos = O.generate_uniform(r, 2 * B).reshape(B, 2)
+        tgt = np.stack([0.5 + 0.5 * np.sin(9 * pos[:, 0]), pos[:, 1], pos[:, 0] * pos[:, 1]], axis=1).astype(np.float32)
+        om.train_step(pos, tgt, n_threads=n_threads)  # warm-up
+        n, t0 = 0, time.perf_counter()
+        while True:
+            om.train_step(pos, tgt, n_threads=n_threads)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= budget_s or n >= max_steps:
+                return n / el, n, el
+
+    c3, n3, e3 = timed(1 << 18, threads, 8.0, 50)
+    c1, n1, e1 = timed(1 << 16, threads, 4.0, 100)
+    s1, ns1, es1 = timed(1 << 16, 1, 6.0, 20)
     return {
-        "value": steps_per_s_2p16 * (B / float(1 << 18)),
-        "unit": "training steps/s (2^18-sample batch equivalent)",
+        "value": c3,
+        "unit": "training steps/s (2^18-sample batches)",
         "cores": threads,
         "kind": "port",
-        "sample": f"{n} oracle training steps of config_hash.json at B=2^16 on {threads} host threads "
-                  f"({el:.1f} s, {steps_per_s_2p16:.3f} steps/s at 2^16, scaled x1/4 to 2^18 samples/step)",
+        "cpu": _cpu_model(),
+        "sample": f"oracle training steps of config_hash.json on the GPU box's host ({_cpu_model()}): "
+                  f"C3 B=2^18 on {threads} threads: {n3} steps in {e3:.1f} s",
+        "variants": {
+            f"C3_2^18_{threads}threads_steps_per_s": c3,
+            f"C1_2^16_{threads}threads_steps_per_s": c1,
+            "C1_2^16_1thread_steps_per_s": s1,
+            "C1_samples": f"{n1} steps in {e1:.1f} s ({threads} threads), {ns1} steps in {es1:.1f} s (1 thread)",
+        },
     }
 
 
@@ -99,6 +125,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (rehearsal)")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                    help="strong: shard the global batch over ranks (configs[4]); weak: a full batch per rank")
+    ap.add_argument("--allreduce-dtype", choices=["fp32", "fp16"], default="fp32")
+    ap.add_argument("--no-overlap", action="store_true", help="all-reduce after the whole backward")
     ap.add_argument("--all-ranks-on-device0", action="store_true",
                     help="rehearse N>1 on a 1-GPU box (gloo); never used for measurements")
     args = ap.parse_args()
@@ -127,7 +157,9 @@ def main():
         cfg["encoding"]["log2_hashmap_size"] = args.log2_hashmap_size
     if args.per_level_scale is not None:
         cfg["encoding"]["per_level_scale"] = args.per_level_scale
-    B = 1 << args.batch_log2
+    B_global = 1 << args.batch_log2
+    B = B_global // world if args.scaling == "strong" else B_global  # this rank's points per step
+    assert B % 256 == 0, "per-rank batch must be a multiple of 256"
     trainer = Trainer(2, 3, cfg, seed=1337)
     g = torch.Generator(device="cuda")
     g.manual_seed(1337 + 7919 * rank)
@@ -138,7 +170,7 @@ def main():
         batches.append((pos, rgb_field_torch(pos)))
 
     from tinycudann.parallel import DataParallelTrainer
-    dp = DataParallelTrainer(trainer)
+    dp = DataParallelTrainer(trainer, overlap=not args.no_overlap, allreduce_dtype=args.allreduce_dtype)
 
     def step(i):
         pos, tgt = batches[i % NB]
@@ -179,30 +211,34 @@ def main():
             dist.destroy_process_group()
         return
 
-    units = world * args.steps
+    units = args.steps if args.scaling == "strong" else world * args.steps  # global 2^18-sample steps
     value = units / elapsed
     res = {
         "metric": "training steps/sec at batch=2^18, config_hash.json (HashGrid+64-wide MLP)",
         "value": value,
-        "unit": "training steps/s (2^18-sample batches, summed over ranks)",
+        "unit": "training steps/s (2^18-sample batches, whole job)",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": 1000.0 * elapsed / args.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "fp16 storage / fp32 MFMA accumulate",
         "data": "synthetic (uniform positions, analytic RGB targets), random-init weights (Trainer seed 1337)",
         "config": {
             "workload": "mlp_learning_an_image training step, data/config_hash.json as-is "
                         "(HashGrid L16 F2 log2T15 s1.5 base16 + FullyFusedMLP W64 H2 ReLU, RelativeL2, Adam)",
-            "global_batch": B * world, "per_gpu_batch": B, "parallelism": f"dp{world}",
+            "global_batch": B * world, "per_gpu_batch": B,
+            "parallelism": "dp1" if world == 1 else (f"dp{world} batch-sharded ({B_global}/{world} points per rank)" if args.scaling == "strong"
+                            else f"dp{world} ({B} points per rank)") +
+                           (f", {args.allreduce_dtype} all-reduce" + ("" if args.no_overlap else " overlapped with the grid backward")
+                            if world > 1 else ""),
         },
-        "samples_per_s": value * B,
+        "samples_per_s": value * B_global,
         "final_loss": loss,
     }
-    if phase_ms:
+    if phase_ms and (phase_ms[PHASES[0]] > 0 or phase_ms[PHASES[1]] > 0):
         res["phase_ms"] = phase_ms
         t_fused = phase_ms[PHASES[0]]
         t_gbwd = phase_ms[PHASES[1]]

@@ -117,6 +117,12 @@ void tcnn_trainer_destroy(tcnn_trainer* t);
 /* Trainer::training_step(stream, input [n x n_in] fp32, target [n x n_out] fp32, run_optimizer) (trainer.h:163-190). */
 int tcnn_trainer_training_step(tcnn_trainer* t, void* stream, uint32_t n, const float* input, const float* target,
                                int run_optimizer);
+/* Data-parallel split of training_step(run_optimizer = 0): part 0 = forward + loss + MLP backward
+ * with the network gradients final in gradients_fp32()[0, n_network_params) and the loss sum; part 1
+ * = the grid backward filling gradients_fp32()[n_network_params, n_params). Between the two the
+ * caller may all-reduce the network gradients on another stream while part 1 runs. Results are
+ * bit-identical to training_step(run_optimizer = 0). */
+int tcnn_trainer_training_step_part(tcnn_trainer* t, void* stream, uint32_t n, const float* input, const float* target, int part);
 /* Trainer::optimizer_step(stream, loss_scale) (trainer.h:155-157) */
 int tcnn_trainer_optimizer_step(tcnn_trainer* t, void* stream);
 /* Trainer::loss(stream, ctx) of the last training step (trainer.h:205-207); synchronises `stream`. */

@@ -354,6 +354,9 @@ int tcnn_trainer_training_step(tcnn_trainer* t, void* stream, uint32_t n, const 
 		t->t->training_step((hipStream_t)stream, n, in, target, run_opt != 0);
 	});
 }
+int tcnn_trainer_training_step_part(tcnn_trainer* t, void* stream, uint32_t n, const float* in, const float* target, int part) {
+	return guard([&] { t->t->training_step_part((hipStream_t)stream, n, in, target, part); });
+}
 int tcnn_trainer_optimizer_step(tcnn_trainer* t, void* stream) {
 	return guard([&] { t->t->optimizer_step((hipStream_t)stream); });
 }

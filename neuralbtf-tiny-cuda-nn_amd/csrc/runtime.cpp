@@ -902,6 +902,32 @@ AdamArgs TrainerHost::adam_args() const {
 	return a;
 }
 
+// Data-parallel step in two parts, so the caller can all-reduce the network gradients while the
+// grid backward runs (part 0: fused grid+MLP kernel, network-gradient column sums into
+// g32[0, n_mlp) and the loss sum; part 1: grid backward + slab reduction into g32[n_mlp, n)). Same
+// kernels and summation orders as training_step(run_optimizer = false). The layer-wise engine does
+// its whole pass in part 0.
+void TrainerHost::training_step_part(hipStream_t st, uint32_t B, const float* input, const float* target, int part) {
+	TCNN_CHECK(B % BATCH_GRANULARITY == 0, "training_step: batch size must be a multiple of 256");
+	TCNN_CHECK(part == 0 || part == 1, "training_step_part: part must be 0 or 1");
+	NetworkHost& m = *model;
+	if (!overlapped_ok()) {
+		if (part == 0) training_step(st, B, input, target, false);
+		return;
+	}
+	if (part == 0) {
+		m.fused_kernel(st, ws, B, input, target, n_output_dims, loss_scale, w16.p, false);
+		launch_column_sums(st, ws.wgrad_partial.as<float>(), ws.n_fused_blocks, (uint32_t)n_mlp, g32.as<float>());
+		launch_sum(st, ws.loss_partial.as<float>(), ws.n_loss_partials, d_loss.as<float>());
+		last_B = B;
+		return;
+	}
+	TCNN_CHECK(last_B == B, "training_step_part: part 1 must follow part 0 of the same batch");
+	m.grid_backward(st, ws, B, input);
+	m.grid->backward_acc(st, ws.gbw, B, ws.dLdenc.p, 0, 0, g32.as<float>() + n_mlp);
+	m.grid->reduce_items(st, ws.gbw, g32.as<float>() + n_mlp);
+}
+
 AdamArgs TrainerHost::adam_args_table(hipStream_t st, uint32_t upto, uint32_t reserve) {
 	AdamArgs a = adam_args();
 	if (ftable_b1 != adam.beta1 || ftable_b2 != adam.beta2) {  // hyper-parameters changed: recompute all

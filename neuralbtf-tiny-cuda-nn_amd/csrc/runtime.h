@@ -274,6 +274,7 @@ struct TrainerHost {
 	TrainerHost(uint32_t n_in, uint32_t n_out, const json& cfg, uint32_t seed);
 	void initialize_params(uint32_t seed);
 	void training_step(hipStream_t st, uint32_t B, const float* input, const float* target, bool run_optimizer);
+	void training_step_part(hipStream_t st, uint32_t B, const float* input, const float* target, int part);
 	void optimizer_step(hipStream_t st);
 	float loss(hipStream_t st);
 	void inference(hipStream_t st, uint32_t B, const float* input, float* out);

@@ -38,6 +38,13 @@ class Trainer:
         L.check(L.lib().tcnn_trainer_training_step(self.h, _stream(stream), input.shape[0], ctypes.c_void_p(input.data_ptr()),
                                                    ctypes.c_void_p(target.data_ptr()), int(run_optimizer)))
 
+    def training_step_part(self, input, target, part, stream=None):
+        """Data-parallel split of training_step(run_optimizer=False): part 0 leaves the network
+        gradients final (gradients_fp32()[:n_network_params]), part 1 runs the grid backward."""
+        assert input.is_contiguous() and target.is_contiguous()
+        L.check(L.lib().tcnn_trainer_training_step_part(self.h, _stream(stream), input.shape[0], ctypes.c_void_p(input.data_ptr()),
+                                                        ctypes.c_void_p(target.data_ptr()), int(part)))
+
     def optimizer_step(self, stream=None):
         L.check(L.lib().tcnn_trainer_optimizer_step(self.h, _stream(stream)))
 

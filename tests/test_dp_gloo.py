@@ -72,3 +72,92 @@ def test_two_rank_gradient_allreduce_matches_full_batch():
     nm = om.n_mlp_params
     assert rel_err(g_avg[:nm], om.grad32[:nm]) < 2e-3
     assert rel_err(g_avg[nm:], om.grad32[nm:]) < 2e-3
+
+
+class _FakeTrainer:
+    """Stands in for tinycudann.Trainer on the CPU: deterministic per-rank gradients, records what
+    the optimizer step would read (gradient buffer x gradient scale)."""
+
+    def __init__(self, rank, n_net=8, n=40):
+        self.rank = rank
+        self.n_network_params = n_net
+        self.g = torch.zeros(n, dtype=torch.float32)
+        self.scale = 1.0
+        self.parts = []
+        self.seen = None
+
+    def gradients_fp32(self):
+        return self.g
+
+    def set_gradient_scale(self, s):
+        self.scale = s
+
+    def _fill(self, lo, hi):
+        idx = torch.arange(lo, hi, dtype=torch.float32)
+        self.g[lo:hi] = (idx + 1.0) * (self.rank + 1) * 0.37
+
+    def training_step_part(self, x, t, part):
+        self.parts.append(part)
+        if part == 0:
+            self._fill(0, self.n_network_params)
+        else:
+            self._fill(self.n_network_params, self.g.numel())
+
+    def training_step(self, x, t, run_optimizer=True):
+        assert not run_optimizer
+        self._fill(0, self.g.numel())
+
+    def optimizer_step(self):
+        self.seen = (self.g * self.scale).clone()
+
+
+def _sched_worker(rank, world, port, out_q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    sys.path[:0] = [repo, os.path.join(repo, "neuralbtf-tiny-cuda-nn_amd"), here]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tinycudann.parallel import DataParallelTrainer, shard
+    res = {}
+    for overlap in (True, False):
+        for dtype in ("fp32", "fp16"):
+            t = _FakeTrainer(rank)
+            dp = DataParallelTrainer(t, overlap=overlap, allreduce_dtype=dtype)
+            dp.training_step(None, None)
+            res[(overlap, dtype)] = (t.seen.numpy(), t.parts)
+    x = torch.arange(10 * 3).reshape(10, 3)
+    res["shard"] = shard(x, rank, world).numpy()
+    out_q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_exchange_schedule_and_sharding():
+    """DataParallelTrainer on gloo world 2 (CPU): the overlapped two-part schedule (network
+    gradients first) and the plain one give the same Adam input = mean of the rank gradients; the
+    fp16 exchange = fp16 sum of the pre-divided fp16 gradients; strong-scaling shards tile the
+    global batch."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sched_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    idx = np.arange(40, dtype=np.float32)
+    mean = ((idx + 1) * 1 * np.float32(0.37) + (idx + 1) * 2 * np.float32(0.37)) / 2
+    for r in range(world):
+        g_over, parts = res[r][(True, "fp32")]
+        assert parts == [0, 1]
+        np.testing.assert_allclose(g_over, mean, rtol=1e-6)
+        np.testing.assert_array_equal(g_over, res[r][(False, "fp32")][0])
+        g16 = res[r][(True, "fp16")][0]
+        h = [((idx + 1) * (k + 1) * np.float32(0.37) / 2).astype(np.float16) for k in range(world)]
+        np.testing.assert_array_equal(g16, (h[0] + h[1]).astype(np.float32))
+    np.testing.assert_array_equal(np.concatenate([res[0]["shard"], res[1]["shard"]]), np.arange(30).reshape(10, 3))

@@ -42,13 +42,18 @@ def _worker(rank, world, port, B, q):
     scale = allreduce_gradients(g)
     g_avg = (g * scale).cpu().numpy()
     # full DataParallelTrainer steps on a fresh replica
-    tr2 = Trainer(2, 3, CONFIG_HASH, seed=1337)
-    dp = DataParallelTrainer(tr2)
-    for s in range(3):
-        pos_s, tgt_s = make_batch(B, step=s)
-        dp.training_step(torch.from_numpy(pos_s[lo:hi]).cuda(), torch.from_numpy(tgt_s[lo:hi]).cuda())
-    torch.cuda.synchronize()
-    q.put((rank, g_avg, trainer_arrays(tr2)["w32"]))
+    def run(**kw):
+        tr2 = Trainer(2, 3, CONFIG_HASH, seed=1337)
+        dp = DataParallelTrainer(tr2, **kw)
+        for s in range(3):
+            pos_s, tgt_s = make_batch(B, step=s)
+            dp.training_step(torch.from_numpy(pos_s[lo:hi]).cuda(), torch.from_numpy(tgt_s[lo:hi]).cuda())
+        torch.cuda.synchronize()
+        return trainer_arrays(tr2)["w32"]
+    w_over = run()                            # two-part step, network all-reduce overlapping the grid backward
+    w_plain = run(overlap=False)              # whole backward, then the all-reduce
+    w_half = run(allreduce_dtype="fp16")      # pre-divided fp16 exchange
+    q.put((rank, g_avg, w_over, w_plain, w_half))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -69,6 +74,11 @@ def test_two_rank_gpu_allreduce_matches_full_batch():
         p.join(timeout=60)
         assert p.exitcode == 0
     np.testing.assert_array_equal(res[0][2], res[1][2])  # replicas identical
+    np.testing.assert_array_equal(res[0][2], res[0][3])  # overlapped schedule == plain schedule, bit for bit
+    np.testing.assert_array_equal(res[0][4], res[1][4])  # fp16 exchange: replicas identical too
+    # close to the fp32 exchange: a gradient that rounds to 0 in one exchange and not the other is
+    # skipped by Adam (adam.h:76-79) in one run only, so parameters differ by ~lr in a few places
+    assert rel_err(res[0][4], res[0][2]) < 1e-2
     np.testing.assert_array_equal(res[0][1], res[1][1])
     from tinycudann import Trainer
     pos, tgt = make_batch(B)
