@@ -207,6 +207,15 @@ size_t reduce_partials_tmp_floats(uint32_t n_parts, uint32_t n);
 void launch_reduce_partials(hipStream_t st, const float* in, uint32_t n_parts, uint32_t stride, uint32_t n,
                             float* out, float* tmp);
 
+// ---- tile engine (mlp_tile.hip): fused MLP training for W in {64, 128}, encoded input fp16 [B][IN] ----
+uint32_t tile_train_lds_bytes(uint32_t W, uint32_t IN, uint32_t NH);
+bool tile_train_supported(uint32_t W, uint32_t IN, uint32_t NH, uint32_t outp, int act);
+uint32_t tile_train_blocks(uint32_t B);
+// dldenc (optional): dL/d(encoding) as level-major pairs [IN/2][B] (dldenc_pairs) or AoS fp16 [B][IN]
+void launch_mlp_tile_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, int act, uint32_t B, uint32_t dims, float loss_scale,
+                           uint32_t loss_l2, const void* params16, const void* enc16, const float* target, const void* dout16, void* out16,
+                           void* dldenc, int dldenc_pairs, float* wgrad_partial, float* loss_partial);
+
 // generate_random_uniform<float> (random.h:57-70) from pcg32 {state, inc} (not advanced here)
 void launch_generate_uniform(hipStream_t st, uint64_t n, uint64_t state, uint64_t inc, float* out, float lo, float hi);
 // factor_table[t - 1] = adam_bias_factor(a, t) for t in (lo, hi]

@@ -505,6 +505,13 @@ bool NetworkHost::fused_ok() const {
 	                             grid->desc.n_features_per_level, mlp.padded_output, mlp.activation, grid->desc.hash_type);
 }
 
+bool NetworkHost::tile_ok() const {
+	const bool ff = ieq(mlp.otype, "FullyFusedMLP") || ieq(mlp.otype, "MegakernelMLP");
+	if (!ff || fused_ok() || mlp.output_activation != 0) return false;
+	if (std::getenv("TCNN_NO_TILE_ENGINE")) return false;  // A/B switch: the layer-wise engine instead
+	return tile_train_supported(mlp.width, mlp.n_input, mlp.n_hidden_layers, mlp.padded_output, mlp.activation);
+}
+
 bool NetworkHost::layered_ok() const {
 	return layered_width_supported(mlp.width) && mlp.n_input % 16 == 0 && mlp.n_input <= 128 && mlp.padded_output <= 128 &&
 	       mlp.activation != ACT_SINE && mlp.output_activation != ACT_SINE;  // Sine has no post-activation backward
@@ -558,6 +565,7 @@ void NetworkHost::fwd_bwd(hipStream_t st, StepWorkspace& ws, uint32_t B, const f
                           float loss_scale, const void* params16, const void* dout16, void* out16, float* grad32,
                           const std::function<void(int)>& mark, float* dL_dinput) {
 	if (fused_ok() && !dL_dinput) fwd_bwd_fused(st, ws, B, pos, target, dims, loss_scale, params16, dout16, out16, grad32, mark);
+	else if (tile_ok()) fwd_bwd_tile(st, ws, B, pos, target, dims, loss_scale, params16, dout16, out16, grad32, mark, dL_dinput);
 	else fwd_bwd_layered(st, ws, B, pos, target, dims, loss_scale, params16, dout16, out16, grad32, mark, dL_dinput);
 }
 
@@ -614,6 +622,39 @@ void NetworkHost::fwd_bwd_fused(hipStream_t st, StepWorkspace& ws, uint32_t B, c
 	if (mark) mark(2);
 	launch_column_sums(st, ws.wgrad_partial.as<float>(), ws.n_fused_blocks, n_mlp, grad32);
 	grid->reduce_items(st, ws.gbw, grad32 + n_mlp);
+	if (mark) mark(3);
+}
+
+// Tile-engine training pass (mlp_tile.hip): encoding forward (AoS fp16), one fused kernel for the
+// whole network over 32-sample tiles (forward, loss, backward, weight-gradient partials, dL/d(enc)),
+// the partial reduction, then the encoding's backward.
+void NetworkHost::fwd_bwd_tile(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target, uint32_t dims,
+                               float loss_scale, const void* params16, const void* dout16, void* out16, float* grad32,
+                               const std::function<void(int)>& mark, float* dL_dinput) {
+	TCNN_CHECK(B % 32 == 0, "training: batch must be a multiple of 32");
+	const uint32_t W = mlp.width, IN = mlp.n_input, NH = mlp.n_hidden_layers;
+	const uint32_t n_mlp = mlp.n_params();
+	const uint8_t* eparams = (const uint8_t*)params16 + (size_t)n_mlp * 2;
+	ws.enc16.reserve((size_t)B * IN * 2);
+	enc->forward_aos(st, B, pos, eparams, ws.enc16.p);
+	const uint32_t nb = tile_train_blocks(B);
+	ws.wgrad_partial.reserve((size_t)nb * n_mlp * 4);
+	ws.loss_partial.reserve((size_t)nb * 4);
+	const bool enc_grad = enc->n_params() > 0 || dL_dinput;
+	// a grid with feature pairs and no padding takes dL/d(encoding) as level-major pairs [L][B]
+	const bool pairs = grid && grid->desc.n_features_per_level == 2 && grid->n_to_pad == 0;
+	if (enc_grad) ws.delta0.reserve((size_t)B * IN * 2);
+	launch_mlp_tile_train(st, W, IN, NH, mlp.activation, B, dims, loss_scale, loss_l2, params16, ws.enc16.p, target, dout16, out16,
+	                      enc_grad ? ws.delta0.p : nullptr, pairs ? 1 : 0, ws.wgrad_partial.as<float>(), ws.loss_partial.as<float>());
+	ws.n_loss_partials = dout16 ? 0 : nb;
+	const size_t tf = reduce_partials_tmp_floats(nb, n_mlp);
+	if (tf) ws.red_tmp.reserve(tf * 4);
+	launch_reduce_partials(st, ws.wgrad_partial.as<float>(), nb, n_mlp, n_mlp, grad32, ws.red_tmp.as<float>());
+	if (mark) mark(1);
+	const int dy_layout = pairs ? 0 : 2;
+	if (dL_dinput) enc->backward_input(st, B, pos, ws.delta0.p, dL_dinput, eparams, dy_layout);
+	if (grid) grid->backward(st, ws.gbw, B, pos, grid->desc.n_pos_dims, ws.delta0.p, dy_layout, IN, grad32 + n_mlp);
+	if (mark) mark(2);
 	if (mark) mark(3);
 }
 

@@ -193,9 +193,10 @@ struct NetworkHost {
 	uint32_t loss_l2 = 0;  // training loss: 0 RelativeL2 (relative_l2.h), 1 L2 (l2.h)
 	NetworkHost(uint32_t n_in, uint32_t n_out, const json& enc, const json& net);
 	uint64_t n_params() const { return (uint64_t)mlp.n_params() + enc->n_params(); }
-	bool fused_ok() const;
+	bool fused_ok() const;   // register-resident kernel (mlp_fused.h): grid input, W <= 64
+	bool tile_ok() const;    // tile kernel (mlp_tile.hip): W in {64, 128}, any encoding, weights + tile in LDS
 	bool layered_ok() const;
-	const char* engine() const { return fused_ok() ? "fused" : layered_ok() ? "layered" : "unsupported"; }
+	const char* engine() const { return (fused_ok() || tile_ok()) ? "fused" : layered_ok() ? "layered" : "unsupported"; }
 	void initialize_params(Pcg32& rng, float* host_out, float scale = 1.0f) const;  // network first (nwie.h:124-130)
 
 	// params16: [mlp | encoding] fp16. out16: fp16 [B][padded_output].
@@ -218,6 +219,9 @@ private:
 	void fwd_bwd_fused(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target, uint32_t dims,
 	                   float loss_scale, const void* params16, const void* dout16, void* out16, float* grad32,
 	                   const std::function<void(int)>& mark);
+	void fwd_bwd_tile(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target, uint32_t dims,
+	                  float loss_scale, const void* params16, const void* dout16, void* out16, float* grad32,
+	                  const std::function<void(int)>& mark, float* dL_dinput);
 	void fwd_bwd_layered(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target, uint32_t dims,
 	                     float loss_scale, const void* params16, const void* dout16, void* out16, float* grad32,
 	                     const std::function<void(int)>& mark, float* dL_dinput);

@@ -35,7 +35,7 @@ def _l2_config(base):
     return cfg
 
 
-@pytest.mark.parametrize("which", ["fused", "layered"])
+@pytest.mark.parametrize("which", ["fused", "tile", "layered"])
 def test_l2_loss_step_matches_oracle(torch_mod, which):
     torch = torch_mod
     from tinycudann import Trainer
@@ -44,8 +44,10 @@ def test_l2_loss_step_matches_oracle(torch_mod, which):
     else:
         cfg = _l2_config(CONFIG_ONEBLOB)
         cfg["network"] = dict(cfg["network"], n_neurons=64, n_hidden_layers=2)
+        if which == "layered":
+            cfg["network"]["otype"] = "CutlassMLP"
     t = Trainer(2, 3, cfg, seed=1337)
-    assert t.engine == which
+    assert t.engine == ("layered" if which == "layered" else "fused")
     om = O.OracleModel(cfg, 2, 3, seed=1337)
     B = 2048
     pos, tgt = make_batch(B)

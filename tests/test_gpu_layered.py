@@ -50,7 +50,13 @@ CONFIGS = {
     # CutlassMLP at widths FullyFusedMLP does not take (any multiple of 16, cutlass_mlp.h:115-121)
     "hashgrid_cutlass_w48_h3": (_cfg(CONFIG_HASH["encoding"], _net(48, 3, "CutlassMLP")), 1e-3),
     "oneblob_cutlass_w112_h2": (_cfg({"otype": "OneBlob", "n_bins": 32}, _net(112, 2, "CutlassMLP")), 2e-3),
+    # FullyFusedMLP shapes of the tile engine (mlp_tile.hip): W64 with IN = 16 / 128 and 5 hidden layers
+    "identity_w64_h3": (_cfg({"otype": "Identity"}, _net(64, 3)), 1e-3),
+    "oneblob_w64_h5": (_cfg({"otype": "OneBlob", "n_bins": 64}, _net(64, 5)), 2e-3),
+    "hashgrid_w128_h2": (_cfg(CONFIG_HASH["encoding"], _net(128, 2)), 1e-3),
 }
+# FullyFusedMLP configurations the tile engine trains (engine "fused"); the rest run layer by layer
+TILE = {"oneblob_w64_h2", "oneblob16_w64_h2", "hashgrid_w128_h4", "identity_w64_h3", "oneblob_w64_h5", "hashgrid_w128_h2"}
 
 
 @pytest.mark.parametrize("n_bins,n_in", [(64, 2), (16, 2), (16, 3), (32, 1)])
@@ -89,7 +95,7 @@ def test_layered_step_gradients_and_loss(torch_mod, name):
     from tinycudann import Trainer
     cfg, tol = CONFIGS[name]
     t = Trainer(2, 3, cfg, seed=1337)
-    assert t.engine == "layered", t.engine
+    assert t.engine == ("fused" if name in TILE else "layered"), t.engine
     om = O.OracleModel(cfg, 2, 3, seed=1337)
     assert t.n_params == om.n_params
     a0 = trainer_arrays(t)
@@ -122,7 +128,7 @@ def test_layered_inference_matches_oracle(torch_mod, name):
     np.testing.assert_allclose(out, ref, rtol=2e-3, atol=2e-4)
 
 
-@pytest.mark.parametrize("name", ["oneblob_as_file_w128_h5", "hashgrid_w128_h4"])
+@pytest.mark.parametrize("name", ["oneblob_as_file_w128_h5", "hashgrid_w128_h4", "oneblob_w64_h5"])
 def test_layered_training_trajectory_tracks_oracle(torch_mod, name):
     torch = torch_mod
     from tinycudann import Trainer
@@ -142,12 +148,13 @@ def test_layered_training_trajectory_tracks_oracle(torch_mod, name):
 
 
 def test_lds_pressure_config_full_batch(torch_mod):
-    """BASELINE configs[3]: HashGrid + W128/H4 at B = 2^20 on one GPU -- finite, decreasing loss
-    (size-independent property; the oracle covers the same code at B = 512 above)."""
+    """BASELINE configs[3]: HashGrid + W128/H4 at B = 2^20 on one GPU (tile engine) -- finite,
+    decreasing loss (size-independent property; the oracle covers the same code at B = 512 above)."""
     torch = torch_mod
     from tinycudann import Trainer
     cfg, _ = CONFIGS["hashgrid_w128_h4"]
     t = Trainer(2, 3, cfg, seed=1337)
+    assert t.engine == "fused"
     B = 1 << 20
     losses = []
     for s in range(6):
