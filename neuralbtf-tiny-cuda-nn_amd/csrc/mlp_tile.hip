@@ -30,14 +30,17 @@ struct TileLayout {
 	static_assert(IN % 16 == 0 && IN <= 128, "tile engine: IN a multiple of 16, <= 128");
 	static constexpr int KP0 = (IN + 31) / 32 * 32;  // K of the first layer, padded to the MFMA depth
 	static constexpr int RS0 = KP0 + 8, RSW = W + 8, RSG = 24;
-	static constexpr int MT = W / 16, MTW = MT / 4;  // output-row tiles per matrix / per wave
+	// W128 runs 8 waves (2 per SIMD: each owns one 16-row tile of every matrix, 108 accumulator
+	// registers), W64 4 waves; either way one output-row tile per wave
+	static constexpr int WAVES = W == 128 ? 8 : 4, NTHR = WAVES * 64;
+	static constexpr int MT = W / 16, MTW = MT / WAVES;  // output-row tiles per matrix / per wave
 	static constexpr int KT0 = IN / 16;              // feature tiles of the input
 	static constexpr int oW0 = 0, oWh = oW0 + W * RS0, oWo = oWh + (NH - 1) * W * RSW;
 	static constexpr int oX = oWo + 16 * RSW;                 // slot 0: the tile's input [32][RS0]
 	static constexpr int oA = oX + 32 * RS0;                  // slots 1..NH: [32][RSW]
 	static constexpr int oG = oA + NH * 32 * RSW;             // dL/dy of the tile [32][RSG]
 	static constexpr int HALVES = oG + 32 * RSG;
-	static constexpr int BYTES = HALVES * 2 + 4 * 4;           // + per-wave loss
+	static constexpr int BYTES = HALVES * 2 + WAVES * 4;       // + per-wave loss
 	static constexpr int N_MLP = W * IN + (NH - 1) * W * W + 16 * W;
 	static_assert(oWh % 8 == 0 && oWo % 8 == 0 && oX % 8 == 0 && oA % 8 == 0 && oG % 8 == 0, "16-byte alignment");
 };
@@ -64,10 +67,11 @@ __device__ __forceinline__ h4 tile_act(f4 v) {
 }
 
 template <int W, int IN, int NH, Act ACT, bool EXT_DOUT>
-__global__ __launch_bounds__(256, 1) void k_mlp_tile_train(const TileTrainArgs a) {
+__global__ __launch_bounds__((W == 128 ? 512 : 256), 1) void k_mlp_tile_train(const TileTrainArgs a) {
 	using L = TileLayout<W, IN, NH>;
 	constexpr int MTW = L::MTW, KT0 = L::KT0, RS0 = L::RS0, RSW = L::RSW, RSG = L::RSG;
-	constexpr int NTW = L::MT / 4;  // Wout column tiles per wave (= MTW)
+	constexpr int WAVES = L::WAVES, NTHR = L::NTHR;
+	constexpr int NTW = L::MT / WAVES;  // Wout column tiles per wave (= MTW)
 	extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
 	const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 	const int c = lane & 15, q = lane >> 4;
@@ -77,23 +81,23 @@ __global__ __launch_bounds__(256, 1) void k_mlp_tile_train(const TileTrainArgs a
 	// ---- weights -> LDS (rows padded; first-layer columns [IN, KP0) zero) ----
 	{
 		const _Float16* p = a.params;
-		for (int idx = tid; idx < W * (L::KP0 / 8); idx += 256) {
+		for (int idx = tid; idx < W * (L::KP0 / 8); idx += NTHR) {
 			const int r = idx / (L::KP0 / 8), c8 = idx % (L::KP0 / 8);
 			*(h8*)(smem + L::oW0 + r * RS0 + 8 * c8) = 8 * c8 < IN ? *(const h8*)(p + (size_t)r * IN + 8 * c8) : zero8();
 		}
 		p += W * IN;
-		for (int idx = tid; idx < (NH - 1) * W * (W / 8); idx += 256) {
+		for (int idx = tid; idx < (NH - 1) * W * (W / 8); idx += NTHR) {
 			const int r = idx / (W / 8), c8 = idx % (W / 8);  // r over all hidden rows
 			*(h8*)(smem + L::oWh + r * RSW + 8 * c8) = *(const h8*)(p + (size_t)r * W + 8 * c8);
 		}
 		p += (NH - 1) * W * W;
-		for (int idx = tid; idx < 16 * (W / 8); idx += 256) {
+		for (int idx = tid; idx < 16 * (W / 8); idx += NTHR) {
 			const int r = idx / (W / 8), c8 = idx % (W / 8);
 			*(h8*)(smem + L::oWo + r * RSW + 8 * c8) = *(const h8*)(p + (size_t)r * W + 8 * c8);
 		}
 		// zero the padded input columns of slot 0 once (the input loads never write them)
 		if (L::KP0 > IN)
-			for (int idx = tid; idx < 32 * (L::KP0 - IN); idx += 256)
+			for (int idx = tid; idx < 32 * (L::KP0 - IN); idx += NTHR)
 				smem[L::oX + (idx / (L::KP0 - IN)) * RS0 + IN + idx % (L::KP0 - IN)] = (_Float16)0.0f;
 	}
 	auto Wm = [&](int m) -> const _Float16* { return m == 0 ? smem + L::oW0 : smem + L::oWh + (m - 1) * W * RSW; };
@@ -118,14 +122,14 @@ __global__ __launch_bounds__(256, 1) void k_mlp_tile_train(const TileTrainArgs a
 	float loss = 0.0f;
 
 	// input rows of a tile: IN/8 16-byte vectors per sample
-	constexpr int XV = 32 * IN / 8, XPT = (XV + 255) / 256;
+	constexpr int XV = 32 * IN / 8, XPT = (XV + NTHR - 1) / NTHR;
 	const uint32_t n_tiles = a.B / 32;
 	uint32_t tile = blockIdx.x;
 	h8 xr[XPT];
 	auto load_x = [&](uint32_t t) {
 #pragma unroll
 		for (int j = 0; j < XPT; ++j) {
-			const int idx = tid + 256 * j;
+			const int idx = tid + NTHR * j;
 			if (idx < XV) xr[j] = *(const h8*)(a.enc + ((size_t)t * 32 + idx / (IN / 8)) * IN + 8 * (idx % (IN / 8)));
 		}
 	};
@@ -137,7 +141,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_tile_train(const TileTrainArgs a
 		// ---- input tile -> slot 0; prefetch the next tile's rows ----
 #pragma unroll
 		for (int j = 0; j < XPT; ++j) {
-			const int idx = tid + 256 * j;
+			const int idx = tid + NTHR * j;
 			if (idx < XV) *(h8*)(slot(0) + (idx / (IN / 8)) * RS0 + 8 * (idx % (IN / 8))) = xr[j];
 		}
 		if (tile + gridDim.x < n_tiles) load_x(tile + gridDim.x);
@@ -293,7 +297,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_tile_train(const TileTrainArgs a
 					for (int tau = 0; tau < 2; ++tau) *(h4*)(dst + (16 * tau + c) * RSW + 16 * (wave * MTW + i) + 4 * q) = dl[i][tau];
 				__syncthreads();
 			} else if (a.dldenc) {
-				for (int t = wave; t < KT0; t += 4) {
+				for (int t = wave; t < KT0; t += WAVES) {
 					f4 v[2] = {fz, fz};
 #pragma unroll
 					for (int s = 0; s < W / 32; ++s) {
@@ -345,7 +349,11 @@ __global__ __launch_bounds__(256, 1) void k_mlp_tile_train(const TileTrainArgs a
 	for (int off = 32; off > 0; off >>= 1) loss += __shfl_xor(loss, off);
 	if (lane == 0) wloss[wave] = loss;
 	__syncthreads();
-	if (tid == 0) a.loss_partial[blockIdx.x] = (wloss[0] + wloss[1]) + (wloss[2] + wloss[3]);
+	if (tid == 0) {
+		float l = 0.0f;
+		for (int w = 0; w < WAVES; ++w) l += wloss[w];
+		a.loss_partial[blockIdx.x] = l;
+	}
 }
 
 // ------------------------------------------------------------------------------------------
@@ -381,7 +389,7 @@ static void tile_launch(hipStream_t st, uint32_t blocks, const TileTrainArgs& a)
 		                                   (int)L::BYTES));
 		attr = true;
 	}
-	hipLaunchKernelGGL((k_mlp_tile_train<W, IN, NH, ACT, EXT>), dim3(blocks), dim3(256), L::BYTES, st, a);
+	hipLaunchKernelGGL((k_mlp_tile_train<W, IN, NH, ACT, EXT>), dim3(blocks), dim3(L::NTHR), L::BYTES, st, a);
 }
 
 uint32_t tile_train_blocks(uint32_t B) { return std::max(1u, std::min(256u, B / 32)); }

@@ -845,7 +845,7 @@ void TrainerHost::training_step_overlapped(hipStream_t st, uint32_t B, const flo
 	ep.factor_step = adam_step;
 	TCNN_CHECK(n_mlp % 4 == 0, "network parameter count must be a multiple of 4");
 	m.grid_backward(st, ws, B, input, &ep);
-	if (run_optimizer) ftable_valid = adam_step;
+	if (run_optimizer) ftable_valid = std::max(ftable_valid, adam_step);
 	GridEncodingHost& g = *m.grid;
 	if (run_optimizer) {
 		// binned levels: Adam applied by the accumulate pass; LDS levels: Adam summing their slabs
@@ -977,14 +977,17 @@ AdamArgs TrainerHost::adam_args_table(hipStream_t st, uint32_t upto, uint32_t re
 		ftable_b2 = adam.beta2;
 	}
 	if (std::max(upto, reserve) > ftable_cap) {
-		ftable_cap = std::max(std::max(upto, reserve), std::max(1024u, 2 * ftable_cap));
+		ftable_cap = std::max((std::max(upto, reserve) + 1023u) / 1024u * 1024u, std::max(1024u, 2 * ftable_cap));
 		TCNN_HIP_CHECK(hipStreamSynchronize(st));  // the old table may still be read by queued work
 		d_ftable.reserve((size_t)ftable_cap * 4);
 		ftable_valid = 0;
 	}
 	if (upto > ftable_valid) {
-		launch_fill_bias_factors(st, a, d_ftable.as<float>(), ftable_valid, upto);
-		ftable_valid = upto;
+		// the factors depend only on t and the betas: fill 1024 steps ahead, so the fill kernel runs
+		// once per 1024 steps instead of once per step
+		const uint32_t ahead = std::min(ftable_cap, (upto + 1023u) / 1024u * 1024u);
+		launch_fill_bias_factors(st, a, d_ftable.as<float>(), ftable_valid, ahead);
+		ftable_valid = ahead;
 	}
 	a.factor_table = d_ftable.as<float>();
 	a.factor_n = ftable_valid;
