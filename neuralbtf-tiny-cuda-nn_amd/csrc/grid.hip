@@ -93,6 +93,41 @@ __global__ __launch_bounds__(256) void k_grid_fwd(uint32_t B, const float* __res
 	}
 }
 
+// AoS forward for F = 2 (the trainer's encoding pass of the tile / layer-wise engines): one
+// workgroup = 64 consecutive points x all levels; wave w encodes levels w, w+4, ... for the 64
+// points, so a level is wave-uniform (scalar LevelInfo loads, no divergence between dense and
+// hashed index math, and the 64 lanes' gathers of a coarse level share cache lines), and the
+// [64][L] half2 tile is transposed through LDS into whole 16-byte output rows.
+template <uint32_t D, HashType H>
+__global__ __launch_bounds__(256) void k_grid_fwd_aos_f2(uint32_t B, const float* __restrict__ pos, uint32_t pstride,
+                                                         const uint32_t* __restrict__ table, _Float16* __restrict__ out,
+                                                         uint32_t out_stride, const LevelInfo* __restrict__ levels, uint32_t hash_grid,
+                                                         uint32_t interp_u, const GridOpts o, uint32_t L) {
+	__shared__ uint32_t tile[64 * 65];  // [point][level], row stride 65 (conflict-free column writes)
+	const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+	const uint32_t i = blockIdx.x * 64 + lane;
+	const bool valid = i < B;
+	const Interp interp = (Interp)interp_u;
+	float x[D];
+#pragma unroll
+	for (uint32_t d = 0; d < D; ++d) x[d] = valid ? pos[(size_t)i * pstride + d] : 0.0f;
+	for (uint32_t level = wave; level < L; level += 4) {
+		const LevelInfo li = levels[level];
+		h2 r = {(_Float16)0.0f, (_Float16)0.0f};
+		if (valid && !(o.active && (float)level >= grid_max_level(o, i, 2) + 1e-3f))  // masked: 0 (grid.h:75-91)
+			r = encode_level_f2<D, H>(table, li, hash_grid != 0, interp, x);
+		tile[lane * 65 + level] = __builtin_bit_cast(uint32_t, r);
+	}
+	__syncthreads();
+	const uint32_t row2 = out_stride / 2;  // half2 columns per output row (grid features + zero padding)
+	uint32_t* o32 = (uint32_t*)out;
+	for (uint32_t idx = threadIdx.x; idx < 64 * row2; idx += 256) {
+		const uint32_t p = idx / row2, c2 = idx % row2;
+		const uint32_t ip = blockIdx.x * 64 + p;
+		if (ip < B) o32[(size_t)ip * row2 + c2] = c2 < L ? tile[p * 65 + c2] : 0u;
+	}
+}
+
 template <uint32_t D, uint32_t F>
 static void grid_fwd_h(hipStream_t st, HashType h, dim3 g, uint32_t B, const float* pos, uint32_t ps, const _Float16* t,
                        _Float16* o, uint32_t soa, uint32_t os, const LevelInfo* lv, uint32_t hg, uint32_t in, const GridOpts& go) {
@@ -121,6 +156,25 @@ void launch_grid_fwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_
                      const float* pos, uint32_t pos_stride, const void* table16, void* out16, bool soa,
                      uint32_t out_stride, const LevelInfo* levels, bool hash_grid, Interp interp, const GridOpts& go) {
 	if (B == 0) return;
+	if (!soa && F == 2 && L <= 64 && out_stride % 2 == 0 && interp != Interp::Nearest) {
+		const dim3 g2(div_round_up(B, 64));
+		const uint32_t* t32 = (const uint32_t*)table16;
+		_Float16* o16 = (_Float16*)out16;
+		const uint32_t hg = hash_grid ? 1u : 0u, in = (uint32_t)interp;
+#define AOS2(DD)                                                                                                                   \
+	switch (h) {                                                                                                                   \
+		case HashType::Prime: hipLaunchKernelGGL((k_grid_fwd_aos_f2<DD, HashType::Prime>), g2, dim3(256), 0, st, B, pos, pos_stride, t32, o16, out_stride, levels, hg, in, go, L); break; \
+		case HashType::ReversedPrime: hipLaunchKernelGGL((k_grid_fwd_aos_f2<DD, HashType::ReversedPrime>), g2, dim3(256), 0, st, B, pos, pos_stride, t32, o16, out_stride, levels, hg, in, go, L); break; \
+		default: hipLaunchKernelGGL((k_grid_fwd_aos_f2<DD, HashType::CoherentPrime>), g2, dim3(256), 0, st, B, pos, pos_stride, t32, o16, out_stride, levels, hg, in, go, L); break; \
+	}
+		if (D == 2) { AOS2(2) }
+		else if (D == 3) { AOS2(3) }
+		else if (D == 4) { AOS2(4) }
+		else throw std::runtime_error("GridEncoding: number of input dims must be 2, 3 or 4");
+#undef AOS2
+		TCNN_HIP_CHECK(hipGetLastError());
+		return;
+	}
 	const dim3 g = soa ? dim3(div_round_up(B, 256), L) : dim3(div_round_up(B * L, 256), 1);
 	GridOpts gol = go;
 	gol.n_levels = L;  // carries L to the AoS mapping

@@ -115,7 +115,7 @@ def test_trainer_stochastic_interpolation_step(torch_mod):
     cfg = copy.deepcopy(CONFIG_HASH)
     cfg["encoding"]["stochastic_interpolation"] = True
     t = Trainer(2, 3, cfg, seed=1337)
-    assert t.engine == "layered", t.engine
+    assert t.engine == "fused", t.engine  # the tile engine (the register-resident kernel takes no grid options)
     om = O.OracleModel(cfg, 2, 3, seed=1337)
     B = 1024
     pos, tgt = make_batch(B)
@@ -135,7 +135,7 @@ def test_trainer_max_level_switches_engine(torch_mod):
     t = Trainer(2, 3, CONFIG_HASH, seed=1337)
     assert t.engine == "fused"
     L.check(L.lib().tcnn_trainer_set_max_level(t.h, 0.5))
-    assert t.engine == "layered"
+    assert t.engine == "fused"  # now the tile engine: encoding pass + grid backward take the mask
     B = 1024
     pos, tgt = make_batch(B)
     for _ in range(3):
