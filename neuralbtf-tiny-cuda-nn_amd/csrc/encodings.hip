@@ -163,7 +163,7 @@ __global__ __launch_bounds__(256) void k_identity_fwd(uint32_t B, uint32_t D, fl
 	const uint32_t fan = D + n_pad;
 	if (t >= B * fan) return;
 	const uint32_t i = t / fan, j = t % fan;
-	out[(size_t)i * out_stride + j] = j < D ? (_Float16)__builtin_fmaf(x[(size_t)i * x_stride + j], scale, offset) : (_Float16)1.0f;
+	out[(size_t)i * out_stride + j] = j < D ? f16_rn(__builtin_fmaf(x[(size_t)i * x_stride + j], scale, offset)) : (_Float16)1.0f;
 }
 
 // identity_backward (identity.h:68-85): dL/dx = (T)(dL/dy * scale) -- stored as fp32 here.

@@ -165,7 +165,10 @@ __device__ __forceinline__ h2 encode_level_f2(const uint32_t* __restrict__ table
 			if ((c & (1u << d)) == 0) { w *= 1.0f - pos[d]; local[d] = pg[d]; }
 			else { w *= pos[d]; local[d] = pg[d] + 1; }
 		}
-		w16[c] = f16_rn(w);
+		// plain conversion: the compiler emits v_cvt_f16_f32 here (no fused mix rounding; pinned for
+		// every kernel by tests/test_isa_rounding.py), and the f16_rn barrier costs the fused kernel
+		// ~10% by serialising the weight / gather schedule
+		w16[c] = (_Float16)w;
 		v[c] = table_u32[li.offset + grid_index<D, H>(hash_grid, li.size, li.res, local)];
 	}
 	h2 r = {(_Float16)0.0f, (_Float16)0.0f};
