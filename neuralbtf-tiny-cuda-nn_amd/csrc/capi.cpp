@@ -451,7 +451,7 @@ int tcnn_debug_fused_phase_cycles(tcnn_trainer* t, void* stream, uint32_t n, con
 		// run one normal step first so the workspace is sized
 		tr.training_step(st, n, input, target, false);
 		const uint32_t nb = fused_train_n_blocks(64, 32, 2, 2, tr.n_output_dims, false, n);
-		constexpr size_t WV = 4;  // waves per workgroup of the fused kernel
+		const size_t WV = fused_train_waves();  // waves per workgroup of the fused kernel
 		DevBuf prof;
 		prof.reserve((size_t)nb * WV * 8 * 8);
 		TCNN_HIP_CHECK(hipMemsetAsync(prof.p, 0, (size_t)nb * WV * 8 * 8, st));

@@ -72,11 +72,14 @@ static uint32_t device_cu_count() {
 	return cached;
 }
 
+uint32_t fused_train_waves() { return FUSED_WAVES; }
+
 uint32_t fused_train_n_blocks(uint32_t W, uint32_t IN, uint32_t NH, uint32_t D, uint32_t dims, bool ext_dout, uint32_t B) {
 	const uint32_t n_cu = device_cu_count();
-	// 4 waves x 32 samples per workgroup iteration; 2 workgroups per CU, persistent.
-	const uint32_t nb = div_round_up(B, 128);
-	return nb < 2 * n_cu ? nb : 2 * n_cu;
+	// FUSED_WAVES waves x 32 samples per workgroup iteration; 8 waves per CU, persistent.
+	const uint32_t nb = div_round_up(B, 32u * FUSED_WAVES);
+	const uint32_t cap = (8u / FUSED_WAVES) * n_cu;
+	return nb < cap ? nb : cap;
 }
 
 template <int W, int IN, int NH, uint32_t D, HashType H, Act A, bool EXT>
@@ -87,7 +90,7 @@ static void launch_fused_e(hipStream_t st, const FusedTrainArgs& args, uint32_t 
 		TCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k_fused_train_grid<W, IN, NH, D, H, A, EXT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
 		attr = true;
 	}
-	hipLaunchKernelGGL((k_fused_train_grid<W, IN, NH, D, H, A, EXT>), dim3(n_blocks), dim3(256), bytes, st, args);
+	hipLaunchKernelGGL((k_fused_train_grid<W, IN, NH, D, H, A, EXT>), dim3(n_blocks), dim3(64 * FUSED_WAVES), bytes, st, args);
 	TCNN_HIP_CHECK(hipGetLastError());
 }
 
@@ -216,7 +219,7 @@ void launch_fused_train_profile(hipStream_t st, uint32_t B, uint32_t dims, const
 		                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)K::BYTES));
 		attr = true;
 	}
-	hipLaunchKernelGGL((k_fused_train_grid<64, 32, 2, 2, HashType::CoherentPrime, Act::ReLU, false, true>), dim3(n_blocks), dim3(256),
+	hipLaunchKernelGGL((k_fused_train_grid<64, 32, 2, 2, HashType::CoherentPrime, Act::ReLU, false, true>), dim3(n_blocks), dim3(64 * FUSED_WAVES),
 	                   K::BYTES, st, a);
 	TCNN_HIP_CHECK(hipGetLastError());
 }

@@ -131,6 +131,7 @@ struct GridBwdEpilogue {
 // Returns false if no fused kernel exists for this shape.
 bool fused_train_supported(uint32_t W, uint32_t IN, uint32_t NH, uint32_t D, uint32_t F, uint32_t OUTP, int act, HashType h);
 // Workgroups the fused launch uses (= partial slabs it writes) for this shape and batch.
+uint32_t fused_train_waves();  // waves per workgroup of k_fused_train_grid
 uint32_t fused_train_n_blocks(uint32_t W, uint32_t IN, uint32_t NH, uint32_t D, uint32_t dims, bool ext_dout, uint32_t B);
 void launch_fused_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, uint32_t D, HashType h, int act,
                         uint32_t B, uint32_t dims, float loss_scale, const void* params16, const void* table16,

@@ -117,11 +117,20 @@ struct FusedLayout {
 	static_assert(oWh % 8 == 0 && oWo % 8 == 0 && oStage % 8 == 0, "16B alignment");
 };
 
-// Register-gather kernel (any D): 4 waves per workgroup, dynamic LDS.
+// Waves per workgroup of the register-gather kernel (2 waves per SIMD either way, the register
+// limit). 8 waves = one workgroup per CU halves the network-gradient partial slabs (256 x 28 KB for
+// config_hash instead of 512) but measured slower: fused kernel 66.6 -> 68.7 us, step 7,425 ->
+// 7,363 steps/s (the 8-wave slab reduction at the end is longer than the traffic it saves).
+#ifndef TCNN_FUSED_WAVES
+#define TCNN_FUSED_WAVES 4
+#endif
+constexpr int FUSED_WAVES = TCNN_FUSED_WAVES;
+
+// Register-gather kernel (any D): FUSED_WAVES waves per workgroup, dynamic LDS.
 template <int W, int IN, int NH>
 struct RegKernelLayout {
 	using L = FusedLayout<W, IN, NH>;
-	static constexpr int WAVES = 4;
+	static constexpr int WAVES = FUSED_WAVES;
 	static constexpr int oEnd = L::oStage + WAVES * 2 * L::STAGE;
 	static constexpr int LVL_BYTES = oEnd * 2;          // LevelInfo table (byte offset)
 	static constexpr int BYTES_MAIN = LVL_BYTES + (int)MAX_LEVELS * 16;
@@ -477,10 +486,10 @@ __device__ __forceinline__ void block_reduce_wgrad(WgradAcc<W, IN, NH>& acc, flo
 	}
 }
 
-// Register-gather variant, any D: one workgroup = 4 waves, each wave runs 32-sample slices in a
-// grid-stride loop; the grid encoding's gathers go straight to registers.
+// Register-gather variant, any D: one workgroup = FUSED_WAVES waves, each wave runs 32-sample
+// slices in a grid-stride loop; the grid encoding's gathers go straight to registers.
 template <int W, int IN, int NH, uint32_t D, HashType H, Act ACT, bool EXT_DOUT, bool PROF = false>
-__global__ __launch_bounds__(256, 2) void k_fused_train_grid(const FusedTrainArgs a) {
+__global__ __launch_bounds__(64 * FUSED_WAVES, 8 / FUSED_WAVES) void k_fused_train_grid(const FusedTrainArgs a) {
 	using L = FusedLayout<W, IN, NH>;
 	using RL = RegKernelLayout<W, IN, NH>;
 	constexpr int NTI = L::NTI, KI = L::KI;
@@ -490,9 +499,10 @@ __global__ __launch_bounds__(256, 2) void k_fused_train_grid(const FusedTrainArg
 	const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 	const int c = lane & 15, q = lane >> 4;
 
-	copy_image_to_lds(smem, a.wimage, L::oStage, tid, 256);
+	constexpr int NTHR = 64 * FUSED_WAVES;
+	copy_image_to_lds(smem, a.wimage, L::oStage, tid, NTHR);
 	LevelInfo* sLvl = (LevelInfo*)((char*)smem + RL::LVL_BYTES);
-	for (int l = tid; l < NLVL; l += 256) sLvl[l] = a.levels[l];
+	for (int l = tid; l < NLVL; l += NTHR) sLvl[l] = a.levels[l];
 	__syncthreads();
 
 	_Float16* bufA = smem + L::oStage + wave * 2 * L::STAGE;
@@ -506,7 +516,7 @@ __global__ __launch_bounds__(256, 2) void k_fused_train_grid(const FusedTrainArg
 	unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 	unsigned long long t0 = 0, t1 = 0;
 	if constexpr (PROF) t0 = stamp();
-	for (uint32_t chunk = blockIdx.x * 4 + wave; chunk < n_chunks; chunk += gridDim.x * 4) {
+	for (uint32_t chunk = blockIdx.x * FUSED_WAVES + wave; chunk < n_chunks; chunk += gridDim.x * FUSED_WAVES) {
 		const uint32_t base = chunk * 32;
 		h4 xt[2][NTI];
 		h4 Gext[2];
@@ -547,12 +557,12 @@ __global__ __launch_bounds__(256, 2) void k_fused_train_grid(const FusedTrainArg
 	}
 	if constexpr (PROF) {
 		if (lane == 0) {
-			unsigned long long* o = a.prof + (size_t)(blockIdx.x * 4 + wave) * 8;
+			unsigned long long* o = a.prof + (size_t)(blockIdx.x * FUSED_WAVES + wave) * 8;
 			for (int k = 0; k < 6; ++k) o[k] = ph[k];
 		}
 	}
 	__syncthreads();
-	block_reduce_wgrad<W, IN, NH, 4>(acc, (float*)smem, a, tid, wave, lane);
+	block_reduce_wgrad<W, IN, NH, FUSED_WAVES>(acc, (float*)smem, a, tid, wave, lane);
 }
 
 
@@ -574,7 +584,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_infer(uint32_t B, const _Float16
 	const _Float16* sWo = smem + L::oWo;
 	const f4 fz = {0.0f, 0.0f, 0.0f, 0.0f};
 	const uint32_t n_chunks = B / 16;
-	for (uint32_t chunk = blockIdx.x * 4 + wave; chunk < n_chunks; chunk += gridDim.x * 4) {
+	for (uint32_t chunk = blockIdx.x * 4 + wave; chunk < n_chunks; chunk += gridDim.x * 4) {  // 4 waves (256 threads)
 		const uint32_t i = chunk * 16 + c;
 		h4 xt[NTI];
 #pragma unroll

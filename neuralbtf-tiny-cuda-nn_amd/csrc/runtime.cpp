@@ -88,6 +88,8 @@ void DevBuf::reserve(size_t n) {
 	if (n == 0) n = 16;
 	TCNN_HIP_CHECK(hipMalloc(&p, n));
 	bytes = n;
+	static const bool poison = std::getenv("TCNN_DEBUG_POISON") != nullptr;  // NaN-fill new buffers (finds reads of unwritten memory)
+	if (poison) TCNN_HIP_CHECK(hipMemset(p, 0xff, n));
 }
 
 bool ieq(const std::string& a, const std::string& b) {

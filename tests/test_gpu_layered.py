@@ -16,7 +16,7 @@ import json
 import numpy as np
 import pytest
 
-from helpers import CONFIG_HASH, CONFIG_ONEBLOB, make_batch, rel_err, trainer_arrays
+from helpers import CONFIG_HASH, CONFIG_ONEBLOB, assert_within_fp16_ulps, make_batch, rel_err, trainer_arrays
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -125,7 +125,7 @@ def test_layered_inference_matches_oracle(torch_mod, name):
     pos, _ = make_batch(1024, seed=3)
     out = t.inference(torch.from_numpy(pos).cuda()).cpu().numpy()
     ref = O.h2f(om.inference(pos, n_threads=4))[:, :3]
-    np.testing.assert_allclose(out, ref, rtol=2e-3, atol=2e-4)
+    assert_within_fp16_ulps(out, ref)
 
 
 @pytest.mark.parametrize("name", ["oneblob_as_file_w128_h5", "hashgrid_w128_h4", "oneblob_w64_h5"])
@@ -196,7 +196,7 @@ def test_create_network_identity_module(torch_mod):
     params16 = p16.cpu().numpy().view(np.uint16)
     enc = O.identity_fwd(x, n_pad=13)
     outr, hidden = O.mlp_fwd(64, 16, 2, 16, params16, enc, input_soa=False)
-    np.testing.assert_allclose(O.h2f(out.cpu().numpy().view(np.uint16)), O.h2f(outr), rtol=2e-3, atol=2e-4)
+    assert_within_fp16_ulps(O.h2f(out.cpu().numpy().view(np.uint16)), O.h2f(outr))
     wg, denc = O.mlp_bwd(64, 16, 2, 16, params16, enc, hidden, dout16.cpu().numpy().view(np.uint16), input_soa=False)
     assert rel_err(grad.float().cpu().numpy(), wg) <= 1e-3
     # identity_backward: dL/dx = (half)(dL/denc * scale)

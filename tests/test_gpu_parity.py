@@ -12,7 +12,7 @@ import json
 import numpy as np
 import pytest
 
-from helpers import CONFIG_HASH, make_batch, rel_err, trainer_arrays
+from helpers import CONFIG_HASH, assert_within_fp16_ulps, make_batch, rel_err, trainer_arrays
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -97,15 +97,25 @@ def test_adam_step_matches_oracle_on_same_gradients(torch_mod):
     assert rel_err(a["w32"], w32) <= 1e-5
 
 
-def test_inference_matches_oracle(torch_mod):
+@pytest.mark.parametrize("grid_gain", [1.0, 5000.0])
+def test_inference_matches_oracle(torch_mod, grid_gain):
+    """Trainer inference (grid forward + the fused inference kernel) vs the oracle, at the init
+    scale and with the grid parameters scaled to O(1) outputs, on a batch that is not a multiple of
+    the inference kernel's 64-sample workgroup."""
     torch = torch_mod
     from tinycudann import Trainer
     t = Trainer(2, 3, CONFIG_HASH, seed=1337)
     om = O.OracleModel(CONFIG_HASH, 2, 3, seed=1337)
-    pos, _ = make_batch(2048, seed=3)
+    if grid_gain != 1.0:
+        w = om.w32.copy()
+        w[om.n_mlp_params:] *= grid_gain
+        t.set_params_full_precision(w)
+        om.w32[:] = w
+        om.w16[:] = O.f2h(w)
+    pos, _ = make_batch(2048 + 96, seed=3)
     out = t.inference(torch.from_numpy(pos).cuda()).cpu().numpy()
     ref = O.h2f(om.inference(pos))[:, :3]
-    np.testing.assert_allclose(out, ref, rtol=2e-3, atol=2e-4)
+    assert_within_fp16_ulps(out, ref)
 
 
 def test_training_trajectory_tracks_oracle(torch_mod):
@@ -156,7 +166,7 @@ def test_module_backward_matches_oracle(torch_mod):
     nm = O.mlp_n_params(64, 32, 2, 16)
     encv = O.grid_fwd(g, pos, params16[nm:])
     outr, hidden = O.mlp_fwd(64, 32, 2, 16, params16[:nm], encv)
-    np.testing.assert_allclose(O.h2f(out.cpu().numpy().view(np.uint16)), O.h2f(outr), rtol=2e-3, atol=2e-4)
+    assert_within_fp16_ulps(O.h2f(out.cpu().numpy().view(np.uint16)), O.h2f(outr))
     wg, denc = O.mlp_bwd(64, 32, 2, 16, params16[:nm], encv, hidden, dout16.cpu().numpy().view(np.uint16))
     gg = O.grid_bwd(g, pos, denc)
     ref = np.concatenate([wg, gg])
