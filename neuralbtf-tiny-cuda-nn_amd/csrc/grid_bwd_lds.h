@@ -69,6 +69,97 @@ __device__ __forceinline__ uint32_t level_index(bool hash_grid, uint32_t size, u
 	}
 }
 
+// One point's corner updates of one work item into the LDS accumulators (reference
+// kernel_grid_backward's per-level body, grid.h:246-317): dy = the point's dL/dy already multiplied by
+// the item's fixed-point scale.
+template <uint32_t D, uint32_t F, HashType H, int KIND, int MODE, bool OPTS>
+__device__ __forceinline__ void accum_point(const float (&x)[D], const float (&dy)[F], uint32_t i, uint32_t level, uint32_t B,
+                                            const LevelInfo& li, bool hash_grid, Interp interp, uint32_t begin, uint32_t len,
+                                            uint32_t f0, uint32_t nf, int* acc, const GridOpts& o) {
+	float p[D];
+	uint32_t pg[D];
+#pragma unroll
+	for (uint32_t d = 0; d < D; ++d) pos_fract(x[d], li.scale, interp, p[d], pg[d]);
+	const bool nearest = interp == Interp::Nearest;
+	// stochastic interpolation (grid.h:284-298): one corner, chosen per (point, level), weight 1
+	const bool single = nearest || (OPTS && o.stochastic);
+	uint32_t cbits = 0;
+	if (single && !nearest) {
+		const float smp = random_val_1337(i + level * B);
+#pragma unroll
+		for (uint32_t d = 0; d < D; ++d) cbits |= (smp >= p[d] ? 0u : 1u) << d;
+	}
+#pragma unroll
+	for (uint32_t c0 = 0; c0 < (1u << D); ++c0) {
+		if (single && c0 > 0) break;
+		const uint32_t c = single ? cbits : c0;
+		float w = 1.0f;
+		uint32_t local[D];
+#pragma unroll
+		for (uint32_t d = 0; d < D; ++d) {
+			if ((c & (1u << d)) == 0) { w *= 1.0f - p[d]; local[d] = pg[d]; }
+			else { w *= p[d]; local[d] = pg[d] + 1; }
+		}
+		const float wh = single ? 1.0f : (float)f16_rn(w);
+		const uint32_t rel = level_index<D, H, KIND>(hash_grid, li.size, li.res, local) - begin;
+		if constexpr (KIND == IDX_GENERIC) {  // entry slices may not cover the level
+			if (rel >= len) continue;
+		}
+		if constexpr (MODE == 0) {
+			const int a = __float2int_rn(wh * dy[0]);
+			const int b = __float2int_rn(wh * dy[1]);
+			const unsigned long long pk = (unsigned long long)(((long long)b << 32) + (long long)a);
+			__hip_atomic_fetch_add((unsigned long long*)acc + rel, pk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+		} else {
+#pragma unroll
+			for (uint32_t f = 0; f < F; ++f) {
+				if constexpr (MODE == 1) {
+					if (f - f0 < nf) lds_add_i32(&acc[rel * nf + (f - f0)], wh * dy[f]);
+				} else {
+					lds_add_i32(&acc[rel * F + f], wh * dy[f]);
+				}
+			}
+		}
+	}
+}
+
+// Register-resident variant (D == 2, F <= 2, no grid options): the chunk's dL/dy bits were loaded
+// into dyb (GRID_BWD_PR points per thread, point i0 + threadIdx.x + p * blockDim.x in slot p) for the
+// scale pre-pass and are reused here; positions stream in batches of 8 with the next batch in flight.
+constexpr uint32_t GRID_BWD_PR = 32;
+template <uint32_t D, uint32_t F, HashType H, int KIND, int MODE>
+__device__ __forceinline__ void grid_bwd_points_regs(const uint32_t (&dyb)[GRID_BWD_PR], uint32_t B, const float* __restrict__ pos,
+                                                     uint32_t pstride, uint32_t level, const LevelInfo& li, bool hash_grid,
+                                                     Interp interp, uint32_t begin, uint32_t len, uint32_t f0, uint32_t nf,
+                                                     uint32_t i0, uint32_t i1, float scale, int* acc, const GridOpts& o) {
+	constexpr uint32_t U = 8, NB = GRID_BWD_PR / U;
+	float xs[2][U][D];
+	auto load_pos = [&](uint32_t k, float (&dst)[U][D]) {
+#pragma unroll
+		for (uint32_t u = 0; u < U; ++u) {
+			const uint32_t i = i0 + threadIdx.x + (k * U + u) * blockDim.x;
+#pragma unroll
+			for (uint32_t d = 0; d < D; ++d) dst[u][d] = i < i1 ? pos[(size_t)i * pstride + d] : 0.0f;
+		}
+	};
+	load_pos(0, xs[0]);
+#pragma unroll
+	for (uint32_t k = 0; k < NB; ++k) {
+		if (i0 + threadIdx.x + k * U * blockDim.x >= i1) break;
+		if (k + 1 < NB) load_pos(k + 1, xs[(k + 1) & 1]);
+#pragma unroll
+		for (uint32_t u = 0; u < U; ++u) {
+			const uint32_t p = k * U + u;
+			const uint32_t i = i0 + threadIdx.x + p * blockDim.x;
+			if (i >= i1) break;
+			float dy[F];
+#pragma unroll
+			for (uint32_t f = 0; f < F; ++f) dy[f] = dy_bits_feature(dyb[p], f) * scale;
+			accum_point<D, F, H, KIND, MODE, false>(xs[k & 1][u], dy, i, level, B, li, hash_grid, interp, begin, len, f0, nf, acc, o);
+		}
+	}
+}
+
 // MODE: 0 = F == 2, both features as one packed int64 (two int32 halves) per entry -> one
 // ds_add_u64 per corner; 1 = the feature group [f0, f0 + nf) per entry (nf < F), ds_add_u32;
 // 2 = all F features, ds_add_u32.
@@ -106,51 +197,8 @@ __device__ __forceinline__ void grid_bwd_points(int layout, uint32_t B, const fl
 #pragma unroll
 		for (uint32_t u = 0; u < U; ++u) {
 			if (base + u * blockDim.x >= i1) break;
-			float p[D];
-			uint32_t pg[D];
-#pragma unroll
-			for (uint32_t d = 0; d < D; ++d) pos_fract(xs[u][d], li.scale, interp, p[d], pg[d]);
-			const bool nearest = interp == Interp::Nearest;
-			// stochastic interpolation (grid.h:284-298): one corner, chosen per (point, level), weight 1
-			const bool single = nearest || (OPTS && o.stochastic);
-			uint32_t cbits = 0;
-			if (single && !nearest) {
-				const float smp = random_val_1337(base + u * blockDim.x + level * B);
-#pragma unroll
-				for (uint32_t d = 0; d < D; ++d) cbits |= (smp >= p[d] ? 0u : 1u) << d;
-			}
-#pragma unroll
-			for (uint32_t c0 = 0; c0 < (1u << D); ++c0) {
-				if (single && c0 > 0) break;
-				const uint32_t c = single ? cbits : c0;
-				float w = 1.0f;
-				uint32_t local[D];
-#pragma unroll
-				for (uint32_t d = 0; d < D; ++d) {
-					if ((c & (1u << d)) == 0) { w *= 1.0f - p[d]; local[d] = pg[d]; }
-					else { w *= p[d]; local[d] = pg[d] + 1; }
-				}
-				const float wh = single ? 1.0f : (float)f16_rn(w);
-				const uint32_t rel = level_index<D, H, KIND>(hash_grid, li.size, li.res, local) - begin;
-				if constexpr (KIND == IDX_GENERIC) {  // entry slices may not cover the level
-					if (rel >= len) continue;
-				}
-				if constexpr (MODE == 0) {
-					const int a = __float2int_rn(wh * dy[u][0]);
-					const int b = __float2int_rn(wh * dy[u][1]);
-					const unsigned long long pk = (unsigned long long)(((long long)b << 32) + (long long)a);
-					__hip_atomic_fetch_add((unsigned long long*)acc + rel, pk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-				} else {
-#pragma unroll
-					for (uint32_t f = 0; f < F; ++f) {
-						if constexpr (MODE == 1) {
-							if (f - f0 < nf) lds_add_i32(&acc[rel * nf + (f - f0)], wh * dy[u][f]);
-						} else {
-							lds_add_i32(&acc[rel * F + f], wh * dy[u][f]);
-						}
-					}
-				}
-			}
+			accum_point<D, F, H, KIND, MODE, OPTS>(xs[u], dy[u], base + u * blockDim.x, level, B, li, hash_grid, interp, begin, len, f0,
+			                                       nf, acc, o);
 		}
 	}
 }
@@ -166,6 +214,17 @@ __device__ __forceinline__ void grid_bwd_mode(int mode, int layout, uint32_t B, 
 		if (mode == 2) { grid_bwd_points<D, F, H, KIND, 2, OPTS>(layout, B, pos, pstride, dLdy, dy_stride, level, li, hash_grid, interp, begin, len, f0, nf, i0, i1, scale, acc, o); return; }
 	}
 	grid_bwd_points<D, F, H, KIND, 1, OPTS>(layout, B, pos, pstride, dLdy, dy_stride, level, li, hash_grid, interp, begin, len, f0, nf, i0, i1, scale, acc, o);
+}
+
+template <uint32_t D, uint32_t F, HashType H, int KIND>
+__device__ __forceinline__ void grid_bwd_mode_regs(int mode, const uint32_t (&dyb)[GRID_BWD_PR], uint32_t B, const float* pos,
+                                                   uint32_t pstride, uint32_t level, const LevelInfo& li, bool hash_grid, Interp interp,
+                                                   uint32_t begin, uint32_t len, uint32_t f0, uint32_t nf, uint32_t i0, uint32_t i1,
+                                                   float scale, int* acc, const GridOpts& o) {
+	if constexpr (F == 2) {
+		if (mode == 0) { grid_bwd_points_regs<D, F, H, KIND, 0>(dyb, B, pos, pstride, level, li, hash_grid, interp, begin, len, f0, nf, i0, i1, scale, acc, o); return; }
+	}
+	grid_bwd_points_regs<D, F, H, KIND, 1>(dyb, B, pos, pstride, level, li, hash_grid, interp, begin, len, f0, nf, i0, i1, scale, acc, o);
 }
 
 // Network-gradient tail (extra workgroups g = 0 .. n_mlp_groups-1, on CUs the grid items leave
@@ -224,8 +283,8 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 	if (blockIdx.x >= n_items * n_chunks) {
 		grid_bwd_mlp_tail(ep, blockIdx.x - n_items * n_chunks, (float*)acc);
 		if (dbg_times && threadIdx.x == 0) {
-			dbg_times[2 * blockIdx.x] = t_start;
-			dbg_times[2 * blockIdx.x + 1] = wall_clock64();
+			dbg_times[6 * blockIdx.x] = t_start;
+			for (int k = 1; k < 5; ++k) dbg_times[6 * blockIdx.x + k] = wall_clock64();
 		}
 		return;
 	}
@@ -252,24 +311,53 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 	// other entries almost no resolution (a max-based bound would lose its whole ratio to the mean).
 	// A non-finite dL/dy makes the item's gradient NaN (the reference's fp16 sums would carry it).
 	float m = 0.0f;
-	for (uint32_t ib = i0 + threadIdx.x; ib < i1; ib += 8 * blockDim.x) {
-		float dy[8][F];
+	// D == 2, F <= 2 without grid options, and a chunk of at most GRID_BWD_PR points per thread (the
+	// config_hash step: 32768-point chunks): the chunk's dL/dy bits are loaded once, all of them in
+	// flight together, kept in registers for the accumulation, and the pre-pass is one load latency
+	// instead of one per 8 points.
+	constexpr bool REGS_OK = D == 2 && F <= 2 && !OPTS;
+	const uint32_t n_pts = i1 > i0 ? i1 - i0 : 0u;
+	const bool use_regs = REGS_OK && n_pts <= GRID_BWD_THREADS * GRID_BWD_PR;
+	uint32_t dyb[GRID_BWD_PR];
+	if constexpr (REGS_OK) {
+		if (use_regs) {
 #pragma unroll
-		for (uint32_t u = 0; u < 8; ++u) {
-			const uint32_t i = ib + u * blockDim.x;
-			if (i < i1) load_dy<F>(layout, dLdy, dy_stride, it.level, B, i, dy[u]);
-			else {
+			for (uint32_t p = 0; p < GRID_BWD_PR; ++p) {
+				const uint32_t i = i0 + threadIdx.x + p * blockDim.x;
+				dyb[p] = i < i1 ? load_dy_bits<F>(layout, dLdy, dy_stride, it.level, B, i) : 0u;
+			}
 #pragma unroll
-				for (uint32_t f = 0; f < F; ++f) dy[u][f] = 0.0f;
+			for (uint32_t p = 0; p < GRID_BWD_PR; ++p) {
+				float s = 0.0f;
+#pragma unroll
+				for (uint32_t f = 0; f < F; ++f) {
+					const float v = dy_bits_feature(dyb[p], f);
+					if (f - f0 < nf) s = __builtin_isfinite(v) ? fmaxf(s, fabsf(v)) : __builtin_inff();
+				}
+				m += s;
 			}
 		}
+	}
+	if (!use_regs) {
+		for (uint32_t ib = i0 + threadIdx.x; ib < i1; ib += 8 * blockDim.x) {
+			float dy[8][F];
 #pragma unroll
-		for (uint32_t u = 0; u < 8; ++u) {
-			float s = 0.0f;
+			for (uint32_t u = 0; u < 8; ++u) {
+				const uint32_t i = ib + u * blockDim.x;
+				if (i < i1) load_dy<F>(layout, dLdy, dy_stride, it.level, B, i, dy[u]);
+				else {
 #pragma unroll
-			for (uint32_t f = 0; f < F; ++f)
-				if (f - f0 < nf) s = __builtin_isfinite(dy[u][f]) ? fmaxf(s, fabsf(dy[u][f])) : __builtin_inff();
-			m += s;
+					for (uint32_t f = 0; f < F; ++f) dy[u][f] = 0.0f;
+				}
+			}
+#pragma unroll
+			for (uint32_t u = 0; u < 8; ++u) {
+				float s = 0.0f;
+#pragma unroll
+				for (uint32_t f = 0; f < F; ++f)
+					if (f - f0 < nf) s = __builtin_isfinite(dy[u][f]) ? fmaxf(s, fabsf(dy[u][f])) : __builtin_inff();
+				m += s;
+			}
 		}
 	}
 #pragma unroll
@@ -288,6 +376,7 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 		e = max(-126, min(e, 100));
 	}
 	const float scale = ldexpf(1.0f, e);
+	if (dbg_times && threadIdx.x == 0) dbg_times[6 * blockIdx.x + 1] = wall_clock64();  // zeroing + pre-pass done
 
 	// uniform per item: index kind and accumulation mode
 	uint64_t full = 1;
@@ -297,13 +386,26 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 	if (whole && full <= li.size) kind = IDX_DENSE;
 	else if (whole && hash_grid && (li.size & (li.size - 1)) == 0) kind = IDX_HASH_POW2;
 	const int mode = nf < F ? 1 : (F == 2 ? 0 : 2);
+	if constexpr (REGS_OK) {
+		if (use_regs) {
+			if (kind == IDX_HASH_POW2)
+				grid_bwd_mode_regs<D, F, H, IDX_HASH_POW2>(mode, dyb, B, pos, pstride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, nf, i0, i1, scale, acc_w, o);
+			else if (kind == IDX_DENSE)
+				grid_bwd_mode_regs<D, F, H, IDX_DENSE>(mode, dyb, B, pos, pstride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, nf, i0, i1, scale, acc_w, o);
+			else
+				grid_bwd_mode_regs<D, F, H, IDX_GENERIC>(mode, dyb, B, pos, pstride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, nf, i0, i1, scale, acc_w, o);
+		}
+	}
+	if (!use_regs) {
 	if (kind == IDX_HASH_POW2)
 		grid_bwd_mode<D, F, H, IDX_HASH_POW2, OPTS>(mode, layout, B, pos, pstride, dLdy, dy_stride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, nf, i0, i1, scale, acc_w, o);
 	else if (kind == IDX_DENSE)
 		grid_bwd_mode<D, F, H, IDX_DENSE, OPTS>(mode, layout, B, pos, pstride, dLdy, dy_stride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, nf, i0, i1, scale, acc_w, o);
 	else
 		grid_bwd_mode<D, F, H, IDX_GENERIC, OPTS>(mode, layout, B, pos, pstride, dLdy, dy_stride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, nf, i0, i1, scale, acc_w, o);
+	}
 	__syncthreads();
+	if (dbg_times && threadIdx.x == 0) dbg_times[6 * blockIdx.x + 2] = wall_clock64();  // accumulation done
 	if (R > 1) {  // merge the replicas into replica 0
 		if (mode == 0) {
 			long long* a64 = (long long*)acc;
@@ -321,6 +423,7 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 		}
 		__syncthreads();
 	}
+	if (dbg_times && threadIdx.x == 0) dbg_times[6 * blockIdx.x + 3] = wall_clock64();  // replica merge done
 	// write the chunk slab (GridSlabMap layout: this item's accumulators are one contiguous range)
 	const float inv = finite ? ldexpf(1.0f, -e) : __builtin_nanf("");
 	float* dst = partial + (size_t)chunk * partial_stride + (size_t)li.offset * F + (size_t)f0 * li.size + (size_t)it.begin * nf;
@@ -355,8 +458,8 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 		}
 	}
 	if (dbg_times && threadIdx.x == 0) {
-		dbg_times[2 * blockIdx.x] = t_start;
-		dbg_times[2 * blockIdx.x + 1] = wall_clock64();
+		dbg_times[6 * blockIdx.x] = t_start;
+		dbg_times[6 * blockIdx.x + 4] = wall_clock64();
 	}
 }
 

@@ -203,4 +203,26 @@ __device__ __forceinline__ void load_dy(int layout, const _Float16* __restrict__
 	}
 }
 
+// The raw fp16 bits of dL/dy of point i, level `level` (F <= 2 features, feature f in bits
+// [16f, 16f + 16)), same layouts as load_dy.
+template <uint32_t F>
+__device__ __forceinline__ uint32_t load_dy_bits(int layout, const _Float16* __restrict__ dLdy, uint32_t dy_stride, uint32_t level,
+                                                 uint32_t B, uint32_t i) {
+	static_assert(F <= 2, "load_dy_bits: F <= 2");
+	const uint16_t* d16 = (const uint16_t*)dLdy;
+	if (layout == 0) {
+		if constexpr (F == 2) return ((const uint32_t*)dLdy)[(size_t)level * B + i];
+		else return d16[(size_t)level * B + i];
+	}
+	uint32_t r = 0;
+#pragma unroll
+	for (uint32_t f = 0; f < F; ++f)
+		r |= (uint32_t)(layout == 1 ? d16[(size_t)(level * F + f) * B + i] : d16[(size_t)i * dy_stride + level * F + f]) << (16 * f);
+	return r;
+}
+
+__device__ __forceinline__ float dy_bits_feature(uint32_t bits, uint32_t f) {
+	return (float)__builtin_bit_cast(_Float16, (uint16_t)(bits >> (16 * f)));
+}
+
 }  // namespace tcnn_amd
