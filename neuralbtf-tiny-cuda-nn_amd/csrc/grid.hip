@@ -528,7 +528,7 @@ void launch_grid_bwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_
 		for (uint32_t it = 0; it < n_slices; ++it) {
 			double sum = 0, mx = 0, st0 = 1e30, ph[4] = {0, 0, 0, 0};
 			for (uint32_t c = 0; c < n_chunks; ++c) {
-				const uint32_t b = c * n_slices + it;
+				const uint32_t b = it * n_chunks + c;
 				const double d = (t[6 * b + 4] - t[6 * b]) / 100.0;
 				sum += d; mx = std::max(mx, d); st0 = std::min(st0, (t[6 * b] - t0) / 100.0);
 				for (int k = 0; k < 4; ++k) ph[k] += (t[6 * b + k + 1] - t[6 * b + k]) / 100.0 / n_chunks;

@@ -126,27 +126,34 @@ __device__ __forceinline__ void accum_point(const float (&x)[D], const float (&d
 // Register-resident variant (D == 2, F <= 2, no grid options): the chunk's dL/dy bits were loaded
 // into dyb (GRID_BWD_PR points per thread, point i0 + threadIdx.x + p * blockDim.x in slot p) for the
 // scale pre-pass and are reused here; positions stream in batches of 8 with the next batch in flight.
-constexpr uint32_t GRID_BWD_PR = 32;
+constexpr uint32_t GRID_BWD_PR = 32, GRID_BWD_PU = 8;
+template <uint32_t D>
+__device__ __forceinline__ void load_pos_batch(const float* __restrict__ pos, uint32_t pstride, uint32_t i0, uint32_t i1, uint32_t k,
+                                               float (&dst)[GRID_BWD_PU][D]) {
+#pragma unroll
+	for (uint32_t u = 0; u < GRID_BWD_PU; ++u) {
+		const uint32_t i = i0 + threadIdx.x + (k * GRID_BWD_PU + u) * blockDim.x;
+#pragma unroll
+		for (uint32_t d = 0; d < D; ++d) dst[u][d] = i < i1 ? pos[(size_t)i * pstride + d] : 0.0f;
+	}
+}
+
 template <uint32_t D, uint32_t F, HashType H, int KIND, int MODE>
-__device__ __forceinline__ void grid_bwd_points_regs(const uint32_t (&dyb)[GRID_BWD_PR], uint32_t B, const float* __restrict__ pos,
+__device__ __forceinline__ void grid_bwd_points_regs(const uint32_t (&dyb)[GRID_BWD_PR], const float (&xs0)[GRID_BWD_PU][D],
+                                                     uint32_t B, const float* __restrict__ pos,
                                                      uint32_t pstride, uint32_t level, const LevelInfo& li, bool hash_grid,
                                                      Interp interp, uint32_t begin, uint32_t len, uint32_t f0, uint32_t nf,
                                                      uint32_t i0, uint32_t i1, float scale, int* acc, const GridOpts& o) {
-	constexpr uint32_t U = 8, NB = GRID_BWD_PR / U;
+	constexpr uint32_t U = GRID_BWD_PU, NB = GRID_BWD_PR / U;
 	float xs[2][U][D];
-	auto load_pos = [&](uint32_t k, float (&dst)[U][D]) {
 #pragma unroll
-		for (uint32_t u = 0; u < U; ++u) {
-			const uint32_t i = i0 + threadIdx.x + (k * U + u) * blockDim.x;
+	for (uint32_t u = 0; u < U; ++u)
 #pragma unroll
-			for (uint32_t d = 0; d < D; ++d) dst[u][d] = i < i1 ? pos[(size_t)i * pstride + d] : 0.0f;
-		}
-	};
-	load_pos(0, xs[0]);
+		for (uint32_t d = 0; d < D; ++d) xs[0][u][d] = xs0[u][d];
 #pragma unroll
 	for (uint32_t k = 0; k < NB; ++k) {
 		if (i0 + threadIdx.x + k * U * blockDim.x >= i1) break;
-		if (k + 1 < NB) load_pos(k + 1, xs[(k + 1) & 1]);
+		if (k + 1 < NB) load_pos_batch<D>(pos, pstride, i0, i1, k + 1, xs[(k + 1) & 1]);
 #pragma unroll
 		for (uint32_t u = 0; u < U; ++u) {
 			const uint32_t p = k * U + u;
@@ -217,14 +224,15 @@ __device__ __forceinline__ void grid_bwd_mode(int mode, int layout, uint32_t B, 
 }
 
 template <uint32_t D, uint32_t F, HashType H, int KIND>
-__device__ __forceinline__ void grid_bwd_mode_regs(int mode, const uint32_t (&dyb)[GRID_BWD_PR], uint32_t B, const float* pos,
+__device__ __forceinline__ void grid_bwd_mode_regs(int mode, const uint32_t (&dyb)[GRID_BWD_PR], const float (&xs0)[GRID_BWD_PU][D],
+                                                   uint32_t B, const float* pos,
                                                    uint32_t pstride, uint32_t level, const LevelInfo& li, bool hash_grid, Interp interp,
                                                    uint32_t begin, uint32_t len, uint32_t f0, uint32_t nf, uint32_t i0, uint32_t i1,
                                                    float scale, int* acc, const GridOpts& o) {
 	if constexpr (F == 2) {
-		if (mode == 0) { grid_bwd_points_regs<D, F, H, KIND, 0>(dyb, B, pos, pstride, level, li, hash_grid, interp, begin, len, f0, nf, i0, i1, scale, acc, o); return; }
+		if (mode == 0) { grid_bwd_points_regs<D, F, H, KIND, 0>(dyb, xs0, B, pos, pstride, level, li, hash_grid, interp, begin, len, f0, nf, i0, i1, scale, acc, o); return; }
 	}
-	grid_bwd_points_regs<D, F, H, KIND, 1>(dyb, B, pos, pstride, level, li, hash_grid, interp, begin, len, f0, nf, i0, i1, scale, acc, o);
+	grid_bwd_points_regs<D, F, H, KIND, 1>(dyb, xs0, B, pos, pstride, level, li, hash_grid, interp, begin, len, f0, nf, i0, i1, scale, acc, o);
 }
 
 // Network-gradient tail (extra workgroups g = 0 .. n_mlp_groups-1, on CUs the grid items leave
@@ -288,7 +296,10 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 		}
 		return;
 	}
-	const uint32_t item = blockIdx.x % n_items, chunk = blockIdx.x / n_items;
+	// chunk-minor numbering: blocks are dealt round-robin over the 8 XCDs, so with 8 chunks every
+	// item of chunk c lands on one XCD and the chunk's positions (re-read by all 26 items of
+	// config_hash) stay in that XCD's L2
+	const uint32_t item = blockIdx.x / n_chunks, chunk = blockIdx.x % n_chunks;
 	const GridSlice it = items[item];
 	const LevelInfo li = levels[it.level];
 	const uint32_t len = it.end - it.begin;
@@ -319,6 +330,7 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 	const uint32_t n_pts = i1 > i0 ? i1 - i0 : 0u;
 	const bool use_regs = REGS_OK && n_pts <= GRID_BWD_THREADS * GRID_BWD_PR;
 	uint32_t dyb[GRID_BWD_PR];
+	float xs0[GRID_BWD_PU][D];  // the accumulation's first position batch, in flight across the scale reduction
 	if constexpr (REGS_OK) {
 		if (use_regs) {
 #pragma unroll
@@ -326,6 +338,7 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 				const uint32_t i = i0 + threadIdx.x + p * blockDim.x;
 				dyb[p] = i < i1 ? load_dy_bits<F>(layout, dLdy, dy_stride, it.level, B, i) : 0u;
 			}
+			load_pos_batch<D>(pos, pstride, i0, i1, 0, xs0);
 #pragma unroll
 			for (uint32_t p = 0; p < GRID_BWD_PR; ++p) {
 				float s = 0.0f;
@@ -389,11 +402,11 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 	if constexpr (REGS_OK) {
 		if (use_regs) {
 			if (kind == IDX_HASH_POW2)
-				grid_bwd_mode_regs<D, F, H, IDX_HASH_POW2>(mode, dyb, B, pos, pstride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, nf, i0, i1, scale, acc_w, o);
+				grid_bwd_mode_regs<D, F, H, IDX_HASH_POW2>(mode, dyb, xs0, B, pos, pstride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, nf, i0, i1, scale, acc_w, o);
 			else if (kind == IDX_DENSE)
-				grid_bwd_mode_regs<D, F, H, IDX_DENSE>(mode, dyb, B, pos, pstride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, nf, i0, i1, scale, acc_w, o);
+				grid_bwd_mode_regs<D, F, H, IDX_DENSE>(mode, dyb, xs0, B, pos, pstride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, nf, i0, i1, scale, acc_w, o);
 			else
-				grid_bwd_mode_regs<D, F, H, IDX_GENERIC>(mode, dyb, B, pos, pstride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, nf, i0, i1, scale, acc_w, o);
+				grid_bwd_mode_regs<D, F, H, IDX_GENERIC>(mode, dyb, xs0, B, pos, pstride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, nf, i0, i1, scale, acc_w, o);
 		}
 	}
 	if (!use_regs) {
