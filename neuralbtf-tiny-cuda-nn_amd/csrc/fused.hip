@@ -120,10 +120,12 @@ void launch_fused_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, ui
                         uint32_t B, uint32_t dims, float loss_scale, const void* params16, const void* table16,
                         const float* pos, const float* target, void* out16, void* dLdenc_pairs,
                         float* wgrad_partial, float* loss_partial, const LevelInfo* levels, bool hash_grid,
-                        Interp interp, uint32_t n_blocks, const void* dout16, const void* wimage, uint32_t loss_l2) {
+                        Interp interp, uint32_t n_blocks, const void* dout16, const void* wimage, uint32_t loss_l2,
+                        bool inrange_index) {
 	TCNN_CHECK(B % 32 == 0, "fused train: batch must be a multiple of 32");
 	FusedTrainArgs a;
 	a.loss_l2 = loss_l2;
+	a.inrange_index = inrange_index ? 1u : 0u;
 	a.wimage = (const _Float16*)wimage;
 	a.dout = (const _Float16*)dout16;
 	a.B = B;
@@ -212,6 +214,7 @@ void launch_fused_train_profile(hipStream_t st, uint32_t B, uint32_t dims, const
 	a.params = (const _Float16*)params16; a.table = (const uint32_t*)table16; a.pos = pos; a.target = target;
 	a.out = nullptr; a.dLdenc = (uint32_t*)dLdenc; a.wgrad_partial = wgrad_partial; a.loss_partial = loss_partial;
 	a.levels = levels; a.hash_grid = 1; a.interp = (uint32_t)Interp::Linear; a.dout = nullptr; a.prof = prof;
+	a.inrange_index = 1;
 	using K = RegKernelLayout<64, 32, 2>;
 	static bool attr = false;
 	if (!attr) {

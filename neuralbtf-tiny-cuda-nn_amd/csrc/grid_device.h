@@ -180,6 +180,58 @@ __device__ __forceinline__ h2 encode_level_f2(const uint32_t* __restrict__ table
 	return r;
 }
 
+// grid_index for positions inside [0, 1] on a level that is hashed with a power-of-two size or dense
+// (res^D <= size): there the dense index is below 2 * size, so `% size` is one conditional
+// subtraction and the whole computation is branch-free -- the compiler can then issue the gathers of
+// several levels before consuming any of them. Same result as grid_index under those conditions
+// (the caller checks them: GridEncodingHost::inrange_index_ok and a wave-wide position test).
+template <uint32_t D, HashType H>
+__device__ __forceinline__ uint32_t grid_index_inrange(bool hash_grid, uint32_t size, uint32_t res, const uint32_t* pg) {
+	uint32_t stride = 1, dense = 0;
+#pragma unroll
+	for (uint32_t d = 0; d < D; ++d) {
+		dense += pg[d] * stride;
+		stride *= res;
+	}
+	uint32_t h = 0;
+#pragma unroll
+	for (uint32_t d = 0; d < D; ++d) h ^= pg[d] * hash_prime<H>(d);
+	const bool hashed = hash_grid && size < stride;
+	const uint32_t dm = dense >= size ? dense - size : dense;
+	return hashed ? (h & (size - 1)) : dm;
+}
+
+template <uint32_t D, HashType H>
+__device__ __forceinline__ h2 encode_level_f2_inrange(const uint32_t* __restrict__ table_u32, const LevelInfo& li, bool hash_grid,
+                                                      const float* x) {
+	float pos[D];
+	uint32_t pg[D];
+#pragma unroll
+	for (uint32_t d = 0; d < D; ++d) pos_fract(x[d], li.scale, Interp::Linear, pos[d], pg[d]);
+	constexpr uint32_t NC = 1u << D;
+	uint32_t v[NC];
+	_Float16 w16[NC];
+#pragma unroll
+	for (uint32_t c = 0; c < NC; ++c) {
+		float w = 1.0f;
+		uint32_t local[D];
+#pragma unroll
+		for (uint32_t d = 0; d < D; ++d) {
+			if ((c & (1u << d)) == 0) { w *= 1.0f - pos[d]; local[d] = pg[d]; }
+			else { w *= pos[d]; local[d] = pg[d] + 1; }
+		}
+		w16[c] = (_Float16)w;  // as encode_level_f2
+		v[c] = table_u32[li.offset + grid_index_inrange<D, H>(hash_grid, li.size, li.res, local)];
+	}
+	h2 r = {(_Float16)0.0f, (_Float16)0.0f};
+#pragma unroll
+	for (uint32_t c = 0; c < NC; ++c) {
+		h2 wv = {w16[c], w16[c]};
+		r = pk_fma_f16(wv, __builtin_bit_cast(h2, v[c]), r);
+	}
+	return r;
+}
+
 // F fp16 features of one table entry / one point-level
 template <uint32_t F>
 struct HVec { _Float16 v[F]; };

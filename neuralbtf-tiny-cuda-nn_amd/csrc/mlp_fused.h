@@ -174,6 +174,7 @@ struct FusedTrainArgs {
 	float loss_scale;
 	float n_total;          // (float)(B * dims) as in relative_l2.h:64
 	uint32_t loss_l2;       // 0: RelativeL2 (relative_l2.h:40-76), 1: L2 (l2.h:40-76)
+	uint32_t inrange_index; // 1: grid_index_inrange is exact for in-range positions (Linear interpolation)
 	const _Float16* params; // MLP weights fp16 [W0 | hidden | Wout]
 	const uint32_t* table;  // grid params as half2 entries (F == 2)
 	const float* pos;       // [B][D]
@@ -531,23 +532,44 @@ __global__ __launch_bounds__(64 * FUSED_WAVES, 8 / FUSED_WAVES) void k_fused_tra
 				tg[tau][r] = (!EXT_DOUT && o < a.dims) ? a.target[(size_t)i * a.dims + o] : 0.0f;
 			}
 		}
+		float xs[2][D];
+		bool inr = true;
 #pragma unroll
 		for (int tau = 0; tau < 2; ++tau) {
 			const uint32_t i = base + 16 * tau + c;
-			float x[D];
 #pragma unroll
-			for (uint32_t d = 0; d < D; ++d) x[d] = a.pos[(size_t)i * D + d];
-			if constexpr (EXT_DOUT) Gext[tau] = *(const h4*)(a.dout + (size_t)i * 16 + 4 * q);
-#pragma unroll
-			for (int s = 0; s < KI; ++s) {
-#pragma unroll
-				for (int pp = 0; pp < 4; ++pp) {
-					const int level = 16 * s + 8 * (pp >> 1) + 2 * q + (pp & 1);
-					const h2 e = encode_level_f2<D, H>(a.table, sLvl[level], hash_grid, interp, x);
-					xt[tau][2 * s + (pp >> 1)][2 * (pp & 1) + 0] = e[0];
-					xt[tau][2 * s + (pp >> 1)][2 * (pp & 1) + 1] = e[1];
-				}
+			for (uint32_t d = 0; d < D; ++d) {
+				xs[tau][d] = a.pos[(size_t)i * D + d];
+				inr = inr && xs[tau][d] >= 0.0f && xs[tau][d] <= 1.0f;
 			}
+			if constexpr (EXT_DOUT) Gext[tau] = *(const h4*)(a.dout + (size_t)i * 16 + 4 * q);
+		}
+		// every position of the wave's slice in [0, 1]: the branch-free index (gathers of several
+		// levels in flight together); otherwise the general index with its rare `% size` path
+		if (a.inrange_index && __builtin_amdgcn_ballot_w64(!inr) == 0) {
+#pragma unroll
+			for (int tau = 0; tau < 2; ++tau)
+#pragma unroll
+				for (int s = 0; s < KI; ++s)
+#pragma unroll
+					for (int pp = 0; pp < 4; ++pp) {
+						const int level = 16 * s + 8 * (pp >> 1) + 2 * q + (pp & 1);
+						const h2 e = encode_level_f2_inrange<D, H>(a.table, sLvl[level], hash_grid, xs[tau]);
+						xt[tau][2 * s + (pp >> 1)][2 * (pp & 1) + 0] = e[0];
+						xt[tau][2 * s + (pp >> 1)][2 * (pp & 1) + 1] = e[1];
+					}
+		} else {
+#pragma unroll
+			for (int tau = 0; tau < 2; ++tau)
+#pragma unroll
+				for (int s = 0; s < KI; ++s)
+#pragma unroll
+					for (int pp = 0; pp < 4; ++pp) {
+						const int level = 16 * s + 8 * (pp >> 1) + 2 * q + (pp & 1);
+						const h2 e = encode_level_f2<D, H>(a.table, sLvl[level], hash_grid, interp, xs[tau]);
+						xt[tau][2 * s + (pp >> 1)][2 * (pp & 1) + 0] = e[0];
+						xt[tau][2 * s + (pp >> 1)][2 * (pp & 1) + 1] = e[1];
+					}
 		}
 		if constexpr (PROF) { t1 = stamp(); ph[0] += t1 - t0; t0 = t1; }
 		auto target = [&](int tau, uint32_t o) { return tg[tau][o & 3]; };

@@ -240,6 +240,23 @@ GridEncodingHost::GridEncodingHost(uint32_t n_dims, const json& enc) {
 		TCNN_HIP_CHECK(hipMemcpy(d_bin_levels.p, bin_levels.data(), bin_levels.size() * sizeof(GridBinLevel), hipMemcpyHostToDevice));
 	}
 
+	// grid_index_inrange (grid_device.h) is exact for positions in [0, 1] on every level iff its
+	// hashing decision matches the reference stride loop's (u32 arithmetic, with the loop's break),
+	// hashed levels have power-of-two sizes and dense levels hold res^D entries
+	inrange_index_ok = true;
+	for (const LevelInfo& li : levels) {
+		uint32_t stride = 1, s2 = 1;
+		for (uint32_t d = 0; d < desc.n_pos_dims; ++d) {
+			if (stride <= li.size) stride *= li.res;
+			s2 *= li.res;
+		}
+		uint64_t full = 1;
+		for (uint32_t d = 0; d < desc.n_pos_dims; ++d) full = std::min<uint64_t>(full * li.res, 1ull << 40);
+		const bool hashed = hash_grid() && li.size < stride;
+		if (hashed != (hash_grid() && li.size < s2)) inrange_index_ok = false;
+		if (hashed ? (li.size & (li.size - 1)) != 0 : full > li.size) inrange_index_ok = false;
+		if (li.res < 2) inrange_index_ok = false;
+	}
 	d_levels.reserve(levels.size() * sizeof(LevelInfo));
 	TCNN_HIP_CHECK(hipMemcpy(d_levels.p, levels.data(), levels.size() * sizeof(LevelInfo), hipMemcpyHostToDevice));
 	d_slices.reserve(slices.size() * sizeof(GridSlice));
@@ -594,7 +611,8 @@ void NetworkHost::fused_kernel(hipStream_t st, StepWorkspace& ws, uint32_t B, co
 	launch_fused_train(st, mlp.width, mlp.n_input, mlp.n_hidden_layers, grid->desc.n_pos_dims, grid->desc.hash_type,
 	                   mlp.activation, B, dims, loss_scale, params16, table, pos, target, out16, ws.dLdenc.p,
 	                   ws.wgrad_partial.as<float>(), ws.loss_partial.as<float>(), grid->dev_levels(), grid->hash_grid(),
-	                   grid->desc.interp, nb, dout16, ws.wimage.p, loss_l2);
+	                   grid->desc.interp, nb, dout16, ws.wimage.p, loss_l2,
+	                   grid->inrange_index_ok && grid->desc.interp == Interp::Linear && !std::getenv("TCNN_NO_INRANGE_INDEX"));
 }
 
 void NetworkHost::grid_backward(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, GridBwdEpilogue* ep) {

@@ -66,6 +66,7 @@ struct GridEncodingHost {
 	// [first_binned, L) go through the binned backward (grid_bin.hip), one slot each
 	std::vector<GridSlice> slices;
 	uint32_t first_binned = 0;
+	bool inrange_index_ok = false;  // grid_index_inrange is exact for in-range positions (ctor)
 	uint32_t n_lds_params = 0;  // offset[first_binned] * F
 	std::vector<GridBinLevel> bin_levels;
 	uint32_t n_buckets = 0, acc_lds_bytes = 0;

@@ -79,6 +79,28 @@ def test_fused_step_gradients_and_loss(torch_mod, B):
     assert e_grid <= 1e-3, e_grid
 
 
+def test_fused_step_positions_outside_unit_square(torch_mod):
+    """The fused kernel takes a branch-free grid index when every position of a wave's slice is in
+    [0, 1] and the general one (with the reference's `% size` wrap, common_device.h:706) otherwise:
+    a batch whose second half lies in [-0.5, 1.5] runs both paths, against the oracle."""
+    torch = torch_mod
+    from tinycudann import Trainer
+    t = Trainer(2, 3, CONFIG_HASH, seed=1337)
+    om = O.OracleModel(CONFIG_HASH, 2, 3, seed=1337)
+    B = 4096
+    pos, tgt = make_batch(B, seed=5)
+    pos[B // 2:] = pos[B // 2:] * 2.0 - 0.5
+    pos[B // 2 + 7] = [1.0, 0.0]  # the edges are in range
+    t.training_step(torch.from_numpy(pos).cuda(), torch.from_numpy(tgt).cuda(), run_optimizer=False)
+    loss_gpu = t.loss()
+    loss_ref = om.train_step(pos, tgt, run_optimizer=False)
+    assert abs(loss_gpu - loss_ref) <= 1e-3 * abs(loss_ref), (loss_gpu, loss_ref)
+    a = trainer_arrays(t)
+    nm = om.n_mlp_params
+    assert rel_err(a["g32"][:nm], om.grad32[:nm]) <= 1e-3
+    assert rel_err(a["g32"][nm:], om.grad32[nm:]) <= 1e-3
+
+
 def test_adam_step_matches_oracle_on_same_gradients(torch_mod):
     """Adam kernel in isolation: the oracle's Adam is fed the GPU's own fp16 gradients."""
     torch = torch_mod
