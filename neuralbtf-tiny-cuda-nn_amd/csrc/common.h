@@ -59,6 +59,7 @@ struct GridOpts {
 	uint32_t n_features = 0;  // n_levels * F (num_grid_features)
 	uint32_t active = 0;      // any option in effect (uniform fast-path test)
 	uint32_t n_levels = 0;    // set by the forward launcher (AoS lane mapping)
+	uint32_t inrange_index = 0;  // grid_index_inrange is exact for in-range positions (Linear)
 };
 
 struct GridDesc {

@@ -109,13 +109,22 @@ __global__ __launch_bounds__(256) void k_grid_fwd_aos_f2(uint32_t B, const float
 	const bool valid = i < B;
 	const Interp interp = (Interp)interp_u;
 	float x[D];
+	bool inr = true;
 #pragma unroll
-	for (uint32_t d = 0; d < D; ++d) x[d] = valid ? pos[(size_t)i * pstride + d] : 0.0f;
+	for (uint32_t d = 0; d < D; ++d) {
+		x[d] = valid ? pos[(size_t)i * pstride + d] : 0.0f;
+		inr = inr && x[d] >= 0.0f && x[d] <= 1.0f;
+	}
+	// all 64 points in [0, 1]: the branch-free index (see grid_index_inrange)
+	const bool fast = o.inrange_index && !o.active && __builtin_amdgcn_ballot_w64(!inr) == 0;
 	for (uint32_t level = wave; level < L; level += 4) {
 		const LevelInfo li = levels[level];
 		h2 r = {(_Float16)0.0f, (_Float16)0.0f};
-		if (valid && !(o.active && (float)level >= grid_max_level(o, i, 2) + 1e-3f))  // masked: 0 (grid.h:75-91)
+		if (fast) {
+			if (valid) r = encode_level_f2_inrange<D, H>(table, li, hash_grid != 0, x);
+		} else if (valid && !(o.active && (float)level >= grid_max_level(o, i, 2) + 1e-3f)) {  // masked: 0 (grid.h:75-91)
 			r = encode_level_f2<D, H>(table, li, hash_grid != 0, interp, x);
+		}
 		tile[lane * 65 + level] = __builtin_bit_cast(uint32_t, r);
 	}
 	__syncthreads();

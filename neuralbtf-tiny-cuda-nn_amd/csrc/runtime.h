@@ -88,6 +88,7 @@ struct GridEncodingHost {
 		o.n_features = n_features;
 		const float t = (max_level * (float)n_features) / (float)desc.n_features_per_level + 1e-3f;
 		o.active = (stochastic || max_level_gpu || (float)(desc.n_levels - 1) >= t) ? 1u : 0u;
+		o.inrange_index = (inrange_index_ok && desc.interp == Interp::Linear && !std::getenv("TCNN_NO_INRANGE_INDEX")) ? 1u : 0u;
 		return o;
 	}
 	const GridSlabMap* slab_map() const { return d_slab_map.as<GridSlabMap>(); }
