@@ -129,6 +129,7 @@ def main():
                     help="strong: shard the global batch over ranks (configs[4]); weak: a full batch per rank")
     ap.add_argument("--allreduce-dtype", choices=["fp32", "fp16"], default="fp32")
     ap.add_argument("--no-overlap", action="store_true", help="all-reduce after the whole backward")
+    ap.add_argument("--graph", action="store_true", help="replay the single-GPU training step as a hipGraph")
     ap.add_argument("--all-ranks-on-device0", action="store_true",
                     help="rehearse N>1 on a 1-GPU box (gloo); never used for measurements")
     args = ap.parse_args()
@@ -171,6 +172,8 @@ def main():
 
     from tinycudann.parallel import DataParallelTrainer
     dp = DataParallelTrainer(trainer, overlap=not args.no_overlap, allreduce_dtype=args.allreduce_dtype)
+    if args.graph:
+        trainer.set_graph(True)
 
     def step(i):
         pos, tgt = batches[i % NB]
@@ -235,6 +238,7 @@ def main():
                            (f", {args.allreduce_dtype} all-reduce" + ("" if args.no_overlap else " overlapped with the grid backward")
                             if world > 1 else ""),
         },
+        "step_graph": bool(args.graph),
         "samples_per_s": value * B_global,
         "final_loss": loss,
     }

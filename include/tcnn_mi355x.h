@@ -141,6 +141,14 @@ void* tcnn_trainer_param_gradients(tcnn_trainer* t);
 float* tcnn_trainer_gradients_fp32(tcnn_trainer* t);
 /* Data-parallel support: Adam reads grad_fp32 * grad_scale (set 1/N after a sum all-reduce). */
 int tcnn_trainer_set_gradient_scale(tcnn_trainer* t, float scale);
+/* hipGraph replay of the single-GPU training step (the reference Trainer's CUDA graph,
+ * trainer.h:163-190 / cuda_graph.h:52-178): off by default. While on, training_step with
+ * run_optimizer = 1 replays a captured graph as long as the batch size, the input / target pointers,
+ * the hyper-parameters and scales are unchanged, and re-captures otherwise; results are bit-identical
+ * to the eager step. The stream may be the legacy null stream (the graph runs on a private stream,
+ * ordered after and before the caller's with events). */
+int tcnn_trainer_set_graph(tcnn_trainer* t, int on);
+int tcnn_trainer_graph_stats(const tcnn_trainer* t, uint64_t* captures, uint64_t* replays);
 /* Re-upload params from a host fp32 array (Trainer::set_params_full_precision, trainer.h:231-244). */
 int tcnn_trainer_set_params_full_precision(tcnn_trainer* t, const float* host_params, uint64_t n);
 /* Adam step counter (AdamOptimizer::step(), adam.h:200-202). */

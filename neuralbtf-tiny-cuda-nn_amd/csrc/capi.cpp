@@ -381,6 +381,14 @@ int tcnn_trainer_set_gradient_scale(tcnn_trainer* t, float s) {
 	t->t->grad_scale = s;
 	return 0;
 }
+int tcnn_trainer_set_graph(tcnn_trainer* t, int on) {
+	return guard([&] { t->t->set_graph(on != 0); });
+}
+int tcnn_trainer_graph_stats(const tcnn_trainer* t, uint64_t* captures, uint64_t* replays) {
+	if (captures) *captures = t->t->graph_captures;
+	if (replays) *replays = t->t->graph_replays;
+	return 0;
+}
 int tcnn_trainer_serialize(tcnn_trainer* t, int with_optimizer, void* buf, uint64_t capacity, uint64_t* size) {
 	return guard([&] {
 		const std::vector<uint8_t> b = t->t->serialize(with_optimizer != 0);

@@ -822,6 +822,7 @@ void TrainerHost::training_step(hipStream_t st, uint32_t B, const float* input, 
 		if (timer.sampling) timer.marks.push_back({-1, -1, -1, -1, -1});
 	}
 	if (overlapped_ok()) {
+		if (use_graph && run_optimizer && !timer.enabled && !adam.adabound && training_step_graph(st, B, input, target)) return;
 		training_step_overlapped(st, B, input, target, run_optimizer);
 		return;
 	}
@@ -861,8 +862,9 @@ void TrainerHost::training_step_overlapped(hipStream_t st, uint32_t B, const flo
 	ep.n_mlp_groups = MLP_TAIL_GROUPS;
 	ep.n_mlp = (uint32_t)n_mlp;
 	ep.d_loss = d_loss.as<float>();
-	ep.factor_out = run_optimizer ? d_ftable.as<float>() + (adam_step - 1) : nullptr;
-	ep.factor_step = adam_step;
+	// this step's bias factor, unless the table already holds it (always, under graph replay)
+	ep.factor_out = (run_optimizer && ftable_valid < adam_step) ? d_ftable.as<float>() + (adam_step - 1) : nullptr;
+	ep.factor_step = ep.factor_out ? adam_step : 0u;
 	TCNN_CHECK(n_mlp % 4 == 0, "network parameter count must be a multiple of 4");
 	m.grid_backward(st, ws, B, input, &ep);
 	if (run_optimizer) ftable_valid = std::max(ftable_valid, adam_step);
@@ -892,6 +894,123 @@ void TrainerHost::training_step_overlapped(hipStream_t st, uint32_t B, const flo
 	}
 	mark(st, 3);
 	last_B = B;
+}
+
+// Captured step graphs, keyed by everything the step's kernels read (graph_key); a few are kept so
+// a caller cycling through a handful of batch buffers replays one graph per buffer.
+struct TrainerHost::StepGraph {
+	static constexpr size_t MAX_GRAPHS = 8;
+	hipStream_t cs = nullptr;  // capture / replay stream (the caller's may be the legacy null stream)
+	hipEvent_t e0 = nullptr, e1 = nullptr;
+	std::vector<std::pair<std::vector<uint64_t>, hipGraphExec_t>> execs;  // most recently used last
+	StepGraph() {
+		TCNN_HIP_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+		TCNN_HIP_CHECK(hipEventCreateWithFlags(&e0, hipEventDisableTiming));
+		TCNN_HIP_CHECK(hipEventCreateWithFlags(&e1, hipEventDisableTiming));
+	}
+	~StepGraph() {
+		for (auto& e : execs) (void)hipGraphExecDestroy(e.second);
+		(void)hipEventDestroy(e0);
+		(void)hipEventDestroy(e1);
+		(void)hipStreamDestroy(cs);
+	}
+	hipGraphExec_t find(const std::vector<uint64_t>& key) {
+		for (size_t i = 0; i < execs.size(); ++i)
+			if (execs[i].first == key) {
+				auto e = execs[i];
+				execs.erase(execs.begin() + i);
+				execs.push_back(e);
+				return e.second;
+			}
+		return nullptr;
+	}
+};
+
+TrainerHost::~TrainerHost() {
+	if (graph) (void)hipDeviceSynchronize();  // replays may still run on the graph's stream
+}
+
+void TrainerHost::set_graph(bool on) {
+	if (!on && graph) {
+		TCNN_HIP_CHECK(hipStreamSynchronize(graph->cs));
+		graph.reset();
+	}
+	use_graph = on;
+}
+
+std::vector<uint64_t> TrainerHost::graph_key(uint32_t B, const float* input, const float* target) const {
+	std::vector<uint64_t> k = {B, (uint64_t)(uintptr_t)input, (uint64_t)(uintptr_t)target, (uint64_t)ftable_valid,
+	                           (uint64_t)(uintptr_t)w32.p, (uint64_t)(uintptr_t)w16.p, (uint64_t)(uintptr_t)g16.p,
+	                           (uint64_t)(uintptr_t)g32.p, (uint64_t)(uintptr_t)m1.p, (uint64_t)(uintptr_t)m2.p,
+	                           (uint64_t)(uintptr_t)steps.p, (uint64_t)(uintptr_t)d_loss.p, (uint64_t)(uintptr_t)d_ftable.p,
+	                           (uint64_t)(uintptr_t)ws.dLdenc.p, (uint64_t)(uintptr_t)ws.wgrad_partial.p,
+	                           (uint64_t)(uintptr_t)ws.loss_partial.p, (uint64_t)(uintptr_t)ws.wimage.p,
+	                           (uint64_t)(uintptr_t)ws.gbw.partial.p, (uint64_t)(uintptr_t)ws.gbw.recs.p,
+	                           (uint64_t)(uintptr_t)ws.gbw.dir.p, (uint64_t)(uintptr_t)ws.gbw.dysum.p, ws.n_fused_blocks,
+	                           ws.gbw.n_chunks, (uint64_t)overlapped_ok()};
+	// every scalar the step's kernels take from the trainer (AdamArgs holds no pointer here)
+	const AdamArgs a = adam_args();
+	const size_t n = sizeof(AdamArgs) / 8 + 1;
+	std::vector<uint64_t> ab(n, 0);
+	std::memcpy(ab.data(), &a, sizeof(AdamArgs));
+	k.insert(k.end(), ab.begin(), ab.end());
+	const GridOpts o = model->grid->opts();
+	uint32_t ml = 0;
+	std::memcpy(&ml, &o.max_level, 4);
+	k.insert(k.end(), {(uint64_t)ml, (uint64_t)(uintptr_t)o.max_level_gpu, o.stochastic, o.n_features, o.active, o.inrange_index});
+	uint32_t ls = 0, gs = 0;
+	std::memcpy(&ls, &loss_scale, 4);
+	std::memcpy(&gs, &grad_scale, 4);
+	k.insert(k.end(), {(uint64_t)ls, (uint64_t)gs});
+	return k;
+}
+
+bool TrainerHost::training_step_graph(hipStream_t st, uint32_t B, const float* input, const float* target) {
+	if (adam_step + 1 >= GRAPH_STEPS || !ws.wimage_valid) return false;  // first step packs the weights eagerly
+	if (ftable_valid < GRAPH_STEPS || ftable_b1 != adam.beta1 || ftable_b2 != adam.beta2)
+		(void)adam_args_table(st, GRAPH_STEPS, GRAPH_STEPS);
+	if (!graph) graph = std::make_unique<StepGraph>();
+	std::vector<uint64_t> key = graph_key(B, input, target);
+	hipGraphExec_t exec = graph->find(key);
+	if (!exec) {
+		// eager step first (sizes every workspace for this B, so the capture allocates nothing)
+		training_step_overlapped(st, B, input, target, true);
+		key = graph_key(B, input, target);
+		TCNN_HIP_CHECK(hipStreamSynchronize(st));
+		TCNN_HIP_CHECK(hipStreamSynchronize(graph->cs));
+		if (graph->execs.size() >= StepGraph::MAX_GRAPHS) {
+			(void)hipGraphExecDestroy(graph->execs.front().second);
+			graph->execs.erase(graph->execs.begin());
+		}
+		const uint32_t step0 = adam_step, ftv0 = ftable_valid, lb0 = last_B;
+		const bool wv0 = ws.wimage_valid;
+		hipGraph_t g = nullptr;
+		TCNN_HIP_CHECK(hipStreamBeginCapture(graph->cs, hipStreamCaptureModeThreadLocal));
+		training_step_overlapped(graph->cs, B, input, target, true);
+		TCNN_HIP_CHECK(hipStreamEndCapture(graph->cs, &g));
+		adam_step = step0;  // the capture ran nothing
+		ftable_valid = ftv0;
+		last_B = lb0;
+		ws.wimage_valid = wv0;
+		hipGraphExec_t e = nullptr;
+		const hipError_t err = hipGraphInstantiate(&e, g, nullptr, nullptr, 0);
+		(void)hipGraphDestroy(g);
+		TCNN_HIP_CHECK(err);
+		graph->execs.emplace_back(key, e);
+		++graph_captures;
+		return true;
+	}
+	TCNN_HIP_CHECK(hipEventRecord(graph->e0, st));
+	TCNN_HIP_CHECK(hipStreamWaitEvent(graph->cs, graph->e0, 0));
+	TCNN_HIP_CHECK(hipGraphLaunch(exec, graph->cs));
+	TCNN_HIP_CHECK(hipEventRecord(graph->e1, graph->cs));
+	TCNN_HIP_CHECK(hipStreamWaitEvent(st, graph->e1, 0));
+	// the host-side effects of training_step_overlapped
+	++adam_step;
+	ws.wimage_valid = true;
+	last_B = B;
+	++graph_replays;
+	return true;
 }
 
 hipEvent_t PhaseTimer::get() {

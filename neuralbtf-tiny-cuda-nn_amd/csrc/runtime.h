@@ -290,6 +290,22 @@ struct TrainerHost {
 	void deserialize(const void* data, size_t size);
 	void mark(hipStream_t st, int phase);  // records phase boundary when timing is enabled
 	void profile_end(double* ms, uint32_t n_phases, uint32_t* n_steps);
+
+	// hipGraph replay of the single-GPU training step (the reference Trainer's CUDA graph,
+	// trainer.h:163-190, cuda_graph.h:52-178). Opt-in (tcnn_trainer_set_graph). A graph is replayed
+	// while every scalar and device pointer the step's kernels read is unchanged (graph_key); any
+	// change (batch size, input / target buffers, hyper-parameters, scales, workspace growth) runs
+	// the step eagerly and re-captures. The Adam bias-factor table is filled GRAPH_STEPS steps ahead
+	// first, so a replayed step carries no step-dependent kernel argument.
+	static constexpr uint32_t GRAPH_STEPS = 1u << 20;
+	bool use_graph = false;
+	struct StepGraph;
+	std::unique_ptr<StepGraph> graph;
+	uint64_t graph_replays = 0, graph_captures = 0;
+	std::vector<uint64_t> graph_key(uint32_t B, const float* input, const float* target) const;
+	bool training_step_graph(hipStream_t st, uint32_t B, const float* input, const float* target);
+	void set_graph(bool on);
+	~TrainerHost();
 };
 
 }  // namespace tcnn_amd

@@ -61,6 +61,17 @@ class Trainer:
                                                ctypes.c_void_p(out.data_ptr())))
         return out
 
+    def set_graph(self, on=True):
+        """Replay the training step as a hipGraph while its inputs are unchanged (the reference
+        Trainer's CUDA graph, trainer.h:163-190); bit-identical to the eager step."""
+        L.check(L.lib().tcnn_trainer_set_graph(self.h, int(bool(on))))
+
+    def graph_stats(self):
+        """(captures, replays) of the training-step graph."""
+        c, r = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        L.check(L.lib().tcnn_trainer_graph_stats(self.h, ctypes.byref(c), ctypes.byref(r)))
+        return c.value, r.value
+
     def set_gradient_scale(self, s):
         L.check(L.lib().tcnn_trainer_set_gradient_scale(self.h, float(s)))
 

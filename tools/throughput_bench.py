@@ -27,6 +27,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--graph", action="store_true", help="training steps replayed as hipGraphs")
     args = ap.parse_args()
     import torch
     from bench import rgb_field_torch
@@ -50,6 +51,8 @@ def main():
         cfg = copy.deepcopy(base)
         cfg["network"]["n_neurons"] = W
         t = Trainer(2, 3, cfg, seed=1337)
+        if args.graph:
+            t.set_graph(True)
         for lb in (14, 18, 21):
             B = 1 << lb
             pos = torch.rand(B, 2, device="cuda")
