@@ -188,10 +188,12 @@ __device__ __forceinline__ h2 encode_level_f2(const uint32_t* __restrict__ table
 template <uint32_t D, HashType H>
 __device__ __forceinline__ uint32_t grid_index_inrange(bool hash_grid, uint32_t size, uint32_t res, const uint32_t* pg) {
 	uint32_t stride = 1, dense = 0;
+	bool brk = false;
 #pragma unroll
-	for (uint32_t d = 0; d < D; ++d) {
-		dense += pg[d] * stride;
-		stride *= res;
+	for (uint32_t d = 0; d < D; ++d) {  // the reference's stride loop, its break as a predicate
+		brk = brk || stride > size;
+		dense = brk ? dense : dense + pg[d] * stride;
+		stride = brk ? stride : stride * res;
 	}
 	uint32_t h = 0;
 #pragma unroll

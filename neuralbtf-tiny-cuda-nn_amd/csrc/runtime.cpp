@@ -240,20 +240,17 @@ GridEncodingHost::GridEncodingHost(uint32_t n_dims, const json& enc) {
 		TCNN_HIP_CHECK(hipMemcpy(d_bin_levels.p, bin_levels.data(), bin_levels.size() * sizeof(GridBinLevel), hipMemcpyHostToDevice));
 	}
 
-	// grid_index_inrange (grid_device.h) is exact for positions in [0, 1] on every level iff its
-	// hashing decision matches the reference stride loop's (u32 arithmetic, with the loop's break),
-	// hashed levels have power-of-two sizes and dense levels hold res^D entries
+	// grid_index_inrange (grid_device.h: the reference stride loop, then a mask or ONE conditional
+	// subtraction) is exact for positions in [0, 1] on every level iff hashed levels have
+	// power-of-two sizes and the others hold res^D entries (their index is then < 2 size)
 	inrange_index_ok = true;
 	for (const LevelInfo& li : levels) {
-		uint32_t stride = 1, s2 = 1;
-		for (uint32_t d = 0; d < desc.n_pos_dims; ++d) {
+		uint32_t stride = 1;
+		for (uint32_t d = 0; d < desc.n_pos_dims; ++d)
 			if (stride <= li.size) stride *= li.res;
-			s2 *= li.res;
-		}
 		uint64_t full = 1;
 		for (uint32_t d = 0; d < desc.n_pos_dims; ++d) full = std::min<uint64_t>(full * li.res, 1ull << 40);
 		const bool hashed = hash_grid() && li.size < stride;
-		if (hashed != (hash_grid() && li.size < s2)) inrange_index_ok = false;
 		if (hashed ? (li.size & (li.size - 1)) != 0 : full > li.size) inrange_index_ok = false;
 		if (li.res < 2) inrange_index_ok = false;
 	}
