@@ -129,6 +129,9 @@ def main():
                     help="strong: shard the global batch over ranks (configs[4]); weak: a full batch per rank")
     ap.add_argument("--allreduce-dtype", choices=["fp32", "fp16"], default="fp32")
     ap.add_argument("--no-overlap", action="store_true", help="all-reduce after the whole backward")
+    ap.add_argument("--optimizer", choices=["sharded", "replicated"], default="sharded",
+                    help="N > 1: sharded = reduce-scatter the gradient sums, Adam on 1/N of the parameters, "
+                         "all-gather the fp16 parameters; replicated = all-reduce, Adam everywhere")
     ap.add_argument("--graph", action="store_true", help="replay the single-GPU training step as a hipGraph")
     ap.add_argument("--all-ranks-on-device0", action="store_true",
                     help="rehearse N>1 on a 1-GPU box (gloo); never used for measurements")
@@ -171,7 +174,9 @@ def main():
         batches.append((pos, rgb_field_torch(pos)))
 
     from tinycudann.parallel import DataParallelTrainer
-    dp = DataParallelTrainer(trainer, overlap=not args.no_overlap, allreduce_dtype=args.allreduce_dtype)
+    sharded = world > 1 and args.optimizer == "sharded" and args.allreduce_dtype == "fp32"
+    dp = DataParallelTrainer(trainer, overlap=not args.no_overlap, allreduce_dtype=args.allreduce_dtype,
+                             shard_optimizer=sharded)
     if args.graph:
         trainer.set_graph(True)
 
@@ -235,7 +240,8 @@ def main():
             "global_batch": B * world, "per_gpu_batch": B,
             "parallelism": "dp1" if world == 1 else (f"dp{world} batch-sharded ({B_global}/{world} points per rank)" if args.scaling == "strong"
                             else f"dp{world} ({B} points per rank)") +
-                           (f", {args.allreduce_dtype} all-reduce" + ("" if args.no_overlap else " overlapped with the grid backward")
+                           ((", fp32 reduce-scatter + Adam on 1/N of the parameters + fp16 all-gather (sharded optimizer)" if sharded else
+                             f", {args.allreduce_dtype} all-reduce" + ("" if args.no_overlap else " overlapped with the grid backward"))
                             if world > 1 else ""),
         },
         "step_graph": bool(args.graph),

@@ -125,6 +125,10 @@ int tcnn_trainer_training_step(tcnn_trainer* t, void* stream, uint32_t n, const 
 int tcnn_trainer_training_step_part(tcnn_trainer* t, void* stream, uint32_t n, const float* input, const float* target, int part);
 /* Trainer::optimizer_step(stream, loss_scale) (trainer.h:155-157) */
 int tcnn_trainer_optimizer_step(tcnn_trainer* t, void* stream);
+/* Adam on parameters [begin, end) only, counting as one optimizer step (data-parallel sharded
+ * optimizer: each rank updates its shard of the reduce-scattered gradient sums; the caller then
+ * all-gathers the fp16 parameters). Not in the reference, which has no multi-GPU path. */
+int tcnn_trainer_optimizer_step_range(tcnn_trainer* t, void* stream, uint64_t begin, uint64_t end);
 /* Trainer::loss(stream, ctx) of the last training step (trainer.h:205-207); synchronises `stream`. */
 float tcnn_trainer_loss(tcnn_trainer* t, void* stream);
 /* Device pointer to the last step's loss sum (fp32 scalar), for graph-friendly readback. */

@@ -360,6 +360,9 @@ int tcnn_trainer_training_step_part(tcnn_trainer* t, void* stream, uint32_t n, c
 int tcnn_trainer_optimizer_step(tcnn_trainer* t, void* stream) {
 	return guard([&] { t->t->optimizer_step((hipStream_t)stream); });
 }
+int tcnn_trainer_optimizer_step_range(tcnn_trainer* t, void* stream, uint64_t begin, uint64_t end) {
+	return guard([&] { t->t->optimizer_step_range((hipStream_t)stream, begin, end); });
+}
 float tcnn_trainer_loss(tcnn_trainer* t, void* stream) {
 	float v = -1.0f;
 	if (guard([&] { v = t->t->loss((hipStream_t)stream); }) != 0) return -1.0f;

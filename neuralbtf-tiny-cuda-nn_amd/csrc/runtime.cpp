@@ -1137,6 +1137,16 @@ void TrainerHost::optimizer_step(hipStream_t st) {  // AdamOptimizer::step, adam
 	ws.wimage_valid = false;
 }
 
+void TrainerHost::optimizer_step_range(hipStream_t st, uint64_t begin, uint64_t end) {
+	TCNN_CHECK(begin <= end && end <= n_params, "optimizer_step_range: range outside the parameter vector");
+	++adam_step;
+	AdamArgs a = adam_args_table(st, adam_step);
+	a.begin = (uint32_t)begin;
+	a.n = (uint32_t)end;
+	launch_adam(st, a, w32.as<float>(), w16.p, g32.as<float>(), g16.p, m1.as<float>(), m2.as<float>(), steps.as<uint32_t>());
+	ws.wimage_valid = false;
+}
+
 float TrainerHost::loss(hipStream_t st) {
 	float v = 0.0f;
 	TCNN_HIP_CHECK(hipMemcpyAsync(&v, d_loss.p, 4, hipMemcpyDeviceToHost, st));

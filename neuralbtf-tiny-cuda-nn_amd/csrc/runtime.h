@@ -282,6 +282,9 @@ struct TrainerHost {
 	void training_step(hipStream_t st, uint32_t B, const float* input, const float* target, bool run_optimizer);
 	void training_step_part(hipStream_t st, uint32_t B, const float* input, const float* target, int part);
 	void optimizer_step(hipStream_t st);
+	// Adam on parameters [begin, end) only (data-parallel sharded optimizer: each rank updates its
+	// shard of the reduce-scattered gradient, then the fp16 parameters are all-gathered)
+	void optimizer_step_range(hipStream_t st, uint64_t begin, uint64_t end);
 	float loss(hipStream_t st);
 	void inference(hipStream_t st, uint32_t B, const float* input, float* out);
 	void set_params_full_precision(const float* host, uint64_t n);

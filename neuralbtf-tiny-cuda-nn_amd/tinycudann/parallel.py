@@ -20,6 +20,16 @@ to fp16 (the reference's gradient buffer is __half, trainer.h:327), the fp16 sum
 collective, and Adam reads it with scale 1. The default fp32 exchange keeps the single-GPU
 numerics (one fp16 rounding of the reduced sum).
 
+shard_optimizer=True (ZeRO-1 style; the default of bench.py for N > 1): instead of the all-reduce,
+the fp32 gradient sums are reduce-scattered (each rank receives the sum of one contiguous 1/N of the
+parameter vector), each rank runs Adam on its shard only (Trainer.optimizer_step_range, grad scale
+1/N), and the updated fp16 parameters -- what the next step's kernels read -- are all-gathered.
+Per step that moves (N-1)/N of 4 + 2 bytes per parameter instead of 2 (N-1)/N of 4, and Adam, whose
+cost does not shrink with the per-rank batch (36 B per parameter), runs on 1/N of the parameters.
+The fp32 master weights and Adam moments stay sharded (each rank's are current on its own shard);
+gather_master() all-gathers the fp32 master weights, e.g. before a snapshot. For two ranks the
+result is bit-identical to the all-reduce schedule (a + b is the same sum either way).
+
 Batch sharding: strong scaling splits one global batch into contiguous shards (shard_bounds);
 weak scaling gives every rank its own full batch. Both use the same step.
 """
@@ -50,14 +60,30 @@ def shard(x, rank, world):
 class DataParallelTrainer:
     """Wraps tinycudann.Trainer: training_step = local fwd/bwd, all-reduce (overlapped), Adam."""
 
-    def __init__(self, trainer, group=None, overlap=True, allreduce_dtype="fp32"):
+    def __init__(self, trainer, group=None, overlap=True, allreduce_dtype="fp32", shard_optimizer=False):
         assert allreduce_dtype in ("fp32", "fp16")
+        assert not (shard_optimizer and allreduce_dtype == "fp16"), "the sharded optimizer exchanges fp32 gradient sums"
         self.trainer = trainer
         self.group = group
         self.overlap = overlap
         self.dtype = allreduce_dtype
+        self.shard_optimizer = shard_optimizer
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        if self.world > 1:
+        if self.world > 1 and shard_optimizer:
+            self.rank = dist.get_rank(group)
+            n = trainer.n_params
+            self._per = (n + self.world - 1) // self.world
+            padded = self._per * self.world
+            self._lo = min(n, self.rank * self._per)
+            self._hi = min(n, self._lo + self._per)
+            self._grad = trainer.gradients_fp32()
+            self._w16 = trainer.params()
+            self._gpad = torch.zeros(padded, dtype=torch.float32, device=self._grad.device)
+            self._gshard = torch.empty(self._per, dtype=torch.float32, device=self._grad.device)
+            self._wpad = torch.zeros(padded, dtype=torch.float16, device=self._grad.device)
+            self._wshard = torch.zeros(self._per, dtype=torch.float16, device=self._grad.device)
+            trainer.set_gradient_scale(1.0 / self.world)
+        elif self.world > 1:
             self._grad = trainer.gradients_fp32()
             nm = trainer.n_network_params
             self._views = (self._grad[:nm], self._grad[nm:])
@@ -75,9 +101,39 @@ class DataParallelTrainer:
             return dist.all_reduce(self._hviews[k], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         return dist.all_reduce(self._views[k], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
+    def _sharded_step(self, input, target):
+        t, n = self.trainer, self.trainer.n_params
+        t.training_step(input, target, run_optimizer=False)
+        self._gpad[:n].copy_(self._grad)
+        dist.reduce_scatter_tensor(self._gshard, self._gpad, op=dist.ReduceOp.SUM, group=self.group)
+        if self._hi > self._lo:
+            self._grad[self._lo:self._hi].copy_(self._gshard[:self._hi - self._lo])
+        t.optimizer_step_range(self._lo, self._hi)
+        if self._hi > self._lo:
+            self._wshard[:self._hi - self._lo].copy_(self._w16[self._lo:self._hi])
+        dist.all_gather_into_tensor(self._wpad, self._wshard, group=self.group)
+        self._w16.copy_(self._wpad[:n])
+
+    def gather_master(self):
+        """All-gather the fp32 master weights (sharded under shard_optimizer) so every rank holds
+        the full vector, e.g. before serialize()."""
+        if self.world == 1 or not self.shard_optimizer:
+            return
+        n = self.trainer.n_params
+        w32 = self.trainer.params_fp32()
+        buf = torch.zeros(self._per * self.world, dtype=torch.float32, device=w32.device)
+        mine = torch.zeros(self._per, dtype=torch.float32, device=w32.device)
+        if self._hi > self._lo:
+            mine[:self._hi - self._lo].copy_(w32[self._lo:self._hi])
+        dist.all_gather_into_tensor(buf, mine, group=self.group)
+        w32.copy_(buf[:n])
+
     def training_step(self, input, target):
         if self.world == 1:
             self.trainer.training_step(input, target, run_optimizer=True)
+            return
+        if self.shard_optimizer:
+            self._sharded_step(input, target)
             return
         if self.overlap:
             self.trainer.training_step_part(input, target, 0)

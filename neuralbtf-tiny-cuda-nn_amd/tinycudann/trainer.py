@@ -48,6 +48,10 @@ class Trainer:
     def optimizer_step(self, stream=None):
         L.check(L.lib().tcnn_trainer_optimizer_step(self.h, _stream(stream)))
 
+    def optimizer_step_range(self, begin, end, stream=None):
+        """Adam on parameters [begin, end) only (one optimizer step; data-parallel sharded optimizer)."""
+        L.check(L.lib().tcnn_trainer_optimizer_step_range(self.h, _stream(stream), int(begin), int(end)))
+
     def loss(self, stream=None):
         v = L.lib().tcnn_trainer_loss(self.h, _stream(stream))
         if v < 0:

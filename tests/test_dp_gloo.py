@@ -111,6 +111,29 @@ class _FakeTrainer:
         self.seen = (self.g * self.scale).clone()
 
 
+class _FakeShardTrainer(_FakeTrainer):
+    """Adds what the sharded optimizer uses: fp16 parameter view, fp32 masters and a ranged Adam
+    that writes the gradient it reads (x grad scale) into both."""
+
+    def __init__(self, rank, n_net=8, n=41):
+        super().__init__(rank, n_net, n)
+        self.n_params = n
+        self.w16 = torch.zeros(n, dtype=torch.float16)
+        self.w32 = torch.zeros(n, dtype=torch.float32)
+        self.ranges = []
+
+    def params(self):
+        return self.w16
+
+    def params_fp32(self):
+        return self.w32
+
+    def optimizer_step_range(self, lo, hi):
+        self.ranges.append((lo, hi))
+        self.w32[lo:hi] = self.g[lo:hi] * self.scale
+        self.w16[lo:hi] = self.w32[lo:hi].half()
+
+
 def _sched_worker(rank, world, port, out_q):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
@@ -127,6 +150,12 @@ def _sched_worker(rank, world, port, out_q):
             dp = DataParallelTrainer(t, overlap=overlap, allreduce_dtype=dtype)
             dp.training_step(None, None)
             res[(overlap, dtype)] = (t.seen.numpy(), t.parts)
+    t = _FakeShardTrainer(rank)
+    dp = DataParallelTrainer(t, shard_optimizer=True)
+    dp.training_step(None, None)
+    w16 = t.w16.clone()
+    dp.gather_master()
+    res["zero"] = (w16.float().numpy(), t.w32.numpy(), t.ranges)
     x = torch.arange(10 * 3).reshape(10, 3)
     res["shard"] = shard(x, rank, world).numpy()
     out_q.put((rank, res))
@@ -161,3 +190,12 @@ def test_two_rank_exchange_schedule_and_sharding():
         h = [((idx + 1) * (k + 1) * np.float32(0.37) / 2).astype(np.float16) for k in range(world)]
         np.testing.assert_array_equal(g16, (h[0] + h[1]).astype(np.float32))
     np.testing.assert_array_equal(np.concatenate([res[0]["shard"], res[1]["shard"]]), np.arange(30).reshape(10, 3))
+    # sharded optimizer over 41 parameters (padded to 42): rank 0 updates [0, 21), rank 1 [21, 41);
+    # afterwards every rank holds the whole fp16 vector and, after gather_master, the fp32 one
+    idx41 = np.arange(41, dtype=np.float32)
+    mean41 = ((idx41 + 1) * np.float32(0.37) + (idx41 + 1) * 2 * np.float32(0.37)) / 2
+    for r in range(world):
+        w16, w32, ranges = res[r]["zero"]
+        assert ranges == [(0, 21)] if r == 0 else ranges == [(21, 41)]
+        np.testing.assert_allclose(w32, mean41, rtol=1e-6)
+        np.testing.assert_array_equal(w16, w32.astype(np.float16).astype(np.float32))

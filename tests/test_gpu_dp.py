@@ -1,7 +1,8 @@
 """Data-parallel path of the HIP engine with two ranks on one GPU (gloo all-reduce on device
 tensors; the 8-GPU RCCL run is the driver's): shard gradients summed by
 tinycudann.parallel.allreduce_gradients and scaled 1/N equal the single-process full-batch
-gradient, and DataParallelTrainer keeps both replicas bit-identical."""
+gradient, and DataParallelTrainer keeps both replicas bit-identical under every
+exchange schedule (overlapped, plain, pre-divided fp16, sharded optimizer)."""
 import os
 import socket
 
@@ -42,18 +43,22 @@ def _worker(rank, world, port, B, q):
     scale = allreduce_gradients(g)
     g_avg = (g * scale).cpu().numpy()
     # full DataParallelTrainer steps on a fresh replica
-    def run(**kw):
+    def run(gather=False, **kw):
         tr2 = Trainer(2, 3, CONFIG_HASH, seed=1337)
         dp = DataParallelTrainer(tr2, **kw)
         for s in range(3):
             pos_s, tgt_s = make_batch(B, step=s)
             dp.training_step(torch.from_numpy(pos_s[lo:hi]).cuda(), torch.from_numpy(tgt_s[lo:hi]).cuda())
+        if gather:
+            dp.gather_master()
         torch.cuda.synchronize()
-        return trainer_arrays(tr2)["w32"]
-    w_over = run()                            # two-part step, network all-reduce overlapping the grid backward
-    w_plain = run(overlap=False)              # whole backward, then the all-reduce
-    w_half = run(allreduce_dtype="fp16")      # pre-divided fp16 exchange
-    q.put((rank, g_avg, w_over, w_plain, w_half))
+        a = trainer_arrays(tr2)
+        return a["w32"], a["w16"]
+    w_over = run()[0]                         # two-part step, network all-reduce overlapping the grid backward
+    w_plain = run(overlap=False)[0]           # whole backward, then the all-reduce
+    w_half = run(allreduce_dtype="fp16")[0]   # pre-divided fp16 exchange
+    w_shard, h_shard = run(gather=True, shard_optimizer=True)  # reduce-scatter, Adam on 1/N, all-gather
+    q.put((rank, g_avg, w_over, w_plain, w_half, w_shard, h_shard, run()[1]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -80,6 +85,11 @@ def test_two_rank_gpu_allreduce_matches_full_batch():
     # skipped by Adam (adam.h:76-79) in one run only, so parameters differ by ~lr in a few places
     assert rel_err(res[0][4], res[0][2]) < 1e-2
     np.testing.assert_array_equal(res[0][1], res[1][1])
+    # sharded optimizer (reduce-scatter, Adam on each rank's half, fp16 all-gather): bit-identical to
+    # the all-reduce schedule for two ranks -- fp16 parameters, and the gathered fp32 masters
+    for r in range(world):
+        np.testing.assert_array_equal(res[r][6], res[r][7])
+        np.testing.assert_array_equal(res[r][5], res[0][2])
     from tinycudann import Trainer
     pos, tgt = make_batch(B)
     t = Trainer(2, 3, CONFIG_HASH, seed=1337)
