@@ -212,10 +212,15 @@ void launch_reduce_partials(hipStream_t st, const float* in, uint32_t n_parts, u
 uint32_t tile_train_lds_bytes(uint32_t W, uint32_t IN, uint32_t NH);
 bool tile_train_supported(uint32_t W, uint32_t IN, uint32_t NH, uint32_t outp, int act);
 uint32_t tile_train_blocks(uint32_t B);
+// hidden matrices whose weights do not fit the LDS beside the rest (e.g. W128/H5/IN128: 2) are read from
+// L2; their transposed copy needs tile_train_wT_bytes of device memory (0: every matrix is staged)
+uint32_t tile_train_n_streamed(uint32_t W, uint32_t IN, uint32_t NH);
+uint32_t tile_train_wT_bytes(uint32_t W, uint32_t IN, uint32_t NH);
 // dldenc (optional): dL/d(encoding) as level-major pairs [IN/2][B] (dldenc_pairs) or AoS fp16 [B][IN]
+// wT: tile_train_wT_bytes of scratch (nullptr when 0), rewritten from params16 by this launch
 void launch_mlp_tile_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, int act, uint32_t B, uint32_t dims, float loss_scale,
                            uint32_t loss_l2, const void* params16, const void* enc16, const float* target, const void* dout16, void* out16,
-                           void* dldenc, int dldenc_pairs, float* wgrad_partial, float* loss_partial);
+                           void* dldenc, int dldenc_pairs, float* wgrad_partial, float* loss_partial, void* wT);
 
 // generate_random_uniform<float> (random.h:57-70) from pcg32 {state, inc} (not advanced here)
 void launch_generate_uniform(hipStream_t st, uint64_t n, uint64_t state, uint64_t inc, float* out, float lo, float hi);

@@ -24,6 +24,20 @@
 
 namespace tcnn_amd {
 
+// LDS halves of a tile workgroup with the first NS hidden matrices streamed from L2 instead of staged
+constexpr int tile_halves(int W, int IN, int NH, int NS) {
+	const int KP0 = (IN + 31) / 32 * 32, RS0 = KP0 + 8, RSW = W + 8, RSG = 24;
+	return W * RS0 + (NH - 1 - NS) * W * RSW + 16 * RSW + 32 * RS0 + NH * 32 * RSW + 32 * RSG;
+}
+constexpr int tile_waves(int W) { return W == 128 ? 8 : 4; }
+constexpr int tile_lds_limit() { return 160 * 1024; }
+// fewest streamed hidden matrices that let the rest of the network + the tile's activations fit
+constexpr int tile_n_streamed(int W, int IN, int NH) {
+	int ns = 0;
+	while (ns < NH - 1 && tile_halves(W, IN, NH, ns) * 2 + tile_waves(W) * 4 > tile_lds_limit()) ++ns;
+	return ns;
+}
+
 template <int W, int IN, int NH>
 struct TileLayout {
 	static_assert(W == 64 || W == 128, "tile engine: W in {64, 128}");
@@ -32,16 +46,20 @@ struct TileLayout {
 	static constexpr int RS0 = KP0 + 8, RSW = W + 8, RSG = 24;
 	// W128 runs 8 waves (2 per SIMD: each owns one 16-row tile of every matrix, 108 accumulator
 	// registers), W64 4 waves; either way one output-row tile per wave
-	static constexpr int WAVES = W == 128 ? 8 : 4, NTHR = WAVES * 64;
+	static constexpr int WAVES = tile_waves(W), NTHR = WAVES * 64;
 	static constexpr int MT = W / 16, MTW = MT / WAVES;  // output-row tiles per matrix / per wave
 	static constexpr int KT0 = IN / 16;              // feature tiles of the input
-	static constexpr int oW0 = 0, oWh = oW0 + W * RS0, oWo = oWh + (NH - 1) * W * RSW;
+	// hidden matrices 1..NS are not staged: their forward A fragments come from the fp16 parameters
+	// (L2-resident, every workgroup reads the same 32 KB), their backward ones from a transposed copy
+	static constexpr int NS = tile_n_streamed(W, IN, NH);
+	static constexpr int oW0 = 0, oWh = oW0 + W * RS0, oWo = oWh + (NH - 1 - NS) * W * RSW;
 	static constexpr int oX = oWo + 16 * RSW;                 // slot 0: the tile's input [32][RS0]
 	static constexpr int oA = oX + 32 * RS0;                  // slots 1..NH: [32][RSW]
 	static constexpr int oG = oA + NH * 32 * RSW;             // dL/dy of the tile [32][RSG]
 	static constexpr int HALVES = oG + 32 * RSG;
 	static constexpr int BYTES = HALVES * 2 + WAVES * 4;       // + per-wave loss
 	static constexpr int N_MLP = W * IN + (NH - 1) * W * W + 16 * W;
+	static_assert(HALVES == tile_halves(W, IN, NH, NS), "layout");
 	static_assert(oWh % 8 == 0 && oWo % 8 == 0 && oX % 8 == 0 && oA % 8 == 0 && oG % 8 == 0, "16-byte alignment");
 };
 
@@ -49,6 +67,7 @@ struct TileTrainArgs {
 	uint32_t B, dims, loss_l2;
 	float loss_scale, n_total;
 	const _Float16* params;  // [W0 | hidden | Wout] fp16
+	const _Float16* wT;      // streamed hidden matrices 1..NS transposed, [NS][W (in)][W (out)] fp16
 	const _Float16* enc;     // encoded input fp16 [B][IN]
 	const float* target;     // [B][dims] (loss)
 	const _Float16* dout;    // external dL/d(output) fp16 [B][16] (EXT_DOUT, loss-scaled by the caller)
@@ -86,9 +105,9 @@ __global__ __launch_bounds__((W == 128 ? 512 : 256), 1) void k_mlp_tile_train(co
 			*(h8*)(smem + L::oW0 + r * RS0 + 8 * c8) = 8 * c8 < IN ? *(const h8*)(p + (size_t)r * IN + 8 * c8) : zero8();
 		}
 		p += W * IN;
-		for (int idx = tid; idx < (NH - 1) * W * (W / 8); idx += NTHR) {
-			const int r = idx / (W / 8), c8 = idx % (W / 8);  // r over all hidden rows
-			*(h8*)(smem + L::oWh + r * RSW + 8 * c8) = *(const h8*)(p + (size_t)r * W + 8 * c8);
+		for (int idx = tid; idx < (NH - 1 - L::NS) * W * (W / 8); idx += NTHR) {
+			const int r = idx / (W / 8), c8 = idx % (W / 8);  // r over the staged hidden rows
+			*(h8*)(smem + L::oWh + r * RSW + 8 * c8) = *(const h8*)(p + (size_t)(L::NS * W + r) * W + 8 * c8);
 		}
 		p += (NH - 1) * W * W;
 		for (int idx = tid; idx < 16 * (W / 8); idx += NTHR) {
@@ -100,7 +119,9 @@ __global__ __launch_bounds__((W == 128 ? 512 : 256), 1) void k_mlp_tile_train(co
 			for (int idx = tid; idx < 32 * (L::KP0 - IN); idx += NTHR)
 				smem[L::oX + (idx / (L::KP0 - IN)) * RS0 + IN + idx % (L::KP0 - IN)] = (_Float16)0.0f;
 	}
-	auto Wm = [&](int m) -> const _Float16* { return m == 0 ? smem + L::oW0 : smem + L::oWh + (m - 1) * W * RSW; };
+	// staged matrices (m == 0 or m > NS); streamed ones (1 <= m <= NS) are read from global memory
+	auto Wm = [&](int m) -> const _Float16* { return m == 0 ? smem + L::oW0 : smem + L::oWh + (m - 1 - L::NS) * W * RSW; };
+	auto streamed = [](int m) { return m >= 1 && m <= L::NS; };
 	auto slot = [&](int m) -> _Float16* { return m == 0 ? smem + L::oX : smem + L::oA + (m - 1) * 32 * RSW; };
 	_Float16* sG = smem + L::oG;
 
@@ -165,18 +186,26 @@ __global__ __launch_bounds__((W == 128 ? 512 : 256), 1) void k_mlp_tile_train(co
 		for (int m = 0; m < NH; ++m) {
 			const int KS = (m == 0 ? L::KP0 : W) / 32;
 			const int rsi = m == 0 ? RS0 : RSW;
-			const _Float16* Wt = Wm(m);
+			const _Float16* Wt = streamed(m) ? nullptr : Wm(m);
 			const _Float16* in = slot(m);
 			f4 acc[MTW][2];
 #pragma unroll
 			for (int i = 0; i < MTW; ++i) acc[i][0] = acc[i][1] = fz;
+			h8 ag[MTW][W / 32];  // a streamed layer's A fragments, all loads issued before the first MFMA
+			if (streamed(m)) {
+				const _Float16* Wg = a.params + (size_t)W * IN + (size_t)(m - 1) * W * W;
+#pragma unroll
+				for (int i = 0; i < MTW; ++i)
+#pragma unroll
+					for (int s = 0; s < W / 32; ++s) ag[i][s] = *(const h8*)(Wg + (size_t)(16 * (wave * MTW + i) + c) * W + 32 * s + 8 * q);
+			}
 #pragma unroll
 			for (int s = 0; s < KS; ++s) {
 				const h8 b0 = *(const h8*)(in + c * rsi + 32 * s + 8 * q);
 				const h8 b1 = *(const h8*)(in + (16 + c) * rsi + 32 * s + 8 * q);
 #pragma unroll
 				for (int i = 0; i < MTW; ++i) {
-					const h8 af = *(const h8*)(Wt + (16 * (wave * MTW + i) + c) * rsi + 32 * s + 8 * q);
+					const h8 af = streamed(m) ? ag[i][s] : *(const h8*)(Wt + (16 * (wave * MTW + i) + c) * rsi + 32 * s + 8 * q);
 					acc[i][0] = mfma16(af, b0, acc[i][0]);
 					acc[i][1] = mfma16(af, b1, acc[i][1]);
 				}
@@ -261,6 +290,16 @@ __global__ __launch_bounds__((W == 128 ? 512 : 256), 1) void k_mlp_tile_train(co
 			const _Float16* dsl = slot(m + 1);  // delta_{m+1} [sample][neuron]
 			const _Float16* am = slot(m);       // a_m [sample][feature]
 			const int rsm = m == 0 ? RS0 : RSW;
+			// a streamed matrix's transposed A fragments (A[feature][neuron] = M^T rows of this wave's
+			// tiles), loaded ahead so the latency hides behind the weight-gradient MFMAs
+			h8 agT[MTW][W / 32];
+			if (streamed(m)) {
+				const _Float16* WgT = a.wT + (size_t)(m - 1) * W * W;
+#pragma unroll
+				for (int i = 0; i < MTW; ++i)
+#pragma unroll
+					for (int s = 0; s < W / 32; ++s) agT[i][s] = *(const h8*)(WgT + (size_t)(16 * (wave * MTW + i) + c) * W + 32 * s + 8 * q);
+			}
 			// dW_m += delta_{m+1} a_m^T (contraction over the tile's 32 samples)
 #pragma unroll
 			for (int i = 0; i < MTW; ++i) {
@@ -274,7 +313,7 @@ __global__ __launch_bounds__((W == 128 ? 512 : 256), 1) void k_mlp_tile_train(co
 				}
 			}
 			// delta_m = act'(a_m) * (M_m^T delta_{m+1})  (m == 0: dL/d(encoding), no transfer)
-			const _Float16* Mt = Wm(m);
+			const _Float16* Mt = streamed(m) ? nullptr : Wm(m);
 			if (m > 0) {
 #pragma unroll
 				for (int i = 0; i < MTW; ++i) {
@@ -282,7 +321,7 @@ __global__ __launch_bounds__((W == 128 ? 512 : 256), 1) void k_mlp_tile_train(co
 					f4 v0 = fz, v1 = fz;
 #pragma unroll
 					for (int s = 0; s < W / 32; ++s) {
-						const h8 af = lds_trfrag(Mt + 32 * s * rsm, rsm, q, c, t);  // A[feature][neuron 32s+8q+e]
+						const h8 af = streamed(m) ? agT[i][s] : lds_trfrag(Mt + 32 * s * rsm, rsm, q, c, t);  // A[feature][neuron 32s+8q+e]
 						v0 = mfma16(af, *(const h8*)(dsl + c * RSW + 32 * s + 8 * q), v0);
 						v1 = mfma16(af, *(const h8*)(dsl + (16 + c) * RSW + 32 * s + 8 * q), v1);
 					}
@@ -364,8 +403,10 @@ __global__ __launch_bounds__((W == 128 ? 512 : 256), 1) void k_mlp_tile_train(co
 	X(64, 32, 1) X(64, 32, 2) X(64, 32, 3) X(64, 32, 4) X(64, 32, 5) \
 	X(64, 64, 2) X(64, 64, 3) X(64, 64, 4) X(64, 64, 5) \
 	X(64, 128, 2) X(64, 128, 3) X(64, 128, 4) X(64, 128, 5) \
-	X(128, 16, 2) X(128, 16, 3) X(128, 16, 4) \
-	X(128, 32, 1) X(128, 32, 2) X(128, 32, 3) X(128, 32, 4)
+	X(128, 16, 2) X(128, 16, 3) X(128, 16, 4) X(128, 16, 5) \
+	X(128, 32, 1) X(128, 32, 2) X(128, 32, 3) X(128, 32, 4) X(128, 32, 5) \
+	X(128, 64, 2) X(128, 64, 3) X(128, 64, 4) X(128, 64, 5) \
+	X(128, 128, 2) X(128, 128, 3) X(128, 128, 4) X(128, 128, 5)
 
 uint32_t tile_train_lds_bytes(uint32_t W, uint32_t IN, uint32_t NH) {
 #define X(w, in, nh) \
@@ -373,6 +414,24 @@ uint32_t tile_train_lds_bytes(uint32_t W, uint32_t IN, uint32_t NH) {
 	TILE_SHAPES(X)
 #undef X
 	return 0;
+}
+
+uint32_t tile_train_n_streamed(uint32_t W, uint32_t IN, uint32_t NH) {
+#define X(w, in, nh) \
+	if (W == w && IN == in && NH == nh) return (uint32_t)TileLayout<w, in, nh>::NS;
+	TILE_SHAPES(X)
+#undef X
+	return 0;
+}
+
+uint32_t tile_train_wT_bytes(uint32_t W, uint32_t IN, uint32_t NH) { return tile_train_n_streamed(W, IN, NH) * W * W * 2; }
+
+// transposed copy of the streamed hidden matrices 1..NS: wT[j][f][n] = M_{j+1}[n][f]
+__global__ void k_tile_transpose_hidden(const _Float16* __restrict__ hidden, _Float16* __restrict__ wT, uint32_t W, uint32_t n) {
+	const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+	if (idx >= n) return;
+	const uint32_t j = idx / (W * W), r = idx % (W * W), f = r / W, o = r % W;
+	wT[idx] = hidden[(size_t)j * W * W + (size_t)o * W + f];
 }
 
 bool tile_train_supported(uint32_t W, uint32_t IN, uint32_t NH, uint32_t outp, int act) {
@@ -396,7 +455,7 @@ uint32_t tile_train_blocks(uint32_t B) { return std::max(1u, std::min(256u, B / 
 
 void launch_mlp_tile_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, int act, uint32_t B, uint32_t dims, float loss_scale,
                            uint32_t loss_l2, const void* params16, const void* enc16, const float* target, const void* dout16, void* out16,
-                           void* dldenc, int dldenc_pairs, float* wgrad_partial, float* loss_partial) {
+                           void* dldenc, int dldenc_pairs, float* wgrad_partial, float* loss_partial, void* wT) {
 	TCNN_CHECK(B % 32 == 0, "tile train: batch must be a multiple of 32");
 	TCNN_CHECK(tile_train_supported(W, IN, NH, 16, act), "tile train: unsupported shape");
 	TCNN_CHECK(dout16 || dims <= 16, "tile train: at most 16 outputs");
@@ -408,6 +467,14 @@ void launch_mlp_tile_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH,
 	a.loss_scale = loss_scale;
 	a.n_total = (float)((uint64_t)B * dims);
 	a.params = (const _Float16*)params16;
+	const uint32_t ns = tile_train_n_streamed(W, IN, NH);
+	if (ns) {
+		TCNN_CHECK(wT != nullptr, "tile train: streamed hidden matrices need the transposed-weight buffer");
+		const uint32_t n = ns * W * W;
+		hipLaunchKernelGGL(k_tile_transpose_hidden, dim3((n + 255) / 256), dim3(256), 0, st, (const _Float16*)params16 + (size_t)W * IN,
+		                   (_Float16*)wT, W, n);
+	}
+	a.wT = (const _Float16*)wT;
 	a.enc = (const _Float16*)enc16;
 	a.target = target;
 	a.dout = (const _Float16*)dout16;

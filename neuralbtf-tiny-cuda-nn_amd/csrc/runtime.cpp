@@ -661,8 +661,11 @@ void NetworkHost::fwd_bwd_tile(hipStream_t st, StepWorkspace& ws, uint32_t B, co
 	// a grid with feature pairs and no padding takes dL/d(encoding) as level-major pairs [L][B]
 	const bool pairs = grid && grid->desc.n_features_per_level == 2 && grid->n_to_pad == 0;
 	if (enc_grad) ws.delta0.reserve((size_t)B * IN * 2);
+	const uint32_t wT_bytes = tile_train_wT_bytes(W, IN, NH);
+	if (wT_bytes) ws.tile_wT.reserve(wT_bytes);
 	launch_mlp_tile_train(st, W, IN, NH, mlp.activation, B, dims, loss_scale, loss_l2, params16, ws.enc16.p, target, dout16, out16,
-	                      enc_grad ? ws.delta0.p : nullptr, pairs ? 1 : 0, ws.wgrad_partial.as<float>(), ws.loss_partial.as<float>());
+	                      enc_grad ? ws.delta0.p : nullptr, pairs ? 1 : 0, ws.wgrad_partial.as<float>(), ws.loss_partial.as<float>(),
+	                      wT_bytes ? ws.tile_wT.p : nullptr);
 	ws.n_loss_partials = dout16 ? 0 : nb;
 	const size_t tf = reduce_partials_tmp_floats(nb, n_mlp);
 	if (tf) ws.red_tmp.reserve(tf * 4);

@@ -178,6 +178,7 @@ struct StepWorkspace {
 	DevBuf dLdenc, wgrad_partial, loss_partial, grad32_tmp, out16, enc16, wimage;
 	GridBwdBufs gbw;
 	DevBuf acts, delta0, delta1, dout16, red_tmp;  // layer-wise engine
+	DevBuf tile_wT;  // tile engine: transposed copy of the streamed hidden matrices
 	uint32_t n_fused_blocks = 0, n_loss_partials = 0;
 	bool wimage_valid = false;  // fused weight image matches the current fp16 params (trainer fast path)
 };
@@ -185,7 +186,8 @@ struct StepWorkspace {
 // NetworkWithInputEncoding<__half> (reference network_with_input_encoding.h:41-190) over two engines:
 //   "fused"   grid encoding + W in {32, 64} FullyFusedMLP: one register-resident kernel
 //             (mlp_fused.h) + the LDS-privatised grid backward;
-//   "layered" everything else (W = 128, OneBlob / Identity, CutlassMLP, output activations):
+//   "fused"   (tile) W in {64, 128} FullyFusedMLP with any encoding (mlp_tile.hip);
+//   "layered" everything else (CutlassMLP, other widths, output activations):
 //             per-layer MFMA kernels (mlp_layers.hip) with fp16 activations in HBM.
 struct NetworkHost {
 	std::unique_ptr<EncodingHost> enc;

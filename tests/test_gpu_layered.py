@@ -1,7 +1,9 @@
 """GPU parity of the layer-wise MFMA engine (mlp_layers.hip) and the OneBlob / Identity encodings
 (encodings.hip) against the CPU oracle, on the BASELINE configs the register-resident fused kernel
 does not take: config_oneblob.json as-is (OneBlob 64 bins + FullyFusedMLP W128/H5), its W64/H2
-variant, HashGrid + W128/H4 (the LDS-pressure config), CutlassMLP, Identity.
+variant, HashGrid + W128/H4 (the LDS-pressure config), CutlassMLP, Identity. FullyFusedMLP W64/W128
+shapes train on the tile engine (mlp_tile.hip, engine "fused"), including those whose weights exceed
+the LDS (hidden matrices streamed from L2); the layer-wise engine is also checked on two of them.
 
 Tolerances (north_star: 1e-3 relative, fp16):
   * OneBlob / Identity encodings: bit-exact (same fp32 op sequence, explicit FMAs)
@@ -54,9 +56,16 @@ CONFIGS = {
     "identity_w64_h3": (_cfg({"otype": "Identity"}, _net(64, 3)), 1e-3),
     "oneblob_w64_h5": (_cfg({"otype": "OneBlob", "n_bins": 64}, _net(64, 5)), 2e-3),
     "hashgrid_w128_h2": (_cfg(CONFIG_HASH["encoding"], _net(128, 2)), 1e-3),
+    # tile shapes whose weights exceed the LDS: the first NS hidden matrices are read from L2
+    # (config_oneblob as-is: NS = 2; IN 128 with 4 hidden layers: NS = 1; HashGrid W128/H5: NS = 2)
+    "oneblob_w128_h4": (_cfg({"otype": "OneBlob", "n_bins": 64}, _net(128, 4)), 2e-3),
+    "hashgrid_w128_h5": (_cfg(CONFIG_HASH["encoding"], _net(128, 5)), 2e-3),
 }
 # FullyFusedMLP configurations the tile engine trains (engine "fused"); the rest run layer by layer
-TILE = {"oneblob_w64_h2", "oneblob16_w64_h2", "hashgrid_w128_h4", "identity_w64_h3", "oneblob_w64_h5", "hashgrid_w128_h2"}
+TILE = {"oneblob_w64_h2", "oneblob16_w64_h2", "hashgrid_w128_h4", "identity_w64_h3", "oneblob_w64_h5", "hashgrid_w128_h2",
+        "oneblob_as_file_w128_h5", "oneblob_w128_h4", "hashgrid_w128_h5"}
+# the same shapes with the tile engine switched off run on the layer-wise engine
+LAYERED_AB = ["oneblob_as_file_w128_h5", "hashgrid_w128_h4"]
 
 
 @pytest.mark.parametrize("n_bins,n_in", [(64, 2), (16, 2), (16, 3), (32, 1)])
@@ -115,6 +124,25 @@ def test_layered_step_gradients_and_loss(torch_mod, name):
         assert e_enc <= tol, e_enc
 
 
+@pytest.mark.parametrize("name", LAYERED_AB)
+def test_layered_engine_forced_matches_oracle(torch_mod, name, monkeypatch):
+    """The layer-wise engine keeps its parity on the shapes the tile engine now takes
+    (TCNN_NO_TILE_ENGINE is read when the trainer is built)."""
+    torch = torch_mod
+    from tinycudann import Trainer
+    monkeypatch.setenv("TCNN_NO_TILE_ENGINE", "1")
+    cfg, tol = CONFIGS[name]
+    t = Trainer(2, 3, cfg, seed=1337)
+    assert t.engine == "layered", t.engine
+    om = O.OracleModel(cfg, 2, 3, seed=1337)
+    pos, tgt = make_batch(512)
+    t.training_step(torch.from_numpy(pos).cuda(), torch.from_numpy(tgt).cuda(), run_optimizer=False)
+    loss_ref = om.train_step(pos, tgt, run_optimizer=False, n_threads=4)
+    assert abs(t.loss() - loss_ref) <= 1e-3 * abs(loss_ref)
+    a = trainer_arrays(t)
+    assert rel_err(a["g32"], om.grad32) <= tol
+
+
 @pytest.mark.parametrize("name", ["oneblob_as_file_w128_h5", "hashgrid_w128_h4", "identity_w32_h3"])
 def test_layered_inference_matches_oracle(torch_mod, name):
     torch = torch_mod
@@ -128,7 +156,7 @@ def test_layered_inference_matches_oracle(torch_mod, name):
     assert_within_fp16_ulps(out, ref)
 
 
-@pytest.mark.parametrize("name", ["oneblob_as_file_w128_h5", "hashgrid_w128_h4", "oneblob_w64_h5"])
+@pytest.mark.parametrize("name", ["oneblob_as_file_w128_h5", "hashgrid_w128_h4", "oneblob_w64_h5", "hashgrid_w128_h5"])
 def test_layered_training_trajectory_tracks_oracle(torch_mod, name):
     torch = torch_mod
     from tinycudann import Trainer

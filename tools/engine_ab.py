@@ -1,6 +1,7 @@
 """A/B timing of the tile engine (mlp_tile.hip) against the layer-wise engine (TCNN_NO_TILE_ENGINE=1)
 on the BASELINE configs it takes: configs[3] (HashGrid + W128/H4, B=2^20), configs[1] (OneBlob 64
-bins + W64/H2, B=2^18), config_oneblob with W64 (H5), the sample's default (OneBlob 32 bins, W64/H4).
+bins + W64/H2, B=2^18), config_oneblob with W64 (H5), the sample's default (OneBlob 32 bins, W64/H4),
+config_oneblob as-is (W128/H5, IN 128) and HashGrid + W128/H5 (hidden matrices streamed from L2).
 Training steps (forward, loss, backward, Adam) timed with torch.cuda events after warm-up.
 
   python tools/engine_ab.py [--out profiles/r02_engine_ab.json]
@@ -36,6 +37,11 @@ def main():
     c = copy.deepcopy(ob); c["network"] = net(64, 5); cases.append(("config_oneblob W64/H5", c, 18))
     c = copy.deepcopy(ob); c["encoding"] = {"otype": "OneBlob", "n_bins": 32}; c["network"] = net(64, 4)
     cases.append(("sample default OneBlob32+W64/H4", c, 18))
+    # shapes whose weights exceed the LDS: hidden matrices 1..NS streamed from L2 (mlp_tile.hip)
+    cases.append(("config_oneblob as-is OneBlob64+W128/H5 (IN 128, 2 streamed)", copy.deepcopy(ob), 18))
+    c = copy.deepcopy(hash_cfg); c["network"] = net(128, 5); cases.append(("HashGrid+W128/H5 (2 streamed)", c, 20))
+    if os.environ.get("AB_ONLY_STREAMED"):
+        cases = cases[-2:]
     rows = []
     for name, cfg, lb in cases:
         B = 1 << lb
