@@ -29,12 +29,15 @@ constexpr int tile_halves(int W, int IN, int NH, int NS) {
 	const int KP0 = (IN + 31) / 32 * 32, RS0 = KP0 + 8, RSW = W + 8, RSG = 24;
 	return W * RS0 + (NH - 1 - NS) * W * RSW + 16 * RSW + 32 * RS0 + NH * 32 * RSW + 32 * RSG;
 }
-constexpr int tile_waves(int W) { return W == 128 ? 8 : 4; }
+// W128 runs 8 waves (2 per SIMD, one 16-row tile of every matrix each) up to 4 hidden layers; with 5
+// its weight-gradient accumulators (>= 164 registers) spill at 256 registers per wave, so it runs 4
+// waves (1 per SIMD, 512 registers incl. AGPRs, two row tiles each: half the activation LDS reads)
+constexpr int tile_waves(int W, int NH) { return W == 128 && NH < 5 ? 8 : 4; }
 constexpr int tile_lds_limit() { return 160 * 1024; }
 // fewest streamed hidden matrices that let the rest of the network + the tile's activations fit
 constexpr int tile_n_streamed(int W, int IN, int NH) {
 	int ns = 0;
-	while (ns < NH - 1 && tile_halves(W, IN, NH, ns) * 2 + tile_waves(W) * 4 > tile_lds_limit()) ++ns;
+	while (ns < NH - 1 && tile_halves(W, IN, NH, ns) * 2 + tile_waves(W, NH) * 4 > tile_lds_limit()) ++ns;
 	return ns;
 }
 
@@ -44,9 +47,7 @@ struct TileLayout {
 	static_assert(IN % 16 == 0 && IN <= 128, "tile engine: IN a multiple of 16, <= 128");
 	static constexpr int KP0 = (IN + 31) / 32 * 32;  // K of the first layer, padded to the MFMA depth
 	static constexpr int RS0 = KP0 + 8, RSW = W + 8, RSG = 24;
-	// W128 runs 8 waves (2 per SIMD: each owns one 16-row tile of every matrix, 108 accumulator
-	// registers), W64 4 waves; either way one output-row tile per wave
-	static constexpr int WAVES = tile_waves(W), NTHR = WAVES * 64;
+	static constexpr int WAVES = tile_waves(W, NH), NTHR = WAVES * 64;
 	static constexpr int MT = W / 16, MTW = MT / WAVES;  // output-row tiles per matrix / per wave
 	static constexpr int KT0 = IN / 16;              // feature tiles of the input
 	// hidden matrices 1..NS are not staged: their forward A fragments come from the fp16 parameters
@@ -86,7 +87,7 @@ __device__ __forceinline__ h4 tile_act(f4 v) {
 }
 
 template <int W, int IN, int NH, Act ACT, bool EXT_DOUT>
-__global__ __launch_bounds__((W == 128 ? 512 : 256), 1) void k_mlp_tile_train(const TileTrainArgs a) {
+__global__ __launch_bounds__(tile_waves(W, NH) * 64, 1) void k_mlp_tile_train(const TileTrainArgs a) {
 	using L = TileLayout<W, IN, NH>;
 	constexpr int MTW = L::MTW, KT0 = L::KT0, RS0 = L::RS0, RSW = L::RSW, RSG = L::RSG;
 	constexpr int WAVES = L::WAVES, NTHR = L::NTHR;
