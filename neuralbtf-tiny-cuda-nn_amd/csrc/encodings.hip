@@ -23,10 +23,22 @@ __device__ __forceinline__ float quartic_cdf_deriv(float x, float inv_radius) {
 	return (15.0f / 16.0f) * tmp * tmp * inv_radius;
 }
 
-// Wrapped CDF at a bin's left boundary (one_blob_subwarp_aligned, oneblob.h:48-51).
+// Wrapped CDF at a bin's left boundary (one_blob_subwarp_aligned, oneblob.h:48-51). The two wrap
+// terms are clamped for all but the bins within one bin width of the domain's ends: quartic_cdf is
+// exactly 0 for u <= -T and exactly 1 for u >= T with T = 1.0625 (every fp32 u checked with this op
+// sequence by tools/quartic_clamp_check.c; the last unclamped values are at |u| ~ 1.004), so those
+// terms are skipped when no lane of the wave needs them, with bit-identical sums (same addition order).
+// The forward is VALU-bound (27 polynomial evaluations per 8 bins before); this removes ~2/3 of them.
 __device__ __forceinline__ float wrapped_cdf(float boundary, float x, float n_bins) {
+	constexpr float T = 1.0625f;
 	const float d = boundary - x;
-	return quartic_cdf(d, n_bins) + quartic_cdf(d - 1.0f, n_bins) + quartic_cdf(d + 1.0f, n_bins);
+	const float c = quartic_cdf(d, n_bins);
+	// the ballot makes the test wave-uniform (a scalar branch, not predication); inside it every lane
+	// evaluates the term, which is exact either way
+	float lo = 0.0f, hi = 1.0f;
+	if (__builtin_amdgcn_ballot_w64(!((d - 1.0f) * n_bins <= -T))) lo = quartic_cdf(d - 1.0f, n_bins);
+	if (__builtin_amdgcn_ballot_w64(!((d + 1.0f) * n_bins >= T))) hi = quartic_cdf(d + 1.0f, n_bins);
+	return c + lo + hi;
 }
 
 // OneBlob forward, one thread per (sample, dim): all n_bins outputs of that dimension.
