@@ -85,8 +85,18 @@ __global__ __launch_bounds__(256) void k_oneblob_fwd8(uint32_t B, uint32_t D, ui
 	const uint32_t per_row = D * (n_bins / 8);
 	const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
 	if (t >= B * per_row) return;
-	const uint32_t i = t / per_row, rem = t % per_row;
-	const uint32_t d = rem / (n_bins / 8), b0 = 8 * (rem % (n_bins / 8));
+	// n_bins / 8 is a power of two (shifts); so is per_row for D = 1, 2, 4 (no 32-bit udiv sequences)
+	const uint32_t lg = log2_bins - 3;
+	uint32_t i, rem;
+	if ((per_row & (per_row - 1)) == 0) {
+		const uint32_t lr = lg + (uint32_t)__builtin_ctz(D);
+		i = t >> lr;
+		rem = t & (per_row - 1);
+	} else {
+		i = t / per_row;
+		rem = t - i * per_row;
+	}
+	const uint32_t d = rem >> lg, b0 = 8 * (rem & ((1u << lg) - 1));
 	const float xv = x[(size_t)i * x_stride + d];
 	const float nb = (float)n_bins;
 	const uint32_t S = n_bins < 32 ? n_bins : 32;
