@@ -211,7 +211,7 @@ void launch_reduce_partials(hipStream_t st, const float* in, uint32_t n_parts, u
 // ---- tile engine (mlp_tile.hip): fused MLP training for W in {64, 128}, encoded input fp16 [B][IN] ----
 uint32_t tile_train_lds_bytes(uint32_t W, uint32_t IN, uint32_t NH);
 bool tile_train_supported(uint32_t W, uint32_t IN, uint32_t NH, uint32_t outp, int act);
-uint32_t tile_train_blocks(uint32_t B);
+uint32_t tile_train_blocks(uint32_t B, uint32_t W, uint32_t IN, uint32_t NH);
 // hidden matrices whose weights do not fit the LDS beside the rest (e.g. W128/H5/IN128: 2) are read from
 // L2; their transposed copy needs tile_train_wT_bytes of device memory (0: every matrix is staged)
 uint32_t tile_train_n_streamed(uint32_t W, uint32_t IN, uint32_t NH);

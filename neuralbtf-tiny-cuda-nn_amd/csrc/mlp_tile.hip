@@ -452,7 +452,19 @@ static void tile_launch(hipStream_t st, uint32_t blocks, const TileTrainArgs& a)
 	hipLaunchKernelGGL((k_mlp_tile_train<W, IN, NH, ACT, EXT>), dim3(blocks), dim3(L::NTHR), L::BYTES, st, a);
 }
 
-uint32_t tile_train_blocks(uint32_t B) { return std::max(1u, std::min(256u, B / 32)); }
+// Workgroups per CU: 2 where the LDS holds two (the W64 shapes: a second workgroup hides the first's
+// barrier and LDS latency at 1 wave per SIMD -- configs[1] 8,240 -> 10,468 steps/s, the sample's
+// default 7,072 -> 9,380; 3 measured mixed, profiles/r02_tile_wg_per_cu.txt), capped by the LDS fit.
+// TCNN_TILE_WG_PER_CU overrides (A/B switch).
+uint32_t tile_train_blocks(uint32_t B, uint32_t W, uint32_t IN, uint32_t NH) {
+	static const uint32_t want = [] {
+		const char* e = std::getenv("TCNN_TILE_WG_PER_CU");
+		return e ? std::max(1u, (uint32_t)std::atoi(e)) : 2u;
+	}();
+	const uint32_t bytes = tile_train_lds_bytes(W, IN, NH);
+	const uint32_t fit = bytes ? std::max(1u, (160u * 1024u) / bytes) : 1u;
+	return std::max(1u, std::min(256u * std::min(want, fit), B / 32));
+}
 
 void launch_mlp_tile_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, int act, uint32_t B, uint32_t dims, float loss_scale,
                            uint32_t loss_l2, const void* params16, const void* enc16, const float* target, const void* dout16, void* out16,
@@ -484,7 +496,7 @@ void launch_mlp_tile_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH,
 	a.dldenc_pairs = dldenc_pairs;
 	a.wgrad_partial = wgrad_partial;
 	a.loss_partial = loss_partial;
-	const uint32_t blocks = tile_train_blocks(B);
+	const uint32_t blocks = tile_train_blocks(B, W, IN, NH);
 	bool ok = false;
 #define X(w, in, nh)                                                                                          \
 	if (!ok && W == w && IN == in && NH == nh) {                                                              \

@@ -654,7 +654,7 @@ void NetworkHost::fwd_bwd_tile(hipStream_t st, StepWorkspace& ws, uint32_t B, co
 	const uint8_t* eparams = (const uint8_t*)params16 + (size_t)n_mlp * 2;
 	ws.enc16.reserve((size_t)B * IN * 2);
 	enc->forward_aos(st, B, pos, eparams, ws.enc16.p);
-	const uint32_t nb = tile_train_blocks(B);
+	const uint32_t nb = tile_train_blocks(B, W, IN, NH);
 	ws.wgrad_partial.reserve((size_t)nb * n_mlp * 4);
 	ws.loss_partial.reserve((size_t)nb * 4);
 	const bool enc_grad = enc->n_params() > 0 || dL_dinput;
