@@ -99,18 +99,46 @@ def cpu_baseline(cfg):
     }
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed PMC summary of this round's build
-    (profiles/*_pmc_traffic.json, tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE), or None."""
+DEFAULT_WORKLOAD = "HashGrid L16 F2 log2T15 s1.5 base16 + FullyFusedMLP W64 H2 ReLU, RelativeL2, Adam, B=2^18"
+
+
+def workload_tag(cfg, B):
+    """the workload's name, derived from the loaded config and the per-rank batch (it also keys the
+    committed PMC traffic files, so a variant's line never carries another config's bytes)"""
+    e, n = cfg.get("encoding", {}), cfg.get("network", {})
+    eo = e.get("otype", "OneBlob")
+    if eo.lower() in ("hashgrid", "grid", "densegrid", "tiledgrid"):
+        L = e.get("n_levels", 16)
+        enc = (f"{eo} L{L} F{e.get('n_features_per_level', 2)} log2T{e.get('log2_hashmap_size', 19)} "
+               f"s{e.get('per_level_scale', 2.0):g} base{e.get('base_resolution', 16)}")
+    elif eo.lower() == "oneblob":
+        enc = f"OneBlob bins{e.get('n_bins', 16)}"
+    else:
+        enc = eo
+    lb = B.bit_length() - 1
+    bs = f"2^{lb}" if B == 1 << lb else str(B)
+    return (f"{enc} + {n.get('otype', 'MLP')} W{n.get('n_neurons', 128)} H{n.get('n_hidden_layers', 5)} "
+            f"{n.get('activation', 'ReLU')}, {cfg.get('loss', {}).get('otype', 'RelativeL2')}, "
+            f"{cfg.get('optimizer', {}).get('otype', 'Adam')}, B={bs}")
+
+
+def pmc_traffic(kernel, tag):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary measured on the SAME
+    workload (profiles/*_pmc_traffic*.json whose "workload" equals `tag`; files without the key
+    predate it and were measured on the default workload), tools/pmc_traffic.py: FETCH_SIZE x2 +
+    WRITE_SIZE; None when no such file exists."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")))
-    if not files:
-        return None
-    try:
-        k = json.load(open(files[-1]))["kernels"].get(kernel)
-        return k["hbm_bytes"] if k else None
-    except (OSError, ValueError, KeyError):
-        return None
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic*.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+            if d.get("workload", DEFAULT_WORKLOAD) != tag:
+                continue
+            k = d["kernels"].get(kernel)
+            return k["hbm_bytes"] if k else None
+        except (OSError, ValueError, KeyError):
+            continue
+    return None
 
 
 def main():
@@ -135,7 +163,19 @@ def main():
     ap.add_argument("--graph", action="store_true", help="replay the single-GPU training step as a hipGraph")
     ap.add_argument("--all-ranks-on-device0", action="store_true",
                     help="rehearse N>1 on a 1-GPU box (gloo); never used for measurements")
+    ap.add_argument("--print-workload", action="store_true", help="print the workload tag and exit (no GPU)")
     args = ap.parse_args()
+
+    if args.print_workload:
+        cfg = json.load(open(args.config))
+        if args.log2_hashmap_size is not None:
+            cfg["encoding"]["log2_hashmap_size"] = args.log2_hashmap_size
+        if args.per_level_scale is not None:
+            cfg["encoding"]["per_level_scale"] = args.per_level_scale
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        B = (1 << args.batch_log2) // (world if args.scaling == "strong" else 1)
+        print(workload_tag(cfg, B))
+        return
 
     import torch
     import torch.distributed as dist
@@ -164,6 +204,7 @@ def main():
     B_global = 1 << args.batch_log2
     B = B_global // world if args.scaling == "strong" else B_global  # this rank's points per step
     assert B % 256 == 0, "per-rank batch must be a multiple of 256"
+    tag = workload_tag(cfg, B)
     trainer = Trainer(2, 3, cfg, seed=1337)
     g = torch.Generator(device="cuda")
     g.manual_seed(1337 + 7919 * rank)
@@ -235,8 +276,9 @@ def main():
         "dtype": "fp16 storage / fp32 MFMA accumulate",
         "data": "synthetic (uniform positions, analytic RGB targets), random-init weights (Trainer seed 1337)",
         "config": {
-            "workload": "mlp_learning_an_image training step, data/config_hash.json as-is "
-                        "(HashGrid L16 F2 log2T15 s1.5 base16 + FullyFusedMLP W64 H2 ReLU, RelativeL2, Adam)",
+            "workload": tag,
+            "config_file": os.path.relpath(args.config, REPO) + ("" if args.log2_hashmap_size is None and
+                                                                args.per_level_scale is None else " (overridden)"),
             "global_batch": B * world, "per_gpu_batch": B,
             "parallelism": "dp1" if world == 1 else (f"dp{world} batch-sharded ({B_global}/{world} points per rank)" if args.scaling == "strong"
                             else f"dp{world} ({B} points per rank)") +
@@ -256,14 +298,14 @@ def main():
             achieved = MLP_TRAIN_FLOP_PER_SAMPLE * B / (t_fused * 1e-3) / 1e12
             res["roofline"] = {"kernel": "k_fused_train_grid", "bound": "mfma", "achieved": achieved,
                                "peak": PEAK_FP16_TFLOPS, "unit": "TFLOP/s", "frac": achieved / PEAK_FP16_TFLOPS,
-                               "traffic": pmc_traffic("k_fused_train_grid")}
+                               "traffic": pmc_traffic("k_fused_train_grid", tag)}
         else:
             # the grid backward launch also carries the network-gradient reduction + Adam on the
             # network parameters (16 extra workgroups); their bytes are < 1 % of the grid's
             achieved = GRID_BWD_BYTES_PER_SAMPLE * B / (t_gbwd * 1e-3) / 1e9
             res["roofline"] = {"kernel": "k_grid_bwd_lds", "bound": "hbm", "achieved": achieved,
                                "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
-                               "traffic": pmc_traffic("k_grid_bwd_lds")}
+                               "traffic": pmc_traffic("k_grid_bwd_lds", tag)}
     if world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(cfg)
     print(json.dumps(res))

@@ -171,8 +171,13 @@ const char* tcnn_trainer_hyperparams(tcnn_trainer* t);
 /* Trainer::initialize_params (trainer.h:68-87): re-seed pcg32{seed_seq{seed}[0]}, re-initialise every
  * parameter, zero the optimizer state and its step counter. */
 int tcnn_trainer_initialize_params(tcnn_trainer* t, uint32_t seed);
-/* Engine diagnostics: name of the path the trainer runs ("fused" / "layered" / "unsupported"). */
+/* Engine diagnostics: name of the path the trainer runs ("fused" / "layered" / "unsupported"), for
+ * training and for network->inference ("fused": the whole MLP in one launch). */
 const char* tcnn_trainer_engine(const tcnn_trainer* t);
+const char* tcnn_trainer_inference_engine(const tcnn_trainer* t);
+/* The same for a network module (NetworkWithInputEncoding / create_network); "encoding" for encodings. */
+const char* tcnn_module_engine(const tcnn_module* m);
+const char* tcnn_module_inference_engine(const tcnn_module* m);
 /* set_max_level on the trainer model's grid encoding (see tcnn_module_set_max_level) */
 int tcnn_trainer_set_max_level(tcnn_trainer* t, float max_level);
 

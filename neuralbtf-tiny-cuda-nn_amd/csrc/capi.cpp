@@ -49,18 +49,55 @@ json parse_json(const char* s) {
 }
 
 // ---- runtime module (cpp_api.cu:64-140) ----
+// What a forward keeps for its backward (the reference's tcnn::Context, cpp_api.cu:84-94). Buffers come
+// from a pool the module and its contexts share, so a context may outlive its module, and steady-state
+// training allocates nothing. Like the reference's stream arenas, a context's buffer is stream-ordered:
+// the backward must run on the forward's stream (or after it).
+struct KeepPool {
+	std::mutex mu;
+	std::vector<std::unique_ptr<DevBuf>> free;
+	std::unique_ptr<DevBuf> get() {
+		std::lock_guard<std::mutex> lk(mu);
+		if (free.empty()) return std::make_unique<DevBuf>();
+		auto b = std::move(free.back());
+		free.pop_back();
+		return b;
+	}
+	void put(std::unique_ptr<DevBuf> b) {
+		std::lock_guard<std::mutex> lk(mu);
+		if (free.size() < 4) free.push_back(std::move(b));  // keeps two forwards in flight without allocating
+	}
+};
+
+struct ModuleCtx {
+	virtual ~ModuleCtx() = default;
+};
+
+struct NwieCtx : ModuleCtx {
+	std::shared_ptr<KeepPool> pool;
+	std::unique_ptr<DevBuf> keep;
+	int layout = 0;
+	const float* in = nullptr;
+	const void* params = nullptr;
+	~NwieCtx() override {
+		if (pool && keep) pool->put(std::move(keep));
+	}
+};
+
 struct ModuleBase {
 	virtual ~ModuleBase() = default;
 	virtual void inference(hipStream_t st, uint32_t n, const float* in, void* out, const void* params) = 0;
-	virtual void forward(hipStream_t st, uint32_t n, const float* in, void* out, const void* params, bool prep) = 0;
-	virtual void backward(hipStream_t st, uint32_t n, float* dL_din, const void* dL_dout, void* dL_dparams, const float* in,
-	                      const void* out, const void* params) = 0;
+	virtual std::unique_ptr<ModuleCtx> forward(hipStream_t st, uint32_t n, const float* in, void* out, const void* params, bool prep) = 0;
+	virtual void backward(hipStream_t st, const ModuleCtx* ctx, uint32_t n, float* dL_din, const void* dL_dout, void* dL_dparams,
+	                      const float* in, const void* out, const void* params) = 0;
 	// object.h:278-288: only encodings that define it (the grid) support second-order gradients
 	virtual void backward_backward_input(hipStream_t, uint32_t, const float*, const float*, const void*, void*, void*, float*,
 	                                     const void*) {
 		throw std::runtime_error("DifferentiableObject::backward_backward_input_impl: not implemented error");
 	}
 	virtual GridEncodingHost* grid_encoding() { return nullptr; }
+	virtual const char* engine() const { return "encoding"; }
+	virtual const char* inference_engine() const { return "encoding"; }
 	virtual uint32_t n_input_dims() const = 0;
 	virtual uint32_t n_output_dims() const = 0;
 	virtual uint64_t n_params() const = 0;
@@ -78,25 +115,39 @@ struct ModuleNWIE : ModuleBase {
 	NetworkHost model;
 	StepWorkspace ws;
 	DevBuf grad32;
+	std::shared_ptr<KeepPool> pool = std::make_shared<KeepPool>();
 	ModuleNWIE(uint32_t n_in, uint32_t n_out, const json& enc, const json& net) : model(n_in, n_out, enc, net) {}
 	void inference(hipStream_t st, uint32_t n, const float* in, void* out, const void* params) override {
 		check_batch(n);
 		model.inference(st, ws, n, in, params, out);
 	}
-	void forward(hipStream_t st, uint32_t n, const float* in, void* out, const void* params, bool prep) override {
+	// The context keeps the encoding of this batch in the layout the backward reads, so the backward
+	// does not encode again (the fused grid kernel skips its gathers; the tile engine its encoding pass).
+	std::unique_ptr<ModuleCtx> forward(hipStream_t st, uint32_t n, const float* in, void* out, const void* params, bool prep) override {
 		check_batch(n);
-		// The backward recomputes activations from the input, so the context carries nothing.
-		model.inference(st, ws, n, in, params, out);
+		auto c = std::make_unique<NwieCtx>();
+		c->pool = pool;
+		c->keep = pool->get();
+		c->layout = model.forward_keep(st, ws, n, in, params, out, prep, *c->keep);
+		c->in = in;
+		c->params = params;
+		return c;
 	}
-	void backward(hipStream_t st, uint32_t n, float* dL_din, const void* dL_dout, void* dL_dparams, const float* in,
+	void backward(hipStream_t st, const ModuleCtx* ctx, uint32_t n, float* dL_din, const void* dL_dout, void* dL_dparams, const float* in,
 	              const void*, const void* params) override {
 		check_batch(n);
 		if (!dL_dparams && !dL_din) return;
 		grad32.reserve(n_params() * 4);
-		model.fwd_bwd(st, ws, n, in, nullptr, model.n_output_dims, 1.0f, params, dL_dout, nullptr, grad32.as<float>(), nullptr, dL_din);
+		// the kept encoding describes this batch only if the backward sees the forward's input and parameters
+		const NwieCtx* c = dynamic_cast<const NwieCtx*>(ctx);
+		const bool use = c && c->keep && c->layout != NetworkHost::KEEP_NONE && c->in == in && c->params == params;
+		model.fwd_bwd(st, ws, n, in, nullptr, model.n_output_dims, 1.0f, params, dL_dout, nullptr, grad32.as<float>(), nullptr, dL_din,
+		              use ? c->keep->p : nullptr, use ? c->layout : NetworkHost::KEEP_NONE);
 		if (dL_dparams) launch_cast_f32_f16(st, grad32.as<float>(), dL_dparams, n_params());
 	}
 	GridEncodingHost* grid_encoding() override { return model.grid; }
+	const char* engine() const override { return model.engine(); }
+	const char* inference_engine() const override { return model.inference_engine(); }
 	uint32_t n_input_dims() const override { return model.n_input_dims; }
 	uint32_t n_output_dims() const override { return model.mlp.padded_output; }
 	uint64_t n_params() const override { return model.n_params(); }
@@ -118,10 +169,11 @@ struct ModuleEncoding : ModuleBase {
 	void inference(hipStream_t st, uint32_t n, const float* in, void* out, const void* params) override {
 		enc.forward_aos(st, n, in, params, out);
 	}
-	void forward(hipStream_t st, uint32_t n, const float* in, void* out, const void* params, bool) override {
+	std::unique_ptr<ModuleCtx> forward(hipStream_t st, uint32_t n, const float* in, void* out, const void* params, bool) override {
 		inference(st, n, in, out, params);
+		return nullptr;
 	}
-	void backward(hipStream_t st, uint32_t n, float* dL_din, const void* dL_dout, void*, const float* in, const void*,
+	void backward(hipStream_t st, const ModuleCtx*, uint32_t n, float* dL_din, const void* dL_dout, void*, const float* in, const void*,
 	              const void*) override {
 		if (dL_din) enc.backward_input(st, n, in, dL_dout, dL_din);
 	}
@@ -144,11 +196,12 @@ struct ModuleGrid : ModuleBase {
 		launch_grid_fwd(st, grid.desc.n_pos_dims, grid.desc.n_features_per_level, grid.desc.hash_type, n, grid.desc.n_levels,
 		                in, grid.desc.n_pos_dims, params, out, false, W, grid.dev_levels(), grid.hash_grid(), grid.desc.interp, grid.opts());
 	}
-	void forward(hipStream_t st, uint32_t n, const float* in, void* out, const void* params, bool prep) override {
+	std::unique_ptr<ModuleCtx> forward(hipStream_t st, uint32_t n, const float* in, void* out, const void* params, bool prep) override {
 		(void)prep;  // dy/dx is recomputed in backward (launch_grid_bwd_input), nothing to keep
 		inference(st, n, in, out, params);
+		return nullptr;
 	}
-	void backward(hipStream_t st, uint32_t n, float* dL_din, const void* dL_dout, void* dL_dparams, const float* in,
+	void backward(hipStream_t st, const ModuleCtx*, uint32_t n, float* dL_din, const void* dL_dout, void* dL_dparams, const float* in,
 	              const void*, const void* params) override {
 		if (dL_din)
 			launch_grid_bwd_input(st, grid.desc.n_pos_dims, grid.desc.n_features_per_level, grid.desc.hash_type, n, grid.desc.n_levels, in,
@@ -193,6 +246,7 @@ struct tcnn_module {
 };
 struct tcnn_context {
 	uint32_t n = 0;
+	std::unique_ptr<ModuleCtx> impl;  // what the forward kept (nullptr: nothing)
 };
 struct tcnn_trainer {
 	std::unique_ptr<TrainerHost> t;
@@ -273,9 +327,9 @@ int tcnn_module_inference(tcnn_module* m, void* stream, uint32_t n, const float*
 
 tcnn_context* tcnn_module_forward(tcnn_module* m, void* stream, uint32_t n, const float* in, void* out, const void* params, int prep) {
 	return guard_ptr<tcnn_context>([&] {
-		if (n) m->m->forward((hipStream_t)stream, n, in, out, params, prep != 0);
 		auto* c = new tcnn_context;
 		c->n = n;
+		if (n) c->impl = m->m->forward((hipStream_t)stream, n, in, out, params, prep != 0);
 		return c;
 	});
 }
@@ -288,7 +342,8 @@ int tcnn_module_backward(tcnn_module* m, void* stream, const tcnn_context* ctx, 
 			if (dL_dparams) TCNN_HIP_CHECK(hipMemsetAsync(dL_dparams, 0, m->m->n_params() * 2, (hipStream_t)stream));
 			return;
 		}
-		m->m->backward((hipStream_t)stream, n, dL_din, dL_dout, dL_dparams, in, out, params);
+		TCNN_CHECK(ctx->n == n, "backward: batch size differs from the forward's");
+		m->m->backward((hipStream_t)stream, ctx->impl.get(), n, dL_din, dL_dout, dL_dparams, in, out, params);
 	});
 }
 
@@ -431,6 +486,9 @@ int tcnn_trainer_initialize_params(tcnn_trainer* t, uint32_t seed) {
 	return guard([&] { t->t->initialize_params(seed); });
 }
 const char* tcnn_trainer_engine(const tcnn_trainer* t) { return t->t->model->engine(); }
+const char* tcnn_trainer_inference_engine(const tcnn_trainer* t) { return t->t->model->inference_engine(); }
+const char* tcnn_module_engine(const tcnn_module* m) { return m->m->engine(); }
+const char* tcnn_module_inference_engine(const tcnn_module* m) { return m->m->inference_engine(); }
 int tcnn_trainer_set_max_level(tcnn_trainer* t, float max_level) {
 	return guard([&] {
 		TCNN_CHECK(t->t->model->grid != nullptr, "trainer model has no grid encoding");

@@ -95,6 +95,18 @@ inline void log_warning(const std::string& m) { log_msg(LogSeverity::Warning, m)
 
 inline uint32_t div_round_up(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device): the attribute is
+// per-device state, so one process-wide "done" flag would skip every device after the first.
+// done: the caller's static mask, one bit per device ordinal (mod 64; setting it again is harmless).
+inline void set_dyn_lds(const void* kernel, int bytes, uint64_t& done) {
+	int dev = 0;
+	TCNN_HIP_CHECK(hipGetDevice(&dev));
+	const uint64_t bit = 1ull << (dev & 63);
+	if (__atomic_load_n(&done, __ATOMIC_ACQUIRE) & bit) return;
+	TCNN_HIP_CHECK(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+	__atomic_fetch_or(&done, bit, __ATOMIC_RELEASE);
+}
+
 // Grow-only scratch allocation owned by a launcher (not stream-ordered: callers on one stream).
 struct DevBufLite {
 	void* p = nullptr;

@@ -82,22 +82,26 @@ uint32_t fused_train_n_blocks(uint32_t W, uint32_t IN, uint32_t NH, uint32_t D, 
 	return nb < cap ? nb : cap;
 }
 
-template <int W, int IN, int NH, uint32_t D, HashType H, Act A, bool EXT>
+template <int W, int IN, int NH, uint32_t D, HashType H, Act A, bool EXT, bool ENC = false>
 static void launch_fused_e(hipStream_t st, const FusedTrainArgs& args, uint32_t n_blocks) {
 	constexpr size_t bytes = RegKernelLayout<W, IN, NH>::BYTES;
-	static bool attr = false;
-	if (!attr) {
-		TCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k_fused_train_grid<W, IN, NH, D, H, A, EXT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
-		attr = true;
-	}
-	hipLaunchKernelGGL((k_fused_train_grid<W, IN, NH, D, H, A, EXT>), dim3(n_blocks), dim3(64 * FUSED_WAVES), bytes, st, args);
+	static uint64_t done = 0;
+	set_dyn_lds((const void*)k_fused_train_grid<W, IN, NH, D, H, A, EXT, ENC>, (int)bytes, done);
+	hipLaunchKernelGGL((k_fused_train_grid<W, IN, NH, D, H, A, EXT, ENC>), dim3(n_blocks), dim3(64 * FUSED_WAVES), bytes, st, args);
 	TCNN_HIP_CHECK(hipGetLastError());
 }
 
 template <int W, int IN, int NH, uint32_t D, HashType H, Act A>
 static void launch_fused_t(hipStream_t st, const FusedTrainArgs& args, uint32_t n_blocks) {
-	if (args.dout) launch_fused_e<W, IN, NH, D, H, A, true>(st, args, n_blocks);
-	else launch_fused_e<W, IN, NH, D, H, A, false>(st, args, n_blocks);
+	if (args.enc) {
+		// the encoding comes from memory: one instantiation serves every D / hash (Module backward)
+		TCNN_CHECK(args.dout, "fused train: a kept encoding is used with an external dL/d(output) only");
+		launch_fused_e<W, IN, NH, 2, HashType::CoherentPrime, A, true, true>(st, args, n_blocks);
+	} else if (args.dout) {
+		launch_fused_e<W, IN, NH, D, H, A, true>(st, args, n_blocks);
+	} else {
+		launch_fused_e<W, IN, NH, D, H, A, false>(st, args, n_blocks);
+	}
 }
 
 template <int W, int IN, int NH>
@@ -121,9 +125,10 @@ void launch_fused_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, ui
                         const float* pos, const float* target, void* out16, void* dLdenc_pairs,
                         float* wgrad_partial, float* loss_partial, const LevelInfo* levels, bool hash_grid,
                         Interp interp, uint32_t n_blocks, const void* dout16, const void* wimage, uint32_t loss_l2,
-                        bool inrange_index) {
+                        bool inrange_index, const void* enc16) {
 	TCNN_CHECK(B % 32 == 0, "fused train: batch must be a multiple of 32");
 	FusedTrainArgs a;
+	a.enc = (const _Float16*)enc16;
 	a.loss_l2 = loss_l2;
 	a.inrange_index = inrange_index ? 1u : 0u;
 	a.wimage = (const _Float16*)wimage;
@@ -153,11 +158,8 @@ void launch_fused_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, ui
 template <int W, int IN, int NH, Act A, bool SOA>
 static void launch_infer_t(hipStream_t st, uint32_t B, const void* wimage, const void* in, void* out) {
 	constexpr size_t bytes = (size_t)FusedLayout<W, IN, NH>::oStage * 2;
-	static bool attr = false;
-	if (!attr) {
-		TCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k_mlp_infer<W, IN, NH, A, SOA>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
-		attr = true;
-	}
+	static uint64_t done = 0;
+	set_dyn_lds((const void*)k_mlp_infer<W, IN, NH, A, SOA>, (int)bytes, done);
 	uint32_t nb = div_round_up(B, 64);
 	if (nb > 1024) nb = 1024;
 	hipLaunchKernelGGL((k_mlp_infer<W, IN, NH, A, SOA>), dim3(nb), dim3(256), bytes, st, B, (const _Float16*)wimage,
@@ -213,17 +215,13 @@ void launch_fused_train_profile(hipStream_t st, uint32_t B, uint32_t dims, const
 	a.B = B; a.dims = dims; a.loss_scale = 128.0f; a.n_total = (float)(B * dims);
 	a.params = (const _Float16*)params16; a.table = (const uint32_t*)table16; a.pos = pos; a.target = target;
 	a.out = nullptr; a.dLdenc = (uint32_t*)dLdenc; a.wgrad_partial = wgrad_partial; a.loss_partial = loss_partial;
-	a.levels = levels; a.hash_grid = 1; a.interp = (uint32_t)Interp::Linear; a.dout = nullptr; a.prof = prof;
+	a.levels = levels; a.hash_grid = 1; a.interp = (uint32_t)Interp::Linear; a.dout = nullptr; a.enc = nullptr; a.prof = prof;
 	a.inrange_index = 1;
 	using K = RegKernelLayout<64, 32, 2>;
-	static bool attr = false;
-	if (!attr) {
-		TCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k_fused_train_grid<64, 32, 2, 2, HashType::CoherentPrime, Act::ReLU, false, true>,
-		                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)K::BYTES));
-		attr = true;
-	}
-	hipLaunchKernelGGL((k_fused_train_grid<64, 32, 2, 2, HashType::CoherentPrime, Act::ReLU, false, true>), dim3(n_blocks), dim3(64 * FUSED_WAVES),
-	                   K::BYTES, st, a);
+	static uint64_t done = 0;
+	set_dyn_lds((const void*)k_fused_train_grid<64, 32, 2, 2, HashType::CoherentPrime, Act::ReLU, false, false, true>, (int)K::BYTES, done);
+	hipLaunchKernelGGL((k_fused_train_grid<64, 32, 2, 2, HashType::CoherentPrime, Act::ReLU, false, false, true>), dim3(n_blocks),
+	                   dim3(64 * FUSED_WAVES), K::BYTES, st, a);
 	TCNN_HIP_CHECK(hipGetLastError());
 }
 

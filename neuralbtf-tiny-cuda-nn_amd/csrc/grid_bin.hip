@@ -391,11 +391,8 @@ void launch_grid_bin(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_
 template <uint32_t NC, uint32_t F>
 static void grid_acc_t(hipStream_t st, int layout, uint32_t dys, uint32_t B, const _Float16* dy, const LevelInfo* lv, const GridBinArgs& a,
                        float* grad32, const GridAccAdam* ad) {
-	static bool attr = false;
-	if (!attr) {
-		TCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k_grid_acc<NC, F>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GRID_ACC_LDS_BYTES));
-		attr = true;
-	}
+	static uint64_t done = 0;
+	set_dyn_lds((const void*)k_grid_acc<NC, F>, (int)GRID_ACC_LDS_BYTES, done);
 	GridAccAdam adv{};
 	if (ad) adv = *ad;
 	TCNN_CHECK(a.acc_lds_bytes <= GRID_ACC_LDS_BYTES, "grid acc: slice exceeds the LDS budget");

@@ -488,12 +488,9 @@ static void grid_bwd_t(hipStream_t st, int layout, uint32_t dys, dim3 g, size_t 
                        const _Float16* dy, const GridSlice* sl, float* part, uint32_t pstr, const LevelInfo* lv,
                        uint32_t hg, uint32_t in, uint32_t ppc, const GridBwdLaunch& gl) {
 	// the options (max_level, stochastic) are a separate instantiation: the default kernel stays lean
-	static bool attr = false;
-	if (!attr) {
-		TCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k_grid_bwd_lds<D, F, H, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GRID_BWD_LDS_BYTES));
-		TCNN_HIP_CHECK(hipFuncSetAttribute((const void*)k_grid_bwd_lds<D, F, H, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GRID_BWD_LDS_BYTES));
-		attr = true;
-	}
+	static uint64_t done0 = 0, done1 = 0;
+	set_dyn_lds((const void*)k_grid_bwd_lds<D, F, H, false>, (int)GRID_BWD_LDS_BYTES, done0);
+	set_dyn_lds((const void*)k_grid_bwd_lds<D, F, H, true>, (int)GRID_BWD_LDS_BYTES, done1);
 	if (gl.opts.active)
 		hipLaunchKernelGGL((k_grid_bwd_lds<D, F, H, true>), g, dim3(GRID_BWD_THREADS), lds, st, layout, B, pos, ps, dy, dys, sl, part, pstr, lv, hg, in,
 		                   ppc, gl.n_items, gl.n_chunks, gl.ep, gl.dbg_times, gl.opts);

@@ -137,7 +137,8 @@ void launch_fused_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, ui
                         uint32_t B, uint32_t dims, float loss_scale, const void* params16, const void* table16,
                         const float* pos, const float* target, void* out16, void* dLdenc_pairs,
                         float* wgrad_partial, float* loss_partial, const LevelInfo* levels, bool hash_grid,
-                        Interp interp, uint32_t n_blocks, const void* dout16, const void* wimage, uint32_t loss_l2 = 0, bool inrange_index = false);
+                        Interp interp, uint32_t n_blocks, const void* dout16, const void* wimage, uint32_t loss_l2 = 0, bool inrange_index = false,
+                        const void* enc16 = nullptr);  // enc16: the forward's encoding, SoA [IN][B] (with dout16 only)
 // LDS weight image of the fused kernels, built once per parameter update.
 size_t fused_weight_image_bytes(uint32_t W, uint32_t IN, uint32_t NH);
 void launch_pack_weights(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, const void* params16, void* image);
@@ -208,7 +209,8 @@ size_t reduce_partials_tmp_floats(uint32_t n_parts, uint32_t n);
 void launch_reduce_partials(hipStream_t st, const float* in, uint32_t n_parts, uint32_t stride, uint32_t n,
                             float* out, float* tmp);
 
-// ---- tile engine (mlp_tile.hip): fused MLP training for W in {64, 128}, encoded input fp16 [B][IN] ----
+// ---- tile engine (mlp_tile.h): fused MLP for W in {16, 32, 64, 128}, IN in {16, 32, 64, 128},
+// 1..5 hidden layers, hidden activation None / ReLU, any output activation; encoded input fp16 [B][IN] ----
 uint32_t tile_train_lds_bytes(uint32_t W, uint32_t IN, uint32_t NH);
 bool tile_train_supported(uint32_t W, uint32_t IN, uint32_t NH, uint32_t outp, int act);
 uint32_t tile_train_blocks(uint32_t B, uint32_t W, uint32_t IN, uint32_t NH);
@@ -218,9 +220,16 @@ uint32_t tile_train_n_streamed(uint32_t W, uint32_t IN, uint32_t NH);
 uint32_t tile_train_wT_bytes(uint32_t W, uint32_t IN, uint32_t NH);
 // dldenc (optional): dL/d(encoding) as level-major pairs [IN/2][B] (dldenc_pairs) or AoS fp16 [B][IN]
 // wT: tile_train_wT_bytes of scratch (nullptr when 0), rewritten from params16 by this launch
-void launch_mlp_tile_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, int act, uint32_t B, uint32_t dims, float loss_scale,
-                           uint32_t loss_l2, const void* params16, const void* enc16, const float* target, const void* dout16, void* out16,
-                           void* dldenc, int dldenc_pairs, float* wgrad_partial, float* loss_partial, void* wT);
+// out_act: output activation (ACT_*) applied to the output, its transfer applied to dL/d(output)
+void launch_mlp_tile_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, int act, int out_act, uint32_t B, uint32_t dims,
+                           float loss_scale, uint32_t loss_l2, const void* params16, const void* enc16, const float* target,
+                           const void* dout16, void* out16, void* dldenc, int dldenc_pairs, float* wgrad_partial, float* loss_partial,
+                           void* wT);
+// forward only (the reference's INFERENCE instantiation): enc16 fp16 [B][IN] -> out16 fp16 [B][16]
+bool tile_infer_supported(uint32_t W, uint32_t IN, uint32_t NH, uint32_t outp, int act);
+uint32_t tile_infer_blocks(uint32_t B, uint32_t W, uint32_t IN, uint32_t NH);
+void launch_mlp_tile_infer(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, int act, int out_act, uint32_t B, const void* params16,
+                           const void* enc16, void* out16);
 
 // generate_random_uniform<float> (random.h:57-70) from pcg32 {state, inc} (not advanced here)
 void launch_generate_uniform(hipStream_t st, uint64_t n, uint64_t state, uint64_t inc, float* out, float lo, float hi);

@@ -23,6 +23,7 @@
 
 #include "common.h"
 #include "grid_device.h"
+#include "kernels.h"
 
 namespace tcnn_amd {
 
@@ -58,6 +59,54 @@ __device__ __forceinline__ h4 act_bwd(h4 fwd, f4 g) {
 	}
 	return r;
 }
+
+// ---- activations (reference common_device.h:102-297), fp32 math on fp16-stored values ----
+__device__ __forceinline__ float logistic_f(float x) { return 1.0f / (1.0f + expf(-x)); }
+constexpr float K_ACT = 10.0f;
+
+__device__ __forceinline__ float act_fwd_rt(int a, float x) {
+	switch (a) {
+		case ACT_RELU: return x > 0.0f ? x : 0.0f;
+		case ACT_LEAKY_RELU: return x * (x > 0.0f ? 1.0f : 0.01f);
+		case ACT_EXPONENTIAL: return expf(x);
+		case ACT_SINE: return sinf(x);
+		case ACT_SIGMOID: return logistic_f(x);
+		case ACT_SQUAREPLUS: {
+			const float y = x * K_ACT;
+			return 0.5f * (y + sqrtf(y * y + 4.0f)) / K_ACT;
+		}
+		case ACT_SOFTPLUS: return logf(expf(x * K_ACT) + 1.0f) / K_ACT;
+		case ACT_TANH: return tanhf(x);
+		default: return x;
+	}
+}
+
+// Transfer given the post-activation value y (warp_activation_backward, common_device.h:240-297):
+// the factor is rounded to fp16 like the reference's (T)(...) before the fp16 product.
+__device__ __forceinline__ float act_bwd_rt(int a, float g, float y) {
+	float f;
+	switch (a) {
+		case ACT_RELU: return y > 0.0f ? g : 0.0f;
+		case ACT_LEAKY_RELU: f = y > 0.0f ? 1.0f : 0.01f; break;
+		case ACT_EXPONENTIAL: f = y; break;
+		case ACT_SIGMOID: f = y * (float)f16_rn(1.0f - y); break;
+		case ACT_SQUAREPLUS: {
+			const float t = y * K_ACT;
+			f = t * t / (t * t + 1.0f);
+			break;
+		}
+		case ACT_SOFTPLUS: f = 1.0f - expf(-y * K_ACT); break;
+		case ACT_TANH: f = 1.0f - y * y; break;
+		default: return g;
+	}
+	return (float)f16_rn(g) * (float)f16_rn(f);
+}
+
+// Out-of-line activation for the rare activations: the MFMA loops inline only None / ReLU, so
+// the kernels stay a few thousand instructions (inlining every activation per element made them
+// ~22K instructions, far beyond the instruction cache).
+static __device__ __noinline__ float act_fwd_ool(int a, float x) { return act_fwd_rt(a, x); }
+static __device__ __noinline__ float act_bwd_ool(int a, float g, float y) { return act_bwd_rt(a, g, y); }
 
 // A operand from a row-major LDS matrix M[row][col] (row stride rs halves):
 // lane (c, q) takes M[row][col0 + 0..3] and M[row][col0 + 16 + 0..3], col0 = 32s + 4q.
@@ -187,6 +236,7 @@ struct FusedTrainArgs {
 	uint32_t hash_grid;
 	uint32_t interp;
 	const _Float16* dout;   // EXT_DOUT: external dL/d(output) fp16 [B][16] (loss-scaled by the caller)
+	const _Float16* enc;    // ENC_MEM: the encoding kept by the forward, SoA [IN][B] (no gathers)
 	unsigned long long* prof;  // diagnostic build only: per-wave phase cycle sums [waves][8]
 };
 
@@ -489,7 +539,9 @@ __device__ __forceinline__ void block_reduce_wgrad(WgradAcc<W, IN, NH>& acc, flo
 
 // Register-gather variant, any D: one workgroup = FUSED_WAVES waves, each wave runs 32-sample
 // slices in a grid-stride loop; the grid encoding's gathers go straight to registers.
-template <int W, int IN, int NH, uint32_t D, HashType H, Act ACT, bool EXT_DOUT, bool PROF = false>
+// ENC_MEM (Module backward after a forward that kept its encoding, cpp_api.cu:84-109): the encoded
+// input is read from a.enc instead of gathered from the table (D and H are then unused).
+template <int W, int IN, int NH, uint32_t D, HashType H, Act ACT, bool EXT_DOUT, bool ENC_MEM = false, bool PROF = false>
 __global__ __launch_bounds__(64 * FUSED_WAVES, 8 / FUSED_WAVES) void k_fused_train_grid(const FusedTrainArgs a) {
 	using L = FusedLayout<W, IN, NH>;
 	using RL = RegKernelLayout<W, IN, NH>;
@@ -532,23 +584,44 @@ __global__ __launch_bounds__(64 * FUSED_WAVES, 8 / FUSED_WAVES) void k_fused_tra
 				tg[tau][r] = (!EXT_DOUT && o < a.dims) ? a.target[(size_t)i * a.dims + o] : 0.0f;
 			}
 		}
-		float xs[2][D];
-		bool inr = true;
 #pragma unroll
 		for (int tau = 0; tau < 2; ++tau) {
-			const uint32_t i = base + 16 * tau + c;
+			if constexpr (EXT_DOUT) Gext[tau] = *(const h4*)(a.dout + (size_t)(base + 16 * tau + c) * 16 + 4 * q);
+		}
+		if constexpr (ENC_MEM) {
+			// xt[tau][2s + (pp >> 1)][2 (pp & 1) + f] = feature f of level 16 s + 8 (pp >> 1) + 2 q + (pp & 1)
 #pragma unroll
-			for (uint32_t d = 0; d < D; ++d) {
-				xs[tau][d] = a.pos[(size_t)i * D + d];
-				inr = inr && xs[tau][d] >= 0.0f && xs[tau][d] <= 1.0f;
+			for (int tau = 0; tau < 2; ++tau) {
+				const uint32_t i = base + 16 * tau + c;
+#pragma unroll
+				for (int s = 0; s < KI; ++s)
+#pragma unroll
+					for (int pp = 0; pp < 4; ++pp) {
+						const int level = 16 * s + 8 * (pp >> 1) + 2 * q + (pp & 1);
+#pragma unroll
+						for (int f = 0; f < 2; ++f) xt[tau][2 * s + (pp >> 1)][2 * (pp & 1) + f] = a.enc[(size_t)(2 * level + f) * a.B + i];
+					}
 			}
-			if constexpr (EXT_DOUT) Gext[tau] = *(const h4*)(a.dout + (size_t)i * 16 + 4 * q);
+		}
+		float xs[2][D];
+		bool inr = true;
+		if constexpr (!ENC_MEM) {
+#pragma unroll
+			for (int tau = 0; tau < 2; ++tau) {
+				const uint32_t i = base + 16 * tau + c;
+#pragma unroll
+				for (uint32_t d = 0; d < D; ++d) {
+					xs[tau][d] = a.pos[(size_t)i * D + d];
+					inr = inr && xs[tau][d] >= 0.0f && xs[tau][d] <= 1.0f;
+				}
+			}
 		}
 		// every position of the wave's slice in [0, 1]: the branch-free index (no per-corner
 		// branches); otherwise the general index with its rare `% size` path. Tried and reverted:
 		// issuing all 16 gathers of a sample before the FMA chains (66.3 vs 64.7 us), fetching the
 		// next slice's positions one slice ahead (no change)
-		if (a.inrange_index && __builtin_amdgcn_ballot_w64(!inr) == 0) {
+		if constexpr (ENC_MEM) {
+		} else if (a.inrange_index && __builtin_amdgcn_ballot_w64(!inr) == 0) {
 #pragma unroll
 			for (int tau = 0; tau < 2; ++tau)
 #pragma unroll

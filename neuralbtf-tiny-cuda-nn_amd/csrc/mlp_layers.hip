@@ -24,48 +24,6 @@
 
 namespace tcnn_amd {
 
-// ---- activations (reference common_device.h:102-297), fp32 math on fp16-stored values ----
-__device__ __forceinline__ float logistic_f(float x) { return 1.0f / (1.0f + expf(-x)); }
-constexpr float K_ACT = 10.0f;
-
-__device__ __forceinline__ float act_fwd_rt(int a, float x) {
-	switch (a) {
-		case ACT_RELU: return x > 0.0f ? x : 0.0f;
-		case ACT_LEAKY_RELU: return x * (x > 0.0f ? 1.0f : 0.01f);
-		case ACT_EXPONENTIAL: return expf(x);
-		case ACT_SINE: return sinf(x);
-		case ACT_SIGMOID: return logistic_f(x);
-		case ACT_SQUAREPLUS: {
-			const float y = x * K_ACT;
-			return 0.5f * (y + sqrtf(y * y + 4.0f)) / K_ACT;
-		}
-		case ACT_SOFTPLUS: return logf(expf(x * K_ACT) + 1.0f) / K_ACT;
-		case ACT_TANH: return tanhf(x);
-		default: return x;
-	}
-}
-
-// Transfer given the post-activation value y (warp_activation_backward, common_device.h:240-297):
-// the factor is rounded to fp16 like the reference's (T)(...) before the fp16 product.
-__device__ __forceinline__ float act_bwd_rt(int a, float g, float y) {
-	float f;
-	switch (a) {
-		case ACT_RELU: return y > 0.0f ? g : 0.0f;
-		case ACT_LEAKY_RELU: f = y > 0.0f ? 1.0f : 0.01f; break;
-		case ACT_EXPONENTIAL: f = y; break;
-		case ACT_SIGMOID: f = y * (float)f16_rn(1.0f - y); break;
-		case ACT_SQUAREPLUS: {
-			const float t = y * K_ACT;
-			f = t * t / (t * t + 1.0f);
-			break;
-		}
-		case ACT_SOFTPLUS: f = 1.0f - expf(-y * K_ACT); break;
-		case ACT_TANH: f = 1.0f - y * y; break;
-		default: return g;
-	}
-	return (float)f16_rn(g) * (float)f16_rn(f);
-}
-
 // Stage a row-major [rows][cols] fp16 matrix into LDS with row stride rs, zero-filling columns
 // [cols, zc) (transpose = false), or its transpose [cols][rows] with columns [rows, zc) zeroed.
 // Untransposed rows go 8 halves (16 B) per load when cols % 8 == 0 (every shape here).
@@ -170,11 +128,6 @@ __device__ __forceinline__ void layer_slices(const _Float16* sA, int rs, const _
 	}
 }
 
-// Out-of-line activation for the rare activations: the MFMA loops inline only None / ReLU, so
-// the kernels stay a few thousand instructions (inlining every activation per element made them
-// ~22K instructions, far beyond the instruction cache).
-__device__ __noinline__ float act_fwd_ool(int a, float x) { return act_fwd_rt(a, x); }
-__device__ __noinline__ float act_bwd_ool(int a, float g, float y) { return act_bwd_rt(a, g, y); }
 
 template <int A>  // ACT_NONE, ACT_RELU, or -1 (any, out of line)
 __device__ __forceinline__ float act_fwd_sel(int a, float x) {

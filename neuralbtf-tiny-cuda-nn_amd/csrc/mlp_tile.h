@@ -1,0 +1,704 @@
+// mlp_tile.h -- fully fused MLP for every FullyFusedMLP shape the register-resident grid kernel
+// (mlp_fused.h: W <= 64, grid input, two hidden layers) does not take: W in {16, 32, 64, 128}, any
+// input encoding (hash grid, OneBlob, Identity) read as fp16 [B][IN], IN <= 128, 1..5 hidden layers,
+// any output activation. Templates here; instantiated per width in mlp_tile_w{16,32,64,128}.hip.
+//
+// Reference: kernel_mlp_fused / kernel_mlp_fused_backward (fully_fused_mlp.cu:47-259, 499-557; widths
+// 16/32/64/128 at :893-896) and the CUTLASS weight-gradient GEMMs (fully_fused_mlp.cu:735-836). The
+// reference writes every hidden activation and every backprop temporary to HBM ([W x B] fp16 per
+// layer, twice) and reads them back for the split-K weight gradients; for W128/H4 at B = 2^20 that is
+// ~5 KB per sample.
+//
+// Training (k_mlp_tile_train): one workgroup owns the whole network for 32-sample tiles:
+//   * all weights are staged once into LDS (W128/H4/IN32: 119 KB, padded rows, fp16);
+//   * a tile's input and its NH post-activations stay in LDS ([32][W+8] fp16 per layer, 35 KB) for
+//     the backward pass, the loss is fused after the output layer (with the output activation and
+//     its transfer), and each backprop delta overwrites the activation slot it no longer needs;
+//   * weight gradients accumulate in registers across all tiles the workgroup processes: wave w owns
+//     output-row tiles w*W/64 .. of every matrix (the MFMA contracts over the 32 samples of a tile,
+//     operands read from LDS with the gfx950 ds_read_b64_tr_b16 transpose read), so no cross-wave
+//     reduction exists; one fp32 partial slab per workgroup leaves at the end;
+//   * dL/d(encoding) = W0^T delta_1 leaves in the layout the grid backward reads (level-major
+//     feature pairs) or AoS for the OneBlob / Identity input gradient.
+// Inference (k_mlp_tile_infer, the reference's INFERENCE=true instantiation, :524-532): weight-
+// stationary -- each wave keeps the A fragments of its two output-row tiles of every matrix in
+// registers for the whole launch (no weight traffic after the first load), activations ping-pong
+// between two LDS tiles, nothing but the input and the 16-wide output touches HBM.
+// W16 networks run the W32 kernels on zero-padded weights: the padded neurons' pre-activations are
+// exactly 0, their deltas exactly 0, so outputs and gradients equal the unpadded network's.
+// fp32 MFMA accumulation (f32_16x16x32_f16), fp16 storage at the reference's points.
+#pragma once
+
+#include "kernels.h"
+#include "mlp_fused.h"
+
+namespace tcnn_amd {
+
+constexpr int tile_kw(int WR) { return WR < 32 ? 32 : WR; }  // kernel width (W16 -> 32, zero-padded)
+constexpr int tile_imax(int a, int b) { return a > b ? a : b; }
+constexpr int tile_imin(int a, int b) { return a < b ? a : b; }
+
+// ---------------------------------------------------------------------------------------------
+// training
+// ---------------------------------------------------------------------------------------------
+// LDS halves of a tile workgroup with the first NS hidden matrices streamed from L2 instead of staged
+constexpr int tile_halves(int W, int IN, int NH, int NS) {
+	const int KP0 = (IN + 31) / 32 * 32, RS0 = KP0 + 8, RSW = W + 8, RSG = 24;
+	return W * RS0 + (NH - 1 - NS) * W * RSW + 16 * RSW + 32 * RS0 + NH * 32 * RSW + 32 * RSG;
+}
+// waves per workgroup: W128 runs 8 (2 per SIMD, one 16-row tile of every matrix each) up to 4 hidden
+// layers; with 5 its weight-gradient accumulators (>= 164 registers) spill at 256 registers per wave,
+// so it runs 4 waves (1 per SIMD, 512 registers incl. AGPRs, two row tiles each); W64 4; W32 2 (one
+// row tile each)
+constexpr int tile_waves(int W, int NH) { return W == 128 && NH < 5 ? 8 : (W == 32 ? 2 : 4); }
+constexpr int tile_lds_limit() { return 160 * 1024; }
+// fewest streamed hidden matrices that let the rest of the network + the tile's activations fit
+constexpr int tile_n_streamed(int W, int IN, int NH) {
+	int ns = 0;
+	while (ns < NH - 1 && tile_halves(W, IN, NH, ns) * 2 + tile_waves(W, NH) * 4 > tile_lds_limit()) ++ns;
+	return ns;
+}
+// workgroups per CU the launch aims for: two waves per SIMD where the LDS allows
+constexpr int tile_train_wg_per_cu(int W, int IN, int NH) {
+	return tile_imax(1, tile_imin(8 / tile_waves(W, NH), tile_lds_limit() / (tile_halves(W, IN, NH, tile_n_streamed(W, IN, NH)) * 2 + tile_waves(W, NH) * 4)));
+}
+
+template <int WR, int IN, int NH>
+struct TileLayout {
+	static constexpr int W = tile_kw(WR);
+	static_assert(W == 32 || W == 64 || W == 128, "tile engine: W in {16, 32, 64, 128}");
+	static_assert(IN % 16 == 0 && IN <= 128, "tile engine: IN a multiple of 16, <= 128");
+	static constexpr int KP0 = (IN + 31) / 32 * 32;  // K of the first layer, padded to the MFMA depth
+	static constexpr int RS0 = KP0 + 8, RSW = W + 8, RSG = 24;
+	static constexpr int WAVES = tile_waves(W, NH), NTHR = WAVES * 64;
+	static constexpr int MT = W / 16, MTW = MT / WAVES;  // output-row tiles per matrix / per wave
+	static constexpr int KT0 = IN / 16;              // feature tiles of the input
+	// hidden matrices 1..NS are not staged: their forward A fragments come from the fp16 parameters
+	// (L2-resident, every workgroup reads the same 32 KB), their backward ones from a transposed copy
+	static constexpr int NS = tile_n_streamed(W, IN, NH);
+	static_assert(NS == 0 || W == WR, "streamed matrices only for unpadded widths");
+	static constexpr int oW0 = 0, oWh = oW0 + W * RS0, oWo = oWh + (NH - 1 - NS) * W * RSW;
+	static constexpr int oX = oWo + 16 * RSW;                 // slot 0: the tile's input [32][RS0]
+	static constexpr int oA = oX + 32 * RS0;                  // slots 1..NH: [32][RSW]
+	static constexpr int oG = oA + NH * 32 * RSW;             // dL/dy of the tile [32][RSG]
+	static constexpr int HALVES = oG + 32 * RSG;
+	static constexpr int BYTES = HALVES * 2 + WAVES * 4;       // + per-wave loss
+	static constexpr int N_MLP = WR * IN + (NH - 1) * WR * WR + 16 * WR;  // parameters (unpadded)
+	static constexpr int WG_PER_CU = tile_train_wg_per_cu(W, IN, NH);
+	// waves per SIMD the launch runs (amdgpu_waves_per_eu: caps the registers so they fit)
+	static constexpr int WAVES_PER_EU = tile_imax(1, WG_PER_CU * WAVES / 4);
+	static_assert(HALVES == tile_halves(W, IN, NH, NS), "layout");
+	static_assert(oWh % 8 == 0 && oWo % 8 == 0 && oX % 8 == 0 && oA % 8 == 0 && oG % 8 == 0, "16-byte alignment");
+	static_assert(BYTES <= tile_lds_limit(), "tile exceeds the LDS");
+};
+
+struct TileTrainArgs {
+	uint32_t B, dims, loss_l2;
+	float loss_scale, n_total;
+	int out_act;             // output activation (ACT_*), applied after the output layer, transfer before the backward
+	const _Float16* params;  // [W0 | hidden | Wout] fp16 (unpadded width WR)
+	const _Float16* wT;      // streamed hidden matrices 1..NS transposed, [NS][W (in)][W (out)] fp16
+	const _Float16* enc;     // encoded input fp16 [B][IN]
+	const float* target;     // [B][dims] (loss)
+	const _Float16* dout;    // external dL/d(output) fp16 [B][16] (loss-scaled by the caller; nullptr: the loss)
+	_Float16* out;           // optional network output fp16 [B][16]
+	void* dldenc;            // optional dL/d(encoding): pairs [IN/2][B] (uint32) or AoS fp16 [B][IN]
+	int dldenc_pairs;
+	float* wgrad_partial;    // [gridDim.x][N_MLP]
+	float* loss_partial;     // [gridDim.x]
+};
+
+__device__ __forceinline__ h8 zero8() { return h8{0, 0, 0, 0, 0, 0, 0, 0}; }
+
+template <Act ACT>
+__device__ __forceinline__ h4 tile_act(f4 v) {
+	return act_fwd<ACT>(v);
+}
+
+// output activation on the fp32 accumulator, rounded once (the layer-wise engine's order)
+__device__ __forceinline__ h4 out_act_fwd(int a, f4 y) {
+	if (a == ACT_NONE) return __builtin_convertvector(y, h4);
+	h4 r;
+#pragma unroll
+	for (int k = 0; k < 4; ++k) r[k] = f16_rn(act_fwd_ool(a, y[k]));
+	return r;
+}
+
+// launch bounds as plain function calls (a template-id's commas would split the macro arguments)
+constexpr int tile_train_nthr(int WR, int NH) { return tile_waves(tile_kw(WR), NH) * 64; }
+constexpr int tile_train_weu(int WR, int IN, int NH) {
+	return tile_imax(1, tile_train_wg_per_cu(tile_kw(WR), IN, NH) * tile_waves(tile_kw(WR), NH) / 4);
+}
+
+template <int WR, int IN, int NH, Act ACT>
+__global__ __launch_bounds__(tile_train_nthr(WR, NH), tile_train_weu(WR, IN, NH)) void k_mlp_tile_train(const TileTrainArgs a) {
+	using L = TileLayout<WR, IN, NH>;
+	constexpr int W = L::W;
+	constexpr int MTW = L::MTW, KT0 = L::KT0, RS0 = L::RS0, RSW = L::RSW, RSG = L::RSG;
+	constexpr int WAVES = L::WAVES, NTHR = L::NTHR;
+	constexpr int NTW = L::MT / WAVES;  // Wout column tiles per wave (= MTW)
+	extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
+	const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+	const int c = lane & 15, q = lane >> 4;
+	const f4 fz = {0.0f, 0.0f, 0.0f, 0.0f};
+	float* wloss = (float*)(smem + L::HALVES);
+	const bool ext = a.dout != nullptr;
+
+	// ---- weights -> LDS (rows padded; first-layer columns [IN, KP0) and W16's padded neurons zero) ----
+	{
+		const _Float16* p = a.params;
+		for (int idx = tid; idx < W * (L::KP0 / 8); idx += NTHR) {
+			const int r = idx / (L::KP0 / 8), c8 = idx % (L::KP0 / 8);
+			*(h8*)(smem + L::oW0 + r * RS0 + 8 * c8) = (r < WR && 8 * c8 < IN) ? *(const h8*)(p + (size_t)r * IN + 8 * c8) : zero8();
+		}
+		p += WR * IN;
+		for (int idx = tid; idx < (NH - 1 - L::NS) * W * (W / 8); idx += NTHR) {
+			const int r = idx / (W / 8), c8 = idx % (W / 8);  // r over the staged hidden rows
+			const int j = r / W + L::NS, rr = r % W;
+			*(h8*)(smem + L::oWh + r * RSW + 8 * c8) =
+			    (rr < WR && 8 * c8 < WR) ? *(const h8*)(p + ((size_t)j * WR + rr) * WR + 8 * c8) : zero8();
+		}
+		p += (NH - 1) * WR * WR;
+		for (int idx = tid; idx < 16 * (W / 8); idx += NTHR) {
+			const int r = idx / (W / 8), c8 = idx % (W / 8);
+			*(h8*)(smem + L::oWo + r * RSW + 8 * c8) = 8 * c8 < WR ? *(const h8*)(p + (size_t)r * WR + 8 * c8) : zero8();
+		}
+		// zero the padded input columns of slot 0 once (the input loads never write them)
+		if (L::KP0 > IN)
+			for (int idx = tid; idx < 32 * (L::KP0 - IN); idx += NTHR)
+				smem[L::oX + (idx / (L::KP0 - IN)) * RS0 + IN + idx % (L::KP0 - IN)] = (_Float16)0.0f;
+	}
+	// staged matrices (m == 0 or m > NS); streamed ones (1 <= m <= NS) are read from global memory
+	auto Wm = [&](int m) -> const _Float16* { return m == 0 ? smem + L::oW0 : smem + L::oWh + (m - 1 - L::NS) * W * RSW; };
+	auto streamed = [](int m) { return m >= 1 && m <= L::NS; };
+	auto slot = [&](int m) -> _Float16* { return m == 0 ? smem + L::oX : smem + L::oA + (m - 1) * 32 * RSW; };
+	_Float16* sG = smem + L::oG;
+
+	// ---- register accumulators of this wave's weight-gradient rows ----
+	f4 dW0[MTW][KT0];
+	f4 dWh[NH > 1 ? NH - 1 : 1][MTW][L::MT];
+	f4 dWo[NTW];
+#pragma unroll
+	for (int i = 0; i < MTW; ++i) {
+#pragma unroll
+		for (int k = 0; k < KT0; ++k) dW0[i][k] = fz;
+#pragma unroll
+		for (int j = 0; j < (NH > 1 ? NH - 1 : 1); ++j)
+#pragma unroll
+			for (int k = 0; k < L::MT; ++k) dWh[j][i][k] = fz;
+	}
+#pragma unroll
+	for (int i = 0; i < NTW; ++i) dWo[i] = fz;
+	float loss = 0.0f;
+
+	// input rows of a tile: IN/8 16-byte vectors per sample
+	constexpr int XV = 32 * IN / 8, XPT = (XV + NTHR - 1) / NTHR;
+	const uint32_t n_tiles = a.B / 32;
+	uint32_t tile = blockIdx.x;
+	h8 xr[XPT];
+	auto load_x = [&](uint32_t t) {
+#pragma unroll
+		for (int j = 0; j < XPT; ++j) {
+			const int idx = tid + NTHR * j;
+			if (idx < XV) xr[j] = *(const h8*)(a.enc + ((size_t)t * 32 + idx / (IN / 8)) * IN + 8 * (idx % (IN / 8)));
+		}
+	};
+	if (tile < n_tiles) load_x(tile);
+	__syncthreads();
+
+	for (; tile < n_tiles; tile += gridDim.x) {
+		const uint32_t base = tile * 32;
+		// ---- input tile -> slot 0; prefetch the next tile's rows ----
+#pragma unroll
+		for (int j = 0; j < XPT; ++j) {
+			const int idx = tid + NTHR * j;
+			if (idx < XV) *(h8*)(slot(0) + (idx / (IN / 8)) * RS0 + 8 * (idx % (IN / 8))) = xr[j];
+		}
+		if (tile + gridDim.x < n_tiles) load_x(tile + gridDim.x);
+		// targets / external dL/dy of this wave's output lanes (waves 0, 1: sample tile tau = wave)
+		float tg[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+		h4 gext = zero4();
+		if (wave < 2) {
+			const uint32_t i = base + 16 * wave + c;
+			if (ext) {
+				gext = *(const h4*)(a.dout + (size_t)i * 16 + 4 * q);
+			} else {
+#pragma unroll
+				for (int r = 0; r < 4; ++r)
+					if (4 * q + r < (int)a.dims) tg[r] = a.target[(size_t)i * a.dims + 4 * q + r];
+			}
+		}
+		__syncthreads();
+
+		// ---- forward: a_{m+1} = act(M_m a_m), this wave's output-row tiles ----
+#pragma unroll
+		for (int m = 0; m < NH; ++m) {
+			const int KS = (m == 0 ? L::KP0 : W) / 32;
+			const int rsi = m == 0 ? RS0 : RSW;
+			const _Float16* Wt = streamed(m) ? nullptr : Wm(m);
+			const _Float16* in = slot(m);
+			f4 acc[MTW][2];
+#pragma unroll
+			for (int i = 0; i < MTW; ++i) acc[i][0] = acc[i][1] = fz;
+			h8 ag[MTW][W / 32];  // a streamed layer's A fragments, all loads issued before the first MFMA
+			if (streamed(m)) {
+				const _Float16* Wg = a.params + (size_t)W * IN + (size_t)(m - 1) * W * W;
+#pragma unroll
+				for (int i = 0; i < MTW; ++i)
+#pragma unroll
+					for (int s = 0; s < W / 32; ++s) ag[i][s] = *(const h8*)(Wg + (size_t)(16 * (wave * MTW + i) + c) * W + 32 * s + 8 * q);
+			}
+#pragma unroll
+			for (int s = 0; s < KS; ++s) {
+				const h8 b0 = *(const h8*)(in + c * rsi + 32 * s + 8 * q);
+				const h8 b1 = *(const h8*)(in + (16 + c) * rsi + 32 * s + 8 * q);
+#pragma unroll
+				for (int i = 0; i < MTW; ++i) {
+					const h8 af = streamed(m) ? ag[i][s] : *(const h8*)(Wt + (16 * (wave * MTW + i) + c) * rsi + 32 * s + 8 * q);
+					acc[i][0] = mfma16(af, b0, acc[i][0]);
+					acc[i][1] = mfma16(af, b1, acc[i][1]);
+				}
+			}
+			_Float16* outs = slot(m + 1);
+#pragma unroll
+			for (int i = 0; i < MTW; ++i)
+#pragma unroll
+				for (int tau = 0; tau < 2; ++tau)
+					*(h4*)(outs + (16 * tau + c) * RSW + 16 * (wave * MTW + i) + 4 * q) = tile_act<ACT>(acc[i][tau]);
+			__syncthreads();
+		}
+
+		// ---- output layer (+ output activation) + loss + output transfer (waves 0, 1: tau = wave) ----
+		if (wave < 2) {
+			const int tau = wave;
+			const _Float16* aN = slot(NH);
+			f4 y = fz;
+#pragma unroll
+			for (int s = 0; s < W / 32; ++s)
+				y = mfma16(*(const h8*)(smem + L::oWo + c * RSW + 32 * s + 8 * q), *(const h8*)(aN + (16 * tau + c) * RSW + 32 * s + 8 * q), y);
+			const uint32_t i = base + 16 * tau + c;
+			const h4 yh = out_act_fwd(a.out_act, y);
+			if (a.out) *(h4*)(a.out + (size_t)i * 16 + 4 * q) = yh;
+			h4 g = zero4();
+			if (ext) {
+				g = gext;
+			} else {
+#pragma unroll
+				for (int r = 0; r < 4; ++r) {
+					const uint32_t o = 4 * q + r;
+					if (o < a.dims) {
+						const float p = (float)yh[r];
+						const float pse = a.loss_l2 ? 1.0f : __builtin_fmaf(p, p, 0.01f);  // relative_l2.h:67-75 / l2.h:66-74
+						const float d = p - tg[r];
+						loss += d * d / pse / a.n_total;
+						g[r] = f16_rn(a.loss_scale * (2.0f * d / pse) / a.n_total);
+					}
+				}
+			}
+			// output-activation transfer given the output (fully_fused_mlp.cu:759-762)
+			if (a.out_act != ACT_NONE) {
+#pragma unroll
+				for (int r = 0; r < 4; ++r) g[r] = f16_rn(act_bwd_ool(a.out_act, (float)g[r], (float)yh[r]));
+			}
+			*(h4*)(sG + (16 * tau + c) * RSG + 4 * q) = g;
+		}
+		__syncthreads();
+
+		// ---- dWout += G^T a_NH ; delta_NH = act'(a_NH) * (Wout^T G) ----
+		h4 dl[MTW][2];
+		{
+			const _Float16* aN = slot(NH);
+			const h8 ga = lds_trfrag(sG, RSG, q, c, 0);  // A[out c][sample 8q+e]
+#pragma unroll
+			for (int i = 0; i < NTW; ++i) dWo[i] = mfma16(ga, lds_trfrag(aN, RSW, q, c, wave * NTW + i), dWo[i]);
+			h8 gb[2];
+#pragma unroll
+			for (int tau = 0; tau < 2; ++tau) gb[tau] = q < 2 ? *(const h8*)(sG + (16 * tau + c) * RSG + 8 * q) : zero8();
+#pragma unroll
+			for (int i = 0; i < MTW; ++i) {
+				const int mt = wave * MTW + i;
+				// A[neuron][out 8q+e]: K = 16 outputs, the upper half of the MFMA depth is zero through gb.
+				// Every lane takes part in the transpose read (lanes q >= 2 re-read rows 0..15): the
+				// ds_read_b64_tr_b16 exchange under a partial EXEC mask returned garbage (NaN deltas).
+				const h8 af = lds_trfrag(smem + L::oWo, RSW, q & 1, c, mt);
+#pragma unroll
+				for (int tau = 0; tau < 2; ++tau) {
+					const f4 v = mfma16(af, gb[tau], fz);
+					dl[i][tau] = act_bwd<ACT>(*(const h4*)(aN + (16 * tau + c) * RSW + 16 * mt + 4 * q), v);
+				}
+			}
+		}
+		__syncthreads();
+		{
+			_Float16* aN = slot(NH);
+#pragma unroll
+			for (int i = 0; i < MTW; ++i)
+#pragma unroll
+				for (int tau = 0; tau < 2; ++tau) *(h4*)(aN + (16 * tau + c) * RSW + 16 * (wave * MTW + i) + 4 * q) = dl[i][tau];
+		}
+		__syncthreads();
+
+		// ---- hidden layers and the first layer, last to first ----
+#pragma unroll
+		for (int m = NH - 1; m >= 0; --m) {
+			const _Float16* dsl = slot(m + 1);  // delta_{m+1} [sample][neuron]
+			const _Float16* am = slot(m);       // a_m [sample][feature]
+			const int rsm = m == 0 ? RS0 : RSW;
+			// a streamed matrix's transposed A fragments (A[feature][neuron] = M^T rows of this wave's
+			// tiles), loaded ahead so the latency hides behind the weight-gradient MFMAs
+			h8 agT[MTW][W / 32];
+			if (streamed(m)) {
+				const _Float16* WgT = a.wT + (size_t)(m - 1) * W * W;
+#pragma unroll
+				for (int i = 0; i < MTW; ++i)
+#pragma unroll
+					for (int s = 0; s < W / 32; ++s) agT[i][s] = *(const h8*)(WgT + (size_t)(16 * (wave * MTW + i) + c) * W + 32 * s + 8 * q);
+			}
+			// dW_m += delta_{m+1} a_m^T (contraction over the tile's 32 samples)
+#pragma unroll
+			for (int i = 0; i < MTW; ++i) {
+				const h8 ad = lds_trfrag(dsl, RSW, q, c, wave * MTW + i);  // A[neuron][sample]
+				if (m == 0) {
+#pragma unroll
+					for (int k = 0; k < KT0; ++k) dW0[i][k] = mfma16(ad, lds_trfrag(am, rsm, q, c, k), dW0[i][k]);
+				} else {
+#pragma unroll
+					for (int k = 0; k < L::MT; ++k) dWh[m > 0 ? m - 1 : 0][i][k] = mfma16(ad, lds_trfrag(am, rsm, q, c, k), dWh[m > 0 ? m - 1 : 0][i][k]);
+				}
+			}
+			// delta_m = act'(a_m) * (M_m^T delta_{m+1})  (m == 0: dL/d(encoding), no transfer)
+			const _Float16* Mt = streamed(m) ? nullptr : Wm(m);
+			if (m > 0) {
+#pragma unroll
+				for (int i = 0; i < MTW; ++i) {
+					const int t = wave * MTW + i;
+					f4 v0 = fz, v1 = fz;
+#pragma unroll
+					for (int s = 0; s < W / 32; ++s) {
+						const h8 af = streamed(m) ? agT[i][s] : lds_trfrag(Mt + 32 * s * rsm, rsm, q, c, t);  // A[feature][neuron 32s+8q+e]
+						v0 = mfma16(af, *(const h8*)(dsl + c * RSW + 32 * s + 8 * q), v0);
+						v1 = mfma16(af, *(const h8*)(dsl + (16 + c) * RSW + 32 * s + 8 * q), v1);
+					}
+					dl[i][0] = act_bwd<ACT>(*(const h4*)(am + c * rsm + 16 * t + 4 * q), v0);
+					dl[i][1] = act_bwd<ACT>(*(const h4*)(am + (16 + c) * rsm + 16 * t + 4 * q), v1);
+				}
+				__syncthreads();
+				_Float16* dst = slot(m);  // a_m is dead: delta_m takes its slot
+#pragma unroll
+				for (int i = 0; i < MTW; ++i)
+#pragma unroll
+					for (int tau = 0; tau < 2; ++tau) *(h4*)(dst + (16 * tau + c) * RSW + 16 * (wave * MTW + i) + 4 * q) = dl[i][tau];
+				__syncthreads();
+			} else if (a.dldenc) {
+				for (int t = wave; t < KT0; t += WAVES) {
+					f4 v[2] = {fz, fz};
+#pragma unroll
+					for (int s = 0; s < W / 32; ++s) {
+						const h8 af = lds_trfrag(Mt + 32 * s * RS0, RS0, q, c, t);
+#pragma unroll
+						for (int tau = 0; tau < 2; ++tau) v[tau] = mfma16(af, *(const h8*)(dsl + (16 * tau + c) * RSW + 32 * s + 8 * q), v[tau]);
+					}
+#pragma unroll
+					for (int tau = 0; tau < 2; ++tau) {
+						const h4 d = __builtin_convertvector(v[tau], h4);
+						const uint32_t i = base + 16 * tau + c;
+						if (a.dldenc_pairs) {  // features 16t + 4q + r -> levels 8t + 2q (r = 0, 1), + 1 (r = 2, 3)
+							uint32_t* d2 = (uint32_t*)a.dldenc;
+							const uint32_t lv = 8 * t + 2 * q;
+							d2[(size_t)lv * a.B + i] = __builtin_bit_cast(uint32_t, h2{d[0], d[1]});
+							d2[(size_t)(lv + 1) * a.B + i] = __builtin_bit_cast(uint32_t, h2{d[2], d[3]});
+						} else {
+							*(h4*)((_Float16*)a.dldenc + (size_t)i * IN + 16 * t + 4 * q) = d;
+						}
+					}
+				}
+				__syncthreads();
+			} else {
+				__syncthreads();
+			}
+		}
+	}
+
+	// ---- this workgroup's weight-gradient partial slab (each parameter owned by one lane) ----
+	float* dst = a.wgrad_partial + (size_t)blockIdx.x * L::N_MLP;
+#pragma unroll
+	for (int i = 0; i < MTW; ++i) {
+#pragma unroll
+		for (int r = 0; r < 4; ++r) {
+			const int row = 16 * (wave * MTW + i) + 4 * q + r;
+			if (row < WR) {
+#pragma unroll
+				for (int k = 0; k < KT0; ++k) dst[row * IN + 16 * k + c] = dW0[i][k][r];
+#pragma unroll
+				for (int j = 0; j < NH - 1; ++j)
+#pragma unroll
+					for (int k = 0; k < L::MT; ++k)
+						if (16 * k + c < WR) dst[WR * IN + j * WR * WR + row * WR + 16 * k + c] = dWh[j][i][k][r];
+			}
+		}
+	}
+#pragma unroll
+	for (int i = 0; i < NTW; ++i)
+#pragma unroll
+		for (int r = 0; r < 4; ++r)
+			if (16 * (wave * NTW + i) + c < WR) dst[WR * IN + (NH - 1) * WR * WR + (4 * q + r) * WR + 16 * (wave * NTW + i) + c] = dWo[i][r];
+#pragma unroll
+	for (int off = 32; off > 0; off >>= 1) loss += __shfl_xor(loss, off);
+	if (lane == 0) wloss[wave] = loss;
+	__syncthreads();
+	if (tid == 0) {
+		float l = 0.0f;
+		for (int w = 0; w < WAVES; ++w) l += wloss[w];
+		a.loss_partial[blockIdx.x] = l;
+	}
+}
+
+// ---------------------------------------------------------------------------------------------
+// inference
+// ---------------------------------------------------------------------------------------------
+// inference geometry (plain functions: also used in the kernel's launch bounds)
+constexpr int tile_infer_nthr(int WR) { return 64 * (tile_kw(WR) / 32); }  // waves: two row tiles each
+constexpr int tile_infer_T(int WR) { return tile_kw(WR) >= 128 ? 32 : 64; }  // samples per tile
+// hidden matrices whose A fragments stay in registers: 176 VGPRs for A (W0: 8 per 32 inputs, Wout: 4
+// per 32 neurons, hidden: 8 per 32 neurons)
+constexpr int tile_infer_nrh(int WR, int IN, int NH) {
+	return tile_imax(0, tile_imin(NH - 1, (176 - 8 * ((IN + 31) / 32) - 4 * (tile_kw(WR) / 32)) / (8 * (tile_kw(WR) / 32))));
+}
+constexpr int tile_infer_bytes(int WR, int IN, int NH) {
+	return 2 * ((NH - 1 - tile_infer_nrh(WR, IN, NH)) * tile_kw(WR) * (tile_kw(WR) + 8) + tile_infer_T(WR) * ((IN + 31) / 32 * 32 + 8) +
+	            2 * tile_infer_T(WR) * (tile_kw(WR) + 8));
+}
+constexpr int tile_infer_weu(int WR, int IN, int NH) {
+	return tile_imax(1, tile_imax(1, tile_imin(8 / (tile_kw(WR) / 32), tile_lds_limit() / tile_infer_bytes(WR, IN, NH))) * (tile_kw(WR) / 32) / 4);
+}
+
+template <int WR, int IN, int NH>
+struct TileInferLayout {
+	static constexpr int W = tile_kw(WR);
+	static constexpr int KP0 = (IN + 31) / 32 * 32, RS0 = KP0 + 8, RSW = W + 8;
+	static constexpr int MT = W / 16, MTW = 2, WAVES = MT / MTW;  // W128 4 waves, W64 2, W32 (and W16) 1
+	static constexpr int NTHR = 64 * WAVES;
+	static constexpr int KS0 = KP0 / 32, KSW = W / 32;
+	// A fragments kept in registers (VGPRs per wave): W0 and Wout always, hidden matrices 1..NRH while
+	// the budget lasts (all of them for every instantiated shape); the rest are staged in LDS
+	static constexpr int NRH = tile_infer_nrh(WR, IN, NH);
+	static constexpr int NLH = NH - 1 - NRH;
+	static constexpr int T = tile_infer_T(WR), NST = T / 16;  // samples per tile / 16-sample MFMA columns
+	static constexpr int oWl = 0;                     // LDS hidden matrices NRH+1.. [NLH][W][RSW]
+	static constexpr int oX = oWl + NLH * W * RSW;    // input tile [T][RS0]
+	static constexpr int oP = oX + T * RS0;           // activation tiles [2][T][RSW]
+	static constexpr int HALVES = oP + 2 * T * RSW;
+	static constexpr int BYTES = HALVES * 2;
+	static constexpr int WG_PER_CU = tile_imax(1, tile_imin(8 / WAVES, tile_lds_limit() / BYTES));
+	static constexpr int WAVES_PER_EU = tile_imax(1, WG_PER_CU * WAVES / 4);
+	static_assert(BYTES <= tile_lds_limit(), "tile inference exceeds the LDS");
+	static_assert(BYTES == tile_infer_bytes(WR, IN, NH) && NTHR == tile_infer_nthr(WR) && WAVES_PER_EU == tile_infer_weu(WR, IN, NH),
+	              "launch-bound helpers");
+	static_assert(oX % 8 == 0 && oP % 8 == 0, "16-byte alignment");
+};
+
+struct TileInferArgs {
+	uint32_t B;
+	int out_act;
+	const _Float16* params;  // [W0 | hidden | Wout] fp16 (unpadded width WR)
+	const _Float16* enc;     // encoded input fp16 [B][IN]
+	_Float16* out;           // network output fp16 [B][16]
+};
+
+template <int WR, int IN, int NH, Act ACT>
+__global__ __launch_bounds__(tile_infer_nthr(WR), tile_infer_weu(WR, IN, NH)) void k_mlp_tile_infer(const TileInferArgs a) {
+	using L = TileInferLayout<WR, IN, NH>;
+	constexpr int W = L::W, MTW = L::MTW, WAVES = L::WAVES, NTHR = L::NTHR, T = L::T, NST = L::NST;
+	constexpr int RS0 = L::RS0, RSW = L::RSW, KS0 = L::KS0, KSW = L::KSW, NRH = L::NRH;
+	extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
+	const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+	const int c = lane & 15, q = lane >> 4;
+	const f4 fz = {0.0f, 0.0f, 0.0f, 0.0f};
+	_Float16* X = smem + L::oX;
+	_Float16* P0 = smem + L::oP;
+	_Float16* P1 = smem + L::oP + T * RSW;
+
+	// ---- weight-stationary A fragments (rows 16 (wave MTW + i) + c, columns 32 s + 8 q ..+7) ----
+	const _Float16* p = a.params;
+	h8 aw0[MTW][KS0];
+	h8 awh[NRH > 0 ? NRH : 1][MTW][KSW];
+	h8 awo[KSW];
+#pragma unroll
+	for (int i = 0; i < MTW; ++i) {
+		const int row = 16 * (wave * MTW + i) + c;
+#pragma unroll
+		for (int s = 0; s < KS0; ++s) {
+			const int col = 32 * s + 8 * q;
+			aw0[i][s] = (row < WR && col < IN) ? *(const h8*)(p + (size_t)row * IN + col) : zero8();
+		}
+#pragma unroll
+		for (int j = 0; j < NRH; ++j)
+#pragma unroll
+			for (int s = 0; s < KSW; ++s) {
+				const int col = 32 * s + 8 * q;
+				awh[j][i][s] = (row < WR && col < WR) ? *(const h8*)(p + (size_t)WR * IN + ((size_t)j * WR + row) * WR + col) : zero8();
+			}
+	}
+	const _Float16* pwo = p + (size_t)WR * IN + (size_t)(NH - 1) * WR * WR;
+#pragma unroll
+	for (int s = 0; s < KSW; ++s) awo[s] = 32 * s + 8 * q < WR ? *(const h8*)(pwo + (size_t)c * WR + 32 * s + 8 * q) : zero8();
+	// hidden matrices beyond the register budget -> LDS
+	for (int idx = tid; idx < L::NLH * W * (W / 8); idx += NTHR) {
+		const int r = idx / (W / 8), c8 = idx % (W / 8);
+		const int j = r / W + NRH, rr = r % W;
+		*(h8*)(smem + L::oWl + r * RSW + 8 * c8) = (rr < WR && 8 * c8 < WR) ? *(const h8*)(p + (size_t)WR * IN + ((size_t)j * WR + rr) * WR + 8 * c8) : zero8();
+	}
+	// zero the padded input columns once (the input loads never write them)
+	if (L::KP0 > IN)
+		for (int idx = tid; idx < T * (L::KP0 - IN); idx += NTHR) X[(idx / (L::KP0 - IN)) * RS0 + IN + idx % (L::KP0 - IN)] = (_Float16)0.0f;
+
+	constexpr int XV = T * IN / 8, XPT = (XV + NTHR - 1) / NTHR;
+	const uint32_t n_tiles = (a.B + T - 1) / T;
+	uint32_t tile = blockIdx.x;
+	h8 xr[XPT];
+	auto load_x = [&](uint32_t t) {
+#pragma unroll
+		for (int j = 0; j < XPT; ++j) {
+			const int idx = tid + NTHR * j;
+			const uint32_t row = t * T + idx / (IN / 8);
+			if (idx < XV) xr[j] = row < a.B ? *(const h8*)(a.enc + (size_t)row * IN + 8 * (idx % (IN / 8))) : zero8();
+		}
+	};
+	if (tile < n_tiles) load_x(tile);
+
+	for (; tile < n_tiles; tile += gridDim.x) {
+		const uint32_t base = tile * T;
+#pragma unroll
+		for (int j = 0; j < XPT; ++j) {
+			const int idx = tid + NTHR * j;
+			if (idx < XV) *(h8*)(X + (idx / (IN / 8)) * RS0 + 8 * (idx % (IN / 8))) = xr[j];
+		}
+		if (tile + gridDim.x < n_tiles) load_x(tile + gridDim.x);
+		__syncthreads();
+
+#pragma unroll
+		for (int m = 0; m < NH; ++m) {
+			const _Float16* in = m == 0 ? X : ((m - 1) & 1 ? P1 : P0);
+			_Float16* outp = (m & 1) ? P1 : P0;
+			const int rsi = m == 0 ? RS0 : RSW;
+			const int KS = m == 0 ? KS0 : KSW;
+			f4 acc[MTW][NST];
+#pragma unroll
+			for (int i = 0; i < MTW; ++i)
+#pragma unroll
+				for (int tau = 0; tau < NST; ++tau) acc[i][tau] = fz;
+#pragma unroll
+			for (int s = 0; s < KS; ++s) {
+				h8 b[NST];
+#pragma unroll
+				for (int tau = 0; tau < NST; ++tau) b[tau] = *(const h8*)(in + (16 * tau + c) * rsi + 32 * s + 8 * q);
+#pragma unroll
+				for (int i = 0; i < MTW; ++i) {
+					h8 af;
+					if (m == 0) af = aw0[i][s];
+					else if (m - 1 < NRH) af = awh[m - 1 < NRH ? m - 1 : 0][i][s];
+					else af = *(const h8*)(smem + L::oWl + (m - 1 - NRH) * W * RSW + (16 * (wave * MTW + i) + c) * RSW + 32 * s + 8 * q);
+#pragma unroll
+					for (int tau = 0; tau < NST; ++tau) acc[i][tau] = mfma16(af, b[tau], acc[i][tau]);
+				}
+			}
+#pragma unroll
+			for (int i = 0; i < MTW; ++i)
+#pragma unroll
+				for (int tau = 0; tau < NST; ++tau)
+					*(h4*)(outp + (16 * tau + c) * RSW + 16 * (wave * MTW + i) + 4 * q) = tile_act<ACT>(acc[i][tau]);
+			__syncthreads();
+		}
+
+		// ---- output layer: 16 rows, one 16-sample tile per wave at a time ----
+		const _Float16* aN = ((NH - 1) & 1) ? P1 : P0;
+#pragma unroll
+		for (int tau = wave; tau < NST; tau += WAVES) {
+			f4 y = fz;
+#pragma unroll
+			for (int s = 0; s < KSW; ++s) y = mfma16(awo[s], *(const h8*)(aN + (16 * tau + c) * RSW + 32 * s + 8 * q), y);
+			const uint32_t i = base + 16 * tau + c;
+			if (i < a.B) *(h4*)(a.out + (size_t)i * 16 + 4 * q) = out_act_fwd(a.out_act, y);
+		}
+	}
+}
+
+// ---------------------------------------------------------------------------------------------
+// per-width dispatch (mlp_tile_w*.hip)
+// ---------------------------------------------------------------------------------------------
+#define TCNN_TILE_SHAPES_OF(X, w) \
+	X(w, 16, 1) X(w, 16, 2) X(w, 16, 3) X(w, 16, 4) X(w, 16, 5) \
+	X(w, 32, 1) X(w, 32, 2) X(w, 32, 3) X(w, 32, 4) X(w, 32, 5) \
+	X(w, 64, 1) X(w, 64, 2) X(w, 64, 3) X(w, 64, 4) X(w, 64, 5) \
+	X(w, 128, 1) X(w, 128, 2) X(w, 128, 3) X(w, 128, 4) X(w, 128, 5)
+
+struct TileShapeInfo {
+	uint32_t lds_bytes, n_streamed, wg_per_cu, waves;  // training
+	uint32_t infer_lds_bytes, infer_wg_per_cu, infer_tile;
+};
+
+// per-width entry points (one translation unit per width); false if (IN, NH) is not instantiated
+bool tile_shape_w16(uint32_t IN, uint32_t NH, TileShapeInfo* info);
+bool tile_shape_w32(uint32_t IN, uint32_t NH, TileShapeInfo* info);
+bool tile_shape_w64(uint32_t IN, uint32_t NH, TileShapeInfo* info);
+bool tile_shape_w128(uint32_t IN, uint32_t NH, TileShapeInfo* info);
+bool tile_train_w16(hipStream_t st, uint32_t IN, uint32_t NH, int act, uint32_t blocks, const TileTrainArgs& a);
+bool tile_train_w32(hipStream_t st, uint32_t IN, uint32_t NH, int act, uint32_t blocks, const TileTrainArgs& a);
+bool tile_train_w64(hipStream_t st, uint32_t IN, uint32_t NH, int act, uint32_t blocks, const TileTrainArgs& a);
+bool tile_train_w128(hipStream_t st, uint32_t IN, uint32_t NH, int act, uint32_t blocks, const TileTrainArgs& a);
+bool tile_infer_w16(hipStream_t st, uint32_t IN, uint32_t NH, int act, uint32_t blocks, const TileInferArgs& a);
+bool tile_infer_w32(hipStream_t st, uint32_t IN, uint32_t NH, int act, uint32_t blocks, const TileInferArgs& a);
+bool tile_infer_w64(hipStream_t st, uint32_t IN, uint32_t NH, int act, uint32_t blocks, const TileInferArgs& a);
+bool tile_infer_w128(hipStream_t st, uint32_t IN, uint32_t NH, int act, uint32_t blocks, const TileInferArgs& a);
+
+// the definitions of one width's entry points (used once per mlp_tile_w*.hip)
+#define TCNN_TILE_WIDTH_TU(w)                                                                                                    \
+	template <int IN, int NH, Act A>                                                                                             \
+	static void tile_train_launch_##w(hipStream_t st, uint32_t blocks, const TileTrainArgs& a) {                                 \
+		using L = TileLayout<w, IN, NH>;                                                                                         \
+		static uint64_t done = 0;                                                                                                \
+		set_dyn_lds((const void*)k_mlp_tile_train<w, IN, NH, A>, L::BYTES, done);                                                \
+		hipLaunchKernelGGL((k_mlp_tile_train<w, IN, NH, A>), dim3(blocks), dim3(L::NTHR), L::BYTES, st, a);                     \
+	}                                                                                                                            \
+	template <int IN, int NH, Act A>                                                                                             \
+	static void tile_infer_launch_##w(hipStream_t st, uint32_t blocks, const TileInferArgs& a) {                                 \
+		using L = TileInferLayout<w, IN, NH>;                                                                                    \
+		static uint64_t done = 0;                                                                                                \
+		set_dyn_lds((const void*)k_mlp_tile_infer<w, IN, NH, A>, L::BYTES, done);                                                \
+		hipLaunchKernelGGL((k_mlp_tile_infer<w, IN, NH, A>), dim3(blocks), dim3(L::NTHR), L::BYTES, st, a);                     \
+	}                                                                                                                            \
+	bool tile_shape_w##w(uint32_t IN, uint32_t NH, TileShapeInfo* info) {                                                        \
+		TCNN_TILE_SHAPES_OF(TCNN_TILE_INFO_X, w)                                                                                 \
+		return false;                                                                                                            \
+	}                                                                                                                            \
+	bool tile_train_w##w(hipStream_t st, uint32_t IN, uint32_t NH, int act, uint32_t blocks, const TileTrainArgs& a) {           \
+		TCNN_TILE_SHAPES_OF(TCNN_TILE_TRAIN_X, w)                                                                                \
+		return false;                                                                                                            \
+	}                                                                                                                            \
+	bool tile_infer_w##w(hipStream_t st, uint32_t IN, uint32_t NH, int act, uint32_t blocks, const TileInferArgs& a) {           \
+		TCNN_TILE_SHAPES_OF(TCNN_TILE_INFER_X, w)                                                                                \
+		return false;                                                                                                            \
+	}
+
+#define TCNN_TILE_INFO_X(w, in, nh)                                                                                              \
+	if (IN == in && NH == nh) {                                                                                                  \
+		using L = TileLayout<w, in, nh>;                                                                                         \
+		using LI = TileInferLayout<w, in, nh>;                                                                                   \
+		*info = TileShapeInfo{(uint32_t)L::BYTES, (uint32_t)L::NS, (uint32_t)L::WG_PER_CU, (uint32_t)L::WAVES,                  \
+		                      (uint32_t)LI::BYTES, (uint32_t)LI::WG_PER_CU, (uint32_t)LI::T};                                    \
+		return true;                                                                                                             \
+	}
+#define TCNN_TILE_TRAIN_X(w, in, nh)                                                                                             \
+	if (IN == in && NH == nh) {                                                                                                  \
+		if (act == ACT_RELU) tile_train_launch_##w<in, nh, Act::ReLU>(st, blocks, a);                                            \
+		else tile_train_launch_##w<in, nh, Act::None>(st, blocks, a);                                                            \
+		return true;                                                                                                             \
+	}
+#define TCNN_TILE_INFER_X(w, in, nh)                                                                                             \
+	if (IN == in && NH == nh) {                                                                                                  \
+		if (act == ACT_RELU) tile_infer_launch_##w<in, nh, Act::ReLU>(st, blocks, a);                                            \
+		else tile_infer_launch_##w<in, nh, Act::None>(st, blocks, a);                                                            \
+		return true;                                                                                                             \
+	}
+
+}  // namespace tcnn_amd

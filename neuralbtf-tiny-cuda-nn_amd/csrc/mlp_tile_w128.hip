@@ -1,0 +1,7 @@
+// mlp_tile_w128.hip -- the tile engine's W128 instantiations (training + inference, every (IN, NH) of
+// TCNN_TILE_SHAPES_OF), one translation unit per width so they compile in parallel. See mlp_tile.h.
+#include "mlp_tile.h"
+
+namespace tcnn_amd {
+TCNN_TILE_WIDTH_TU(128)
+}  // namespace tcnn_amd

@@ -521,11 +521,23 @@ bool NetworkHost::fused_ok() const {
 	                             grid->desc.n_features_per_level, mlp.padded_output, mlp.activation, grid->desc.hash_type);
 }
 
-bool NetworkHost::tile_ok() const {
+bool NetworkHost::tile_shape_ok() const {
 	const bool ff = ieq(mlp.otype, "FullyFusedMLP") || ieq(mlp.otype, "MegakernelMLP");
-	if (!ff || fused_ok() || mlp.output_activation != 0) return false;
+	if (!ff || mlp.output_activation == ACT_SINE) return false;  // Sine has no post-activation backward (common_device.h:271-275)
 	if (std::getenv("TCNN_NO_TILE_ENGINE")) return false;  // A/B switch: the layer-wise engine instead
 	return tile_train_supported(mlp.width, mlp.n_input, mlp.n_hidden_layers, mlp.padded_output, mlp.activation);
+}
+
+bool NetworkHost::tile_ok() const { return !fused_ok() && tile_shape_ok(); }
+
+bool NetworkHost::tile_infer_ok() const {
+	return tile_shape_ok() && tile_infer_supported(mlp.width, mlp.n_input, mlp.n_hidden_layers, mlp.padded_output, mlp.activation);
+}
+
+const char* NetworkHost::inference_engine() const {
+	if (fused_ok() && mlp_infer_supported(mlp.width, mlp.n_input, mlp.n_hidden_layers, mlp.padded_output, mlp.activation)) return "fused";
+	if (tile_infer_ok()) return "fused";
+	return layered_ok() ? "layered" : "unsupported";
 }
 
 bool NetworkHost::layered_ok() const {
@@ -571,17 +583,56 @@ void NetworkHost::inference(hipStream_t st, StepWorkspace& ws, uint32_t B, const
 		launch_mlp_infer(st, mlp.width, IN, mlp.n_hidden_layers, mlp.activation, true, B, ws.wimage.p, ws.enc16.p, out16);
 		return;
 	}
-	TCNN_CHECK(layered_ok(), "inference: network shape not supported by the MI355X engine");
 	ws.enc16.reserve((size_t)IN * B * 2);
+	if (tile_infer_ok()) {  // the whole network in one launch (mlp_tile.h k_mlp_tile_infer)
+		enc->forward_aos(st, B, pos, eparams, ws.enc16.p);
+		launch_mlp_tile_infer(st, mlp.width, IN, mlp.n_hidden_layers, mlp.activation, mlp.output_activation, B, params16, ws.enc16.p, out16);
+		return;
+	}
+	TCNN_CHECK(layered_ok(), "inference: network shape not supported by the MI355X engine");
 	enc->forward_aos(st, B, pos, eparams, ws.enc16.p);
 	forward_layers(st, ws, B, params16, out16, false);
 }
 
+int NetworkHost::backward_engine_keep(bool with_dinput) const {
+	if (fused_ok() && !with_dinput) return KEEP_FUSED_SOA;
+	if (tile_shape_ok()) return KEEP_TILE_AOS;
+	return KEEP_NONE;
+}
+
+int NetworkHost::forward_keep(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const void* params16, void* out16,
+                              bool with_dinput, DevBuf& keep) {
+	const int layout = backward_engine_keep(with_dinput);
+	const uint32_t IN = mlp.n_input;
+	const uint8_t* eparams = (const uint8_t*)params16 + (size_t)mlp.n_params() * 2;
+	if (layout == KEEP_FUSED_SOA && mlp_infer_supported(mlp.width, IN, mlp.n_hidden_layers, mlp.padded_output, mlp.activation)) {
+		keep.reserve((size_t)IN * B * 2);
+		launch_grid_fwd(st, grid->desc.n_pos_dims, grid->desc.n_features_per_level, grid->desc.hash_type, B, grid->desc.n_levels, pos,
+		                grid->desc.n_pos_dims, eparams, keep.p, true, 0, grid->dev_levels(), grid->hash_grid(), grid->desc.interp);
+		ws.wimage.reserve(fused_weight_image_bytes(mlp.width, IN, mlp.n_hidden_layers));
+		launch_pack_weights(st, mlp.width, IN, mlp.n_hidden_layers, params16, ws.wimage.p);
+		launch_mlp_infer(st, mlp.width, IN, mlp.n_hidden_layers, mlp.activation, true, B, ws.wimage.p, keep.p, out16);
+		return KEEP_FUSED_SOA;
+	}
+	if (layout == KEEP_TILE_AOS && tile_infer_ok()) {
+		keep.reserve((size_t)IN * B * 2);
+		enc->forward_aos(st, B, pos, eparams, keep.p);
+		launch_mlp_tile_infer(st, mlp.width, IN, mlp.n_hidden_layers, mlp.activation, mlp.output_activation, B, params16, keep.p, out16);
+		return KEEP_TILE_AOS;
+	}
+	inference(st, ws, B, pos, params16, out16);
+	return KEEP_NONE;
+}
+
 void NetworkHost::fwd_bwd(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target, uint32_t dims,
                           float loss_scale, const void* params16, const void* dout16, void* out16, float* grad32,
-                          const std::function<void(int)>& mark, float* dL_dinput) {
-	if (fused_ok() && !dL_dinput) fwd_bwd_fused(st, ws, B, pos, target, dims, loss_scale, params16, dout16, out16, grad32, mark);
-	else if (tile_ok()) fwd_bwd_tile(st, ws, B, pos, target, dims, loss_scale, params16, dout16, out16, grad32, mark, dL_dinput);
+                          const std::function<void(int)>& mark, float* dL_dinput, const void* kept, int kept_layout) {
+	if (fused_ok() && !dL_dinput)
+		fwd_bwd_fused(st, ws, B, pos, target, dims, loss_scale, params16, dout16, out16, grad32, mark,
+		              kept_layout == KEEP_FUSED_SOA ? kept : nullptr);
+	else if (tile_shape_ok())
+		fwd_bwd_tile(st, ws, B, pos, target, dims, loss_scale, params16, dout16, out16, grad32, mark, dL_dinput,
+		             kept_layout == KEEP_TILE_AOS ? kept : nullptr);
 	else fwd_bwd_layered(st, ws, B, pos, target, dims, loss_scale, params16, dout16, out16, grad32, mark, dL_dinput);
 }
 
@@ -592,7 +643,7 @@ void NetworkHost::pack_weights(hipStream_t st, StepWorkspace& ws, const void* pa
 }
 
 void NetworkHost::fused_kernel(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target, uint32_t dims,
-                               float loss_scale, const void* params16, bool pack, const void* dout16, void* out16) {
+                               float loss_scale, const void* params16, bool pack, const void* dout16, void* out16, const void* enc_soa) {
 	TCNN_CHECK(B % 32 == 0, "training: batch must be a multiple of 32");
 	const uint32_t n_mlp = mlp.n_params();
 	const uint32_t L = grid->desc.n_levels, F = grid->desc.n_features_per_level;
@@ -609,7 +660,7 @@ void NetworkHost::fused_kernel(hipStream_t st, StepWorkspace& ws, uint32_t B, co
 	                   mlp.activation, B, dims, loss_scale, params16, table, pos, target, out16, ws.dLdenc.p,
 	                   ws.wgrad_partial.as<float>(), ws.loss_partial.as<float>(), grid->dev_levels(), grid->hash_grid(),
 	                   grid->desc.interp, nb, dout16, ws.wimage.p, loss_l2,
-	                   grid->inrange_index_ok && grid->desc.interp == Interp::Linear && !std::getenv("TCNN_NO_INRANGE_INDEX"));
+	                   grid->inrange_index_ok && grid->desc.interp == Interp::Linear && !std::getenv("TCNN_NO_INRANGE_INDEX"), enc_soa);
 }
 
 void NetworkHost::grid_backward(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, GridBwdEpilogue* ep) {
@@ -630,9 +681,9 @@ void NetworkHost::grid_backward(hipStream_t st, StepWorkspace& ws, uint32_t B, c
 
 void NetworkHost::fwd_bwd_fused(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target,
                                 uint32_t dims, float loss_scale, const void* params16, const void* dout16, void* out16, float* grad32,
-                                const std::function<void(int)>& mark) {
+                                const std::function<void(int)>& mark, const void* enc_soa) {
 	const uint32_t n_mlp = mlp.n_params();
-	fused_kernel(st, ws, B, pos, target, dims, loss_scale, params16, true, dout16, out16);
+	fused_kernel(st, ws, B, pos, target, dims, loss_scale, params16, true, dout16, out16, enc_soa);
 	if (mark) mark(1);
 	grid_backward(st, ws, B, pos);
 	grid->backward_acc(st, ws.gbw, B, ws.dLdenc.p, 0, 0, grad32 + n_mlp);
@@ -647,13 +698,16 @@ void NetworkHost::fwd_bwd_fused(hipStream_t st, StepWorkspace& ws, uint32_t B, c
 // the partial reduction, then the encoding's backward.
 void NetworkHost::fwd_bwd_tile(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target, uint32_t dims,
                                float loss_scale, const void* params16, const void* dout16, void* out16, float* grad32,
-                               const std::function<void(int)>& mark, float* dL_dinput) {
+                               const std::function<void(int)>& mark, float* dL_dinput, const void* enc_aos) {
 	TCNN_CHECK(B % 32 == 0, "training: batch must be a multiple of 32");
 	const uint32_t W = mlp.width, IN = mlp.n_input, NH = mlp.n_hidden_layers;
 	const uint32_t n_mlp = mlp.n_params();
 	const uint8_t* eparams = (const uint8_t*)params16 + (size_t)n_mlp * 2;
-	ws.enc16.reserve((size_t)B * IN * 2);
-	enc->forward_aos(st, B, pos, eparams, ws.enc16.p);
+	if (!enc_aos) {
+		ws.enc16.reserve((size_t)B * IN * 2);
+		enc->forward_aos(st, B, pos, eparams, ws.enc16.p);
+		enc_aos = ws.enc16.p;
+	}
 	const uint32_t nb = tile_train_blocks(B, W, IN, NH);
 	ws.wgrad_partial.reserve((size_t)nb * n_mlp * 4);
 	ws.loss_partial.reserve((size_t)nb * 4);
@@ -663,7 +717,8 @@ void NetworkHost::fwd_bwd_tile(hipStream_t st, StepWorkspace& ws, uint32_t B, co
 	if (enc_grad) ws.delta0.reserve((size_t)B * IN * 2);
 	const uint32_t wT_bytes = tile_train_wT_bytes(W, IN, NH);
 	if (wT_bytes) ws.tile_wT.reserve(wT_bytes);
-	launch_mlp_tile_train(st, W, IN, NH, mlp.activation, B, dims, loss_scale, loss_l2, params16, ws.enc16.p, target, dout16, out16,
+	launch_mlp_tile_train(st, W, IN, NH, mlp.activation, mlp.output_activation, B, dims, loss_scale, loss_l2, params16, enc_aos, target,
+	                      dout16, out16,
 	                      enc_grad ? ws.delta0.p : nullptr, pairs ? 1 : 0, ws.wgrad_partial.as<float>(), ws.loss_partial.as<float>(),
 	                      wT_bytes ? ws.tile_wT.p : nullptr);
 	ws.n_loss_partials = dout16 ? 0 : nb;

@@ -186,7 +186,8 @@ struct StepWorkspace {
 // NetworkWithInputEncoding<__half> (reference network_with_input_encoding.h:41-190) over two engines:
 //   "fused"   grid encoding + W in {32, 64} FullyFusedMLP: one register-resident kernel
 //             (mlp_fused.h) + the LDS-privatised grid backward;
-//   "fused"   (tile) W in {64, 128} FullyFusedMLP with any encoding (mlp_tile.hip);
+//   "fused"   (tile) W in {16, 32, 64, 128} FullyFusedMLP with any encoding (mlp_tile.h), training
+//             and inference;
 //   "layered" everything else (CutlassMLP, other widths, output activations):
 //             per-layer MFMA kernels (mlp_layers.hip) with fp16 activations in HBM.
 struct NetworkHost {
@@ -198,34 +199,49 @@ struct NetworkHost {
 	NetworkHost(uint32_t n_in, uint32_t n_out, const json& enc, const json& net);
 	uint64_t n_params() const { return (uint64_t)mlp.n_params() + enc->n_params(); }
 	bool fused_ok() const;   // register-resident kernel (mlp_fused.h): grid input, W <= 64
-	bool tile_ok() const;    // tile kernel (mlp_tile.hip): W in {64, 128}, any encoding, weights + tile in LDS
+	bool tile_shape_ok() const;  // tile kernels (mlp_tile.h): FullyFusedMLP W in {16..128}, any encoding, IN <= 128, H <= 5
+	bool tile_ok() const;        // the training engine is the tile kernel (tile_shape_ok and not fused_ok)
+	bool tile_infer_ok() const;  // inference runs the tile inference kernel
 	bool layered_ok() const;
 	const char* engine() const { return (fused_ok() || tile_ok()) ? "fused" : layered_ok() ? "layered" : "unsupported"; }
+	const char* inference_engine() const;  // "fused" (one MLP launch) or "layered"
 	void initialize_params(Pcg32& rng, float* host_out, float scale = 1.0f) const;  // network first (nwie.h:124-130)
 
 	// params16: [mlp | encoding] fp16. out16: fp16 [B][padded_output].
 	void inference(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const void* params16, void* out16);
+	// Forward that keeps what the backward needs (the reference's forward context, cpp_api.cu:84-109,
+	// network_with_input_encoding.h:70-81): the encoding, in the layout of the engine the backward will
+	// run (with_dinput: the caller wants dL/dinput) -- SoA [IN][B] for the register-resident grid kernel,
+	// AoS [B][IN] for the tile kernel -- into keep (grown here). Returns the layout kept (KEEP_*); the
+	// layer-wise engine keeps nothing (its backward recomputes the forward).
+	enum : int { KEEP_NONE = 0, KEEP_FUSED_SOA = 1, KEEP_TILE_AOS = 2 };
+	int backward_engine_keep(bool with_dinput) const;
+	int forward_keep(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const void* params16, void* out16, bool with_dinput,
+	                 DevBuf& keep);
 	// forward+backward; dout16 == nullptr -> RelativeL2 on target, else external dL/dout.
 	// Writes fp32 gradient sums into grad32 ([mlp | encoding]) and the loss partials
 	// (ws.loss_partial[0 .. ws.n_loss_partials)). dL_dinput (optional): fp32 [B][n_input_dims].
+	// kept / kept_layout: a forward_keep encoding of this batch (used when the layout matches the engine).
 	void fwd_bwd(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target, uint32_t dims,
 	             float loss_scale, const void* params16, const void* dout16, void* out16, float* grad32,
-	             const std::function<void(int)>& mark = nullptr, float* dL_dinput = nullptr);
+	             const std::function<void(int)>& mark = nullptr, float* dL_dinput = nullptr, const void* kept = nullptr,
+	             int kept_layout = KEEP_NONE);
 	json hyperparams() const;
 
 	// pieces of the fused engine for the trainer's overlapped step
 	void fused_kernel(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target, uint32_t dims,
-	                  float loss_scale, const void* params16, bool pack, const void* dout16 = nullptr, void* out16 = nullptr);
+	                  float loss_scale, const void* params16, bool pack, const void* dout16 = nullptr, void* out16 = nullptr,
+	                  const void* enc_soa = nullptr);
 	void grid_backward(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, GridBwdEpilogue* ep = nullptr);
 	void pack_weights(hipStream_t st, StepWorkspace& ws, const void* params16);
 
 private:
 	void fwd_bwd_fused(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target, uint32_t dims,
 	                   float loss_scale, const void* params16, const void* dout16, void* out16, float* grad32,
-	                   const std::function<void(int)>& mark);
+	                   const std::function<void(int)>& mark, const void* enc_soa);
 	void fwd_bwd_tile(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target, uint32_t dims,
 	                  float loss_scale, const void* params16, const void* dout16, void* out16, float* grad32,
-	                  const std::function<void(int)>& mark, float* dL_dinput);
+	                  const std::function<void(int)>& mark, float* dL_dinput, const void* enc_aos);
 	void fwd_bwd_layered(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const float* target, uint32_t dims,
 	                     float loss_scale, const void* params16, const void* dout16, void* out16, float* grad32,
 	                     const std::function<void(int)>& mark, float* dL_dinput);

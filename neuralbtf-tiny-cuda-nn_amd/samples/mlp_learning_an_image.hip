@@ -7,14 +7,19 @@
 // runtime where the reference uses CUDA's (stream). CDNA GPUs have no texture-sampling hardware
 // (HIP marks tex2D unavailable for gfx950), so the image lookup is an explicit bilinear fetch with
 // the semantics of the reference's texture (normalized coordinates, clamp addressing, linear filter
-// at texel centres); the reference's hardware filter quantises weights to 8 bits, this one is fp32.
+// at texel centres, and the texture unit's 8-bit fractional weights).
 //
 // Image I/O: the reference reads JPEG/EXR through stb_image and writes JPEGs; this repository has no
-// image codec, so the image is a binary PGM (tests/golden/albert_768x1024.pgm, albert.jpg decoded
-// and downscaled by tools/make_albert_fixture.py), converted to RGBA float with the 2.2 gamma
-// linearisation of stbi_loadf (stbi_wrapper.cpp:37-44), and learned images are written as PPM.
+// image codec, so the image is a binary PGM (the full-resolution albert.jpg as decoded by the
+// reference's stb_image, tests/golden/albert_full.png, tools/make_albert_full.py; or the 768x1024
+// tests/golden/albert_768x1024.pgm), converted to RGBA float with the 2.2 gamma linearisation of
+// stbi_loadf (stbi_wrapper.cpp:37-44), and learned images are written as PPM (the reference: JPEG q100).
 //
 //   mlp_learning_an_image <image.pgm> [config.json] [n_training_steps] [final_image.ppm]
+//
+// Test hooks (not in the reference): TCNN_SAMPLE_SEED replaces the batch RNG's seed 1337 and
+// TCNN_SAMPLE_TRAINER_SEED the Trainer's parameter seed 1337 (tests/test_gpu_render_pin.py measures
+// the seed-to-seed spread of the render PSNR with them).
 #include <tiny-cuda-nn/common_device.h>
 
 #include <tiny-cuda-nn/config.h>
@@ -82,19 +87,22 @@ struct ImageTexture {
 	int width, height;
 };
 
-// tex2D<float4>(texture, u, v) with cudaFilterModeLinear, normalizedCoords, cudaAddressModeClamp
+// tex2D<float4>(texture, u, v) with cudaFilterModeLinear, normalizedCoords, cudaAddressModeClamp:
+// x_B = u * width - 0.5, i = floor(x_B), alpha = frac(x_B), tex = (1-a)(1-b) T[i,j] + a(1-b) T[i+1,j]
+// + (1-a) b T[i,j+1] + a b T[i+1,j+1], alpha and beta held by the texture unit in 9-bit fixed point
+// with 8 fractional bits (CUDA programming guide, "Texture Fetching", linear filtering); the rounding
+// of the fraction to 1/256 is taken as round-to-nearest (the guide does not specify it)
 __device__ inline float4 sample_bilinear(const ImageTexture& t, float u, float v) {
 	const float x = u * t.width - 0.5f, y = v * t.height - 0.5f;
 	const float fx = floorf(x), fy = floorf(y);
-	const float ax = x - fx, ay = y - fy;
+	const float ax = rintf((x - fx) * 256.0f) * (1.0f / 256.0f), ay = rintf((y - fy) * 256.0f) * (1.0f / 256.0f);
 	const int x0 = min(max((int)fx, 0), t.width - 1), x1 = min(max((int)fx + 1, 0), t.width - 1);
 	const int y0 = min(max((int)fy, 0), t.height - 1), y1 = min(max((int)fy + 1, 0), t.height - 1);
 	const float4 a = t.data[y0 * t.width + x0], b = t.data[y0 * t.width + x1];
 	const float4 c = t.data[y1 * t.width + x0], d = t.data[y1 * t.width + x1];
-	auto lerp4 = [](float4 p, float4 q, float w) {
-		return make_float4(p.x + (q.x - p.x) * w, p.y + (q.y - p.y) * w, p.z + (q.z - p.z) * w, p.w + (q.w - p.w) * w);
-	};
-	return lerp4(lerp4(a, b, ax), lerp4(c, d, ax), ay);
+	const float w00 = (1.0f - ax) * (1.0f - ay), w10 = ax * (1.0f - ay), w01 = (1.0f - ax) * ay, w11 = ax * ay;
+	return make_float4(w00 * a.x + w10 * b.x + w01 * c.x + w11 * d.x, w00 * a.y + w10 * b.y + w01 * c.y + w11 * d.y,
+	                   w00 * a.z + w10 * b.z + w01 * c.z + w11 * d.z, w00 * a.w + w10 * b.w + w01 * c.w + w11 * d.w);
 }
 
 template <uint32_t stride>
@@ -120,7 +128,7 @@ int main(int argc, char* argv[]) {
 
 		if (argc < 2) {
 			std::cout << "USAGE: " << argv[0] << " path-to-image.pgm [path-to-optional-config.json] [n_steps] [final.ppm]" << std::endl;
-			std::cout << "The sample image is tests/golden/albert_768x1024.pgm." << std::endl;
+			std::cout << "Sample images: tests/golden/albert_768x1024.pgm, or albert_full.png converted to PGM." << std::endl;
 			return 0;
 		}
 
@@ -180,7 +188,8 @@ int main(int argc, char* argv[]) {
 		HIP_CHECK_THROW(hipStreamCreate(&inference_stream));
 		hipStream_t training_stream = inference_stream;
 
-		default_rng_t rng{1337};
+		const char* seed_env = std::getenv("TCNN_SAMPLE_SEED");  // test hook, see the header
+		default_rng_t rng{seed_env ? (uint64_t)std::strtoull(seed_env, nullptr, 10) : 1337u};
 
 		// Auxiliary matrices for training
 		GPUMatrix<float> training_target(n_output_dims, batch_size);
@@ -200,7 +209,9 @@ int main(int argc, char* argv[]) {
 		std::shared_ptr<NetworkWithInputEncoding<precision_t>> network =
 		    std::make_shared<NetworkWithInputEncoding<precision_t>>(n_input_dims, n_output_dims, encoding_opts, network_opts);
 
-		auto trainer = std::make_shared<Trainer<float, precision_t, precision_t>>(network, optimizer, loss);
+		const char* tseed_env = std::getenv("TCNN_SAMPLE_TRAINER_SEED");  // test hook, see the header
+		auto trainer = std::make_shared<Trainer<float, precision_t, precision_t>>(
+		    network, optimizer, loss, tseed_env ? (uint32_t)std::strtoul(tseed_env, nullptr, 10) : 1337u);
 
 		std::chrono::steady_clock::time_point begin = std::chrono::steady_clock::now();
 

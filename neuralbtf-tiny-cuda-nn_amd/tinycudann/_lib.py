@@ -74,6 +74,9 @@ _SIGS = {
     "tcnn_trainer_hyperparams": (c_char_p, [c_void_p]),
     "tcnn_trainer_initialize_params": (c_int, [c_void_p, c_uint32]),
     "tcnn_trainer_engine": (c_char_p, [c_void_p]),
+    "tcnn_trainer_inference_engine": (c_char_p, [c_void_p]),
+    "tcnn_module_engine": (c_char_p, [c_void_p]),
+    "tcnn_module_inference_engine": (c_char_p, [c_void_p]),
     "tcnn_trainer_profile_begin": (c_int, [c_void_p]),
     "tcnn_trainer_profile_begin_sampled": (c_int, [c_void_p, c_uint32]),
     "tcnn_trainer_serialize": (c_int, [c_void_p, c_int, c_void_p, c_uint64, c_void_p]),

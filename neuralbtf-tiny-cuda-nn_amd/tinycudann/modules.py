@@ -104,6 +104,13 @@ class _NativeModule:
     def name(self):
         return L.lib().tcnn_module_name(self.h).decode()
 
+    def engine(self):
+        """the engine training / backward runs on ("fused", "layered"; "encoding" for encodings)"""
+        return L.lib().tcnn_module_engine(self.h).decode()
+
+    def inference_engine(self):
+        return L.lib().tcnn_module_inference_engine(self.h).decode()
+
     def initial_params(self, seed):
         p = torch.zeros(self.n_params(), dtype=torch.float32, device="cuda")
         torch.cuda.synchronize()

@@ -32,6 +32,10 @@ class Trainer:
     def engine(self):
         return L.lib().tcnn_trainer_engine(self.h).decode()
 
+    @property
+    def inference_engine(self):
+        return L.lib().tcnn_trainer_inference_engine(self.h).decode()
+
     def training_step(self, input, target, run_optimizer=True, stream=None):
         """input: float32 [B, n_in] CUDA, target float32 [B, n_out] CUDA (contiguous)."""
         assert input.is_contiguous() and target.is_contiguous()

@@ -109,6 +109,8 @@ def lib():
                                           ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]
         _lib.orc_hfma.restype = ctypes.c_uint16
         _lib.orc_hfma.argtypes = [ctypes.c_uint16] * 3
+        _lib.orc_set_mimic.argtypes = [ctypes.c_int]
+        _lib.orc_act_bwd_output.argtypes = [ctypes.c_uint32, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
     return _lib
 
 
@@ -366,6 +368,27 @@ def adam_step(cfg, n_matrix, loss_scale, current_step, w32, w16, grad16, m1, m2,
                         _p(w32), _p(w16), _p(grad16), _p(m1), _p(m2), _p(steps))
 
 
+ACTIVATIONS = ["none", "relu", "leakyrelu", "exponential", "sine", "sigmoid", "squareplus", "softplus", "tanh"]
+
+
+def act_code(name):
+    """Activation enum value (common.h:126-136) of a config string (case-insensitive)"""
+    return ACTIVATIONS.index(name.lower())
+
+
+def set_mimic(on):
+    """reference-mimic fp16 accumulation on / off, process-wide"""
+    lib().orc_set_mimic(1 if on else 0)
+
+
+def act_bwd_output(act, out16, g16):
+    """in-place output-activation transfer (act: hidden | output << 8) of fp16 dL/dout given fp16 outputs"""
+    g16 = np.ascontiguousarray(g16, dtype=np.uint16)
+    out16 = np.ascontiguousarray(out16, dtype=np.uint16)
+    lib().orc_act_bwd_output(act, ctypes.c_size_t(g16.size), _p(out16), _p(g16))
+    return g16
+
+
 class OracleModel:
     """Trainer<float,__half,__half> over NetworkWithInputEncoding<Grid | OneBlob | Identity,
     FullyFusedMLP> on the CPU (encoding padded to 16 columns, network.cu:76-95)."""
@@ -391,8 +414,7 @@ class OracleModel:
         self.m.NH = int(net.get("n_hidden_layers", 5))
         self.m.n_output_dims = n_output_dims
         self.m.OUTP = (n_output_dims + 15) // 16 * 16
-        act = net.get("activation", "ReLU").lower()
-        self.m.activation = {"none": 0, "relu": 1}[act]
+        self.m.activation = act_code(net.get("activation", "ReLU")) | (act_code(net.get("output_activation", "None")) << 8)
         self.m.adam = adam_cfg(opt)
         lo = config.get("loss", {}).get("otype", "RelativeL2").lower()
         self.m.loss_type = {"relativel2": 0, "l2": 1}[lo]

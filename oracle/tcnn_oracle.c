@@ -355,7 +355,24 @@ void orc_grid_fwd(const orc_grid* g, uint32_t B, const float* pos_in, const uint
 /* kernel_grid_backward, grid.h:214-320, ideal precision (fp32 sums of exact products). */
 /* ADD: one update of grid parameter (level base + p): the gradient sum, or (stats mode) the sum of
  * |update| and the number of updates per parameter -- the per-element tolerance of the GPU tests */
-#define ADD(p, v) do { const float v_ = (v); if (grad) grad[base + (p)] += v_; \
+/* Reference-mimic mode: the reference accumulates in fp16 -- WMMA fragments
+ * with __half accumulators in the fused MLP kernels (fully_fused_mlp.cu:68,198: one fp16 rounding of
+ * the running sum per 16-deep K step), CUTLASS GEMMs with half_t accumulators (cutlass_matmul.h:67-68,
+ * mma 16x8x8: one rounding per 8-deep K step; split-K slices of min(4096, B) samples whose partials
+ * are reduced in half, fully_fused_mlp.cu:775), and the grid gradient through fp16 atomics into the
+ * __half gradient buffer (grid.h:252-255,655-666). With the mode on the oracle rounds at those points
+ * (the atomics in point order); off (default) it is the "ideal" fp32-accumulating restatement the GPU
+ * engine is checked against. Used to size the gap between this engine and the reference's binary
+ * (tests/golden/oracle_render.json). */
+static int g_mimic = 0;
+void orc_set_mimic(int on) { g_mimic = on; }
+static inline float hround(float x) { return orc_h2f(orc_f2h(x)); }
+/* fp16 running sum update after k products (chunked), see g_mimic */
+#define MIMIC_STEP(acc, part, k, chunk, K) \
+	do { if (g_mimic && (((k) + 1) % (chunk) == 0 || (k) + 1 == (K))) { (acc) = hround((acc) + (part)); (part) = 0.0f; } } while (0)
+
+#define ADD(p, v) do { const float v_ = (v); if (grad) { if (g_mimic) grad[base + (p)] = hround(grad[base + (p)] + hround(v_)); \
+	else grad[base + (p)] += v_; } \
 	if (abssum) { abssum[base + (p)] += fabsf(v_); count[base + (p)] += 1; } } while (0)
 static void grid_bwd_impl(const orc_grid* g, uint32_t B, const float* pos_in, const uint16_t* dL_dy, float* grad, float* abssum,
                           uint32_t* count) {
@@ -604,9 +621,49 @@ uint32_t orc_mlp_n_params(uint32_t W, uint32_t IN, uint32_t NH, uint32_t OUTP) {
 	return W * IN + (NH - 1) * W * W + OUTP * W;
 }
 
-static inline float act_fwd(uint32_t act, float x) { return act == 1 ? (x > 0.0f ? x : 0.0f) : x; }
-/* ReLU transfer from the post-activation value (common_device.h:240-297) */
-static inline int act_pass(uint32_t act, float y) { return act == 1 ? (y > 0.0f) : 1; }
+/* Activations (common_device.h:102-160, warp_activation; fp32 math on the fp32 accumulator, rounded
+ * to fp16 by the caller). The activation argument of the MLP functions carries the hidden activation
+ * in bits 0-7 and the output activation in bits 8-15 (Activation enum order, common.h:126-136:
+ * None, ReLU, LeakyReLU, Exponential, Sine, Sigmoid, Squareplus, Softplus, Tanh). */
+#define ORC_K_ACT 10.0f
+static inline float act_fwd(uint32_t act, float x) {
+	switch (act & 0xffu) {
+		case 1: return x > 0.0f ? x : 0.0f;
+		case 2: return x * (x > 0.0f ? 1.0f : 0.01f);
+		case 3: return expf(x);
+		case 4: return sinf(x);
+		case 5: return 1.0f / (1.0f + expf(-x));
+		case 6: { const float y = x * ORC_K_ACT; return 0.5f * (y + sqrtf(y * y + 4.0f)) / ORC_K_ACT; }
+		case 7: return logf(expf(x * ORC_K_ACT) + 1.0f) / ORC_K_ACT;
+		case 8: return tanhf(x);
+		default: return x;
+	}
+}
+/* Transfer given the post-activation value y (warp_activation_backward, common_device.h:240-297):
+ * g * (T)factor(y) in fp16 -- both operands fp16, the product rounded once (exact in fp32 first).
+ * ReLU / None pass the fp16 value of g unchanged or 0. Sine has no post-activation backward. */
+static inline float act_bwd(uint32_t act, float g, float y) {
+	const float gh = orc_h2f(orc_f2h(g));
+	float f;
+	switch (act & 0xffu) {
+		case 0: return gh;
+		case 1: return y > 0.0f ? gh : 0.0f;
+		case 2: f = y > 0.0f ? 1.0f : 0.01f; break;
+		case 3: f = y; break;
+		case 5: f = y * orc_h2f(orc_f2h(1.0f - y)); break;
+		case 6: { const float t = y * ORC_K_ACT; f = t * t / (t * t + 1.0f); break; }
+		case 7: f = 1.0f - expf(-y * ORC_K_ACT); break;
+		case 8: f = 1.0f - y * y; break;
+		default: return gh;
+	}
+	return orc_h2f(orc_f2h(gh * orc_h2f(orc_f2h(f))));
+}
+
+void orc_act_bwd_output(uint32_t act, size_t n, const uint16_t* out16, uint16_t* g16) {
+	const uint32_t a = (act >> 8) & 0xffu;
+	if (a == 0) return;
+	for (size_t i = 0; i < n; ++i) g16[i] = orc_f2h(act_bwd(a, orc_h2f(g16[i]), orc_h2f(out16[i])));
+}
 
 typedef struct {
 	uint32_t W, IN, NH, OUTP;
@@ -634,8 +691,9 @@ static void mlp_fwd_sample(const mlp_view* v, uint32_t act, const float* x, floa
 	const uint32_t W = v->W, IN = v->IN, NH = v->NH, OUTP = v->OUTP;
 	const float* W0 = v->wf + v->off[0];
 	for (uint32_t n = 0; n < W; ++n) {
-		float acc = 0.0f;
-		for (uint32_t k = 0; k < IN; ++k) acc += W0[(size_t)n * IN + k] * x[k];
+		float acc = 0.0f, part = 0.0f;
+		for (uint32_t k = 0; k < IN; ++k) { part += W0[(size_t)n * IN + k] * x[k]; MIMIC_STEP(acc, part, k, 16, IN); }
+		if (!g_mimic) acc = part;
 		h[n] = orc_h2f(orc_f2h(act_fwd(act, acc)));
 	}
 	for (uint32_t l = 1; l < NH; ++l) {
@@ -643,17 +701,19 @@ static void mlp_fwd_sample(const mlp_view* v, uint32_t act, const float* x, floa
 		const float* hp = h + (size_t)(l - 1) * W;
 		float* hn = h + (size_t)l * W;
 		for (uint32_t n = 0; n < W; ++n) {
-			float acc = 0.0f;
-			for (uint32_t k = 0; k < W; ++k) acc += Wl[(size_t)n * W + k] * hp[k];
+			float acc = 0.0f, part = 0.0f;
+			for (uint32_t k = 0; k < W; ++k) { part += Wl[(size_t)n * W + k] * hp[k]; MIMIC_STEP(acc, part, k, 16, W); }
+			if (!g_mimic) acc = part;
 			hn[n] = orc_h2f(orc_f2h(act_fwd(act, acc)));
 		}
 	}
 	const float* Wo = v->wf + v->off[NH];
 	const float* hl = h + (size_t)(NH - 1) * W;
 	for (uint32_t o = 0; o < OUTP; ++o) {
-		float acc = 0.0f;
-		for (uint32_t k = 0; k < W; ++k) acc += Wo[(size_t)o * W + k] * hl[k];
-		out[o] = orc_f2h(acc); /* output activation None */
+		float acc = 0.0f, part = 0.0f;
+		for (uint32_t k = 0; k < W; ++k) { part += Wo[(size_t)o * W + k] * hl[k]; MIMIC_STEP(acc, part, k, 16, W); }
+		if (!g_mimic) acc = part;
+		out[o] = orc_f2h(act_fwd(act >> 8, acc));  /* output activation (last_layer_forward) */
 	}
 }
 
@@ -689,52 +749,63 @@ void orc_mlp_fwd(uint32_t W, uint32_t IN, uint32_t NH, uint32_t OUTP, uint32_t a
 /* backward of one sample: g fp16 dL/dout (OUTP), h hidden (NH*W). Accumulates wgrad (fp32),
  * writes dx (fp16 rounded, IN) if dx != NULL. delta scratch: 2*W floats. */
 static void mlp_bwd_sample(const mlp_view* v, uint32_t act, const float* x, const float* h, const float* g,
-                           float* wgrad, float* dx, float* scratch) {
+                           float* wgrad, float* dx, float* scratch, float* deltas) {
 	const uint32_t W = v->W, IN = v->IN, NH = v->NH, OUTP = v->OUTP;
 	float* d_cur = scratch;      /* delta of layer being processed (fp16-rounded) */
 	float* d_nxt = scratch + W;
 	/* output layer: dWout[o][k] += g[o] * h_last[k]; delta_H = act'(h_H) * Wout^T g */
 	const float* Wo = v->wf + v->off[NH];
 	const float* hl = h + (size_t)(NH - 1) * W;
-	float* gWo = wgrad + v->off[NH];
-	for (uint32_t o = 0; o < OUTP; ++o) {
-		if (g[o] == 0.0f) continue;
-		for (uint32_t k = 0; k < W; ++k) gWo[(size_t)o * W + k] += g[o] * hl[k];
+	if (wgrad) {
+		float* gWo = wgrad + v->off[NH];
+		for (uint32_t o = 0; o < OUTP; ++o) {
+			if (g[o] == 0.0f) continue;
+			for (uint32_t k = 0; k < W; ++k) gWo[(size_t)o * W + k] += g[o] * hl[k];
+		}
 	}
 	for (uint32_t k = 0; k < W; ++k) {
-		float acc = 0.0f;
-		for (uint32_t o = 0; o < OUTP; ++o) acc += Wo[(size_t)o * W + k] * g[o];
-		d_cur[k] = act_pass(act, hl[k]) ? orc_h2f(orc_f2h(acc)) : 0.0f;
+		float acc = 0.0f, part = 0.0f;
+		for (uint32_t o = 0; o < OUTP; ++o) { part += Wo[(size_t)o * W + k] * g[o]; MIMIC_STEP(acc, part, o, 16, OUTP); }
+		if (!g_mimic) acc = part;
+		d_cur[k] = act_bwd(act, acc, hl[k]);
 	}
+	if (deltas) memcpy(deltas + (size_t)(NH - 1) * W, d_cur, sizeof(float) * W);
 	/* hidden layers, from the last to the first hidden matmul */
 	for (uint32_t l = NH - 1; l >= 1; --l) {
 		const float* Wl = v->wf + v->off[l];
 		const float* hin = h + (size_t)(l - 1) * W;
-		float* gWl = wgrad + v->off[l];
-		for (uint32_t n = 0; n < W; ++n) {
-			float dn = d_cur[n];
-			if (dn == 0.0f) continue;
-			for (uint32_t k = 0; k < W; ++k) gWl[(size_t)n * W + k] += dn * hin[k];
+		if (wgrad) {
+			float* gWl = wgrad + v->off[l];
+			for (uint32_t n = 0; n < W; ++n) {
+				float dn = d_cur[n];
+				if (dn == 0.0f) continue;
+				for (uint32_t k = 0; k < W; ++k) gWl[(size_t)n * W + k] += dn * hin[k];
+			}
 		}
 		for (uint32_t k = 0; k < W; ++k) {
-			float acc = 0.0f;
-			for (uint32_t n = 0; n < W; ++n) acc += Wl[(size_t)n * W + k] * d_cur[n];
-			d_nxt[k] = act_pass(act, hin[k]) ? orc_h2f(orc_f2h(acc)) : 0.0f;
+			float acc = 0.0f, part = 0.0f;
+			for (uint32_t n = 0; n < W; ++n) { part += Wl[(size_t)n * W + k] * d_cur[n]; MIMIC_STEP(acc, part, n, 16, W); }
+			if (!g_mimic) acc = part;
+			d_nxt[k] = act_bwd(act, acc, hin[k]);
 		}
 		float* t = d_cur; d_cur = d_nxt; d_nxt = t;
+		if (deltas) memcpy(deltas + (size_t)(l - 1) * W, d_cur, sizeof(float) * W);
 	}
 	/* first layer: dW0[n][k] += delta_1[n] * x[k]; dx = W0^T delta_1 */
 	const float* W0 = v->wf + v->off[0];
-	float* gW0 = wgrad + v->off[0];
-	for (uint32_t n = 0; n < W; ++n) {
-		float dn = d_cur[n];
-		if (dn == 0.0f) continue;
-		for (uint32_t k = 0; k < IN; ++k) gW0[(size_t)n * IN + k] += dn * x[k];
+	if (wgrad) {
+		float* gW0 = wgrad + v->off[0];
+		for (uint32_t n = 0; n < W; ++n) {
+			float dn = d_cur[n];
+			if (dn == 0.0f) continue;
+			for (uint32_t k = 0; k < IN; ++k) gW0[(size_t)n * IN + k] += dn * x[k];
+		}
 	}
 	if (dx) {
 		for (uint32_t k = 0; k < IN; ++k) {
-			float acc = 0.0f;
-			for (uint32_t n = 0; n < W; ++n) acc += W0[(size_t)n * IN + k] * d_cur[n];
+			float acc = 0.0f, part = 0.0f;
+			for (uint32_t n = 0; n < W; ++n) { part += W0[(size_t)n * IN + k] * d_cur[n]; MIMIC_STEP(acc, part, n, 8, W); }
+			if (!g_mimic) acc = part;
 			dx[k] = orc_h2f(orc_f2h(acc));
 		}
 	}
@@ -749,6 +820,7 @@ void orc_mlp_bwd(uint32_t W, uint32_t IN, uint32_t NH, uint32_t OUTP, uint32_t a
 	size_t np = orc_mlp_n_params(W, IN, NH, OUTP);
 	if (n_threads <= 0) n_threads = 1;
 	float* partial = (float*)calloc((size_t)n_threads * np, sizeof(float));
+	float* deltas = g_mimic ? (float*)malloc(sizeof(float) * (size_t)B * NH * W) : NULL;  /* [B][NH][W] */
 #ifdef _OPENMP
 #pragma omp parallel num_threads(n_threads)
 #endif
@@ -772,7 +844,8 @@ void orc_mlp_bwd(uint32_t W, uint32_t IN, uint32_t NH, uint32_t OUTP, uint32_t a
 			for (uint32_t l = 0; l < NH; ++l)
 				for (uint32_t n = 0; n < W; ++n) h[(size_t)l * W + n] = orc_h2f(hidden[(size_t)l * W * B + (size_t)i * W + n]);
 			for (uint32_t o = 0; o < OUTP; ++o) g[o] = orc_h2f(dL_dout[(size_t)i * OUTP + o]);
-			mlp_bwd_sample(&v, act, x, h, g, wg, dL_dinput ? dx : NULL, scratch);
+			mlp_bwd_sample(&v, act, x, h, g, g_mimic ? NULL : wg, dL_dinput ? dx : NULL, scratch,
+			               g_mimic ? deltas + (size_t)i * NH * W : NULL);
 			if (dL_dinput) {
 				for (uint32_t k = 0; k < IN; ++k) {
 					uint16_t hv = orc_f2h(dx[k]);
@@ -782,10 +855,42 @@ void orc_mlp_bwd(uint32_t W, uint32_t IN, uint32_t NH, uint32_t OUTP, uint32_t a
 		}
 		free(x); free(h); free(g); free(dx); free(scratch);
 	}
-	for (size_t p = 0; p < np; ++p) {
-		float s = 0.0f;
-		for (int t = 0; t < n_threads; ++t) s += partial[(size_t)t * np + p];
-		wgrad[p] = s;
+	if (g_mimic) {
+		/* CUTLASS split-K weight gradients (fully_fused_mlp.cu:775-829): slices of min(4096, B)
+		 * samples, each accumulated in fp16 per 8-sample mma step, slice partials summed in fp16 */
+		const uint32_t slice = B < 4096 ? B : 4096;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 16) num_threads(n_threads)
+#endif
+		for (int64_t pp = 0; pp < (int64_t)np; ++pp) {
+			const size_t p = (size_t)pp;
+			uint32_t m, r, c, K;  /* matrix m (0 = W0, 1..NH-1 hidden, NH = Wout), row r, column c */
+			if (p < v.off[1 < NH ? 1 : NH]) { m = 0; K = IN; }
+			else if (p >= v.off[NH]) { m = NH; K = W; }
+			else { m = 1 + (uint32_t)((p - v.off[1]) / ((size_t)W * W)); K = W; }
+			r = (uint32_t)((p - v.off[m]) / K);
+			c = (uint32_t)((p - v.off[m]) % K);
+			float tot = 0.0f;
+			for (uint32_t s0 = 0; s0 < B; s0 += slice) {
+				float acc = 0.0f, part = 0.0f;
+				for (uint32_t i = s0; i < s0 + slice && i < B; ++i) {
+					const float dy = m == NH ? orc_h2f(dL_dout[(size_t)i * OUTP + r]) : deltas[((size_t)i * NH + m) * W + r];
+					const float xv = m == 0 ? in_at(input, input_soa, IN, B, i, c)
+					                        : orc_h2f(hidden[(size_t)(m - 1) * W * B + (size_t)i * W + c]);
+					part += dy * xv;
+					MIMIC_STEP(acc, part, i - s0, 8, slice);
+				}
+				tot = hround(tot + acc);
+			}
+			wgrad[p] = tot;
+		}
+		free(deltas);
+	} else {
+		for (size_t p = 0; p < np; ++p) {
+			float s = 0.0f;
+			for (int t = 0; t < n_threads; ++t) s += partial[(size_t)t * np + p];
+			wgrad[p] = s;
+		}
 	}
 	free(partial);
 	free(v.wf);
@@ -1037,6 +1142,8 @@ double orc_train_step(orc_model* m, uint32_t B, const float* pos, const float* t
 	orc_mlp_fwd(m->W, IN, m->NH, m->OUTP, m->activation, m->w16, B, enc, soa, out, hidden, n_threads);
 	double loss = m->loss_type == 1 ? orc_l2(B, m->OUTP, m->n_output_dims, loss_scale, out, target, NULL, dout)
 	                                : orc_relative_l2(B, m->OUTP, m->n_output_dims, loss_scale, out, target, NULL, dout);
+	/* output-activation transfer of dL/dout (fully_fused_mlp.cu:759-762, activation_backward_output_gpu) */
+	orc_act_bwd_output(m->activation, (size_t)m->OUTP * B, out, dout);
 	orc_mlp_bwd(m->W, IN, m->NH, m->OUTP, m->activation, m->w16, B, enc, soa, hidden, dout, m->grad32,
 	            m->enc_type == 0 ? denc : NULL, n_threads);
 	if (m->enc_type == 0) {

@@ -97,8 +97,15 @@ void orc_grid_bwd_bwd(const orc_grid* g, uint32_t B, const float* pos, const uin
  * params fp16: W0 [W x IN] RM, W_1..W_{NH-1} [W x W] RM, Wout [OUTP x W] RM (contiguous).
  * input fp16: SoA [IN][B] (in[k*B+i], the grid's RM layout) if input_soa else CM (in[i*IN+k]).
  * out fp16 CM [OUTP][B] (out[i*OUTP+o]); hidden fp16 NH x CM [W][B] (post-activation) or NULL.
- * activation: 0 = None, 1 = ReLU (common_device.h:102-160); output activation None. */
+ * activation: hidden activation in bits 0-7, output activation in bits 8-15, Activation enum order
+ * (common.h:126-136: None, ReLU, LeakyReLU, Exponential, Sine, Sigmoid, Squareplus, Softplus, Tanh;
+ * common_device.h:102-297). orc_mlp_bwd's dL_dout is AFTER the output-activation transfer
+ * (orc_act_bwd_output). */
 uint32_t orc_mlp_n_params(uint32_t W, uint32_t IN, uint32_t NH, uint32_t OUTP);
+/* reference-mimic fp16 accumulation on (1) / off (0, default): see g_mimic in tcnn_oracle.c */
+void orc_set_mimic(int on);
+/* in-place output-activation transfer of dL/dout given the network output (bits 8-15 of act) */
+void orc_act_bwd_output(uint32_t act, size_t n, const uint16_t* out16, uint16_t* g16);
 void orc_mlp_fwd(uint32_t W, uint32_t IN, uint32_t NH, uint32_t OUTP, uint32_t activation,
                  const uint16_t* params, uint32_t B, const uint16_t* input, int input_soa,
                  uint16_t* out, uint16_t* hidden, int n_threads);

@@ -1,9 +1,10 @@
 """GPU parity of the layer-wise MFMA engine (mlp_layers.hip) and the OneBlob / Identity encodings
 (encodings.hip) against the CPU oracle, on the BASELINE configs the register-resident fused kernel
 does not take: config_oneblob.json as-is (OneBlob 64 bins + FullyFusedMLP W128/H5), its W64/H2
-variant, HashGrid + W128/H4 (the LDS-pressure config), CutlassMLP, Identity. FullyFusedMLP W64/W128
-shapes train on the tile engine (mlp_tile.hip, engine "fused"), including those whose weights exceed
-the LDS (hidden matrices streamed from L2); the layer-wise engine is also checked on two of them.
+variant, HashGrid + W128/H4 (the LDS-pressure config), CutlassMLP, Identity. FullyFusedMLP W16-W128
+shapes train on the tile engine (mlp_tile.h, engine "fused"), including those whose weights exceed
+the LDS (hidden matrices streamed from L2); the layer-wise engine is also checked on two of them
+(tests/test_gpu_tile_engine.py covers W16 / W32, activations and fused inference).
 
 Tolerances (north_star: 1e-3 relative, fp16):
   * OneBlob / Identity encodings: bit-exact (same fp32 op sequence, explicit FMAs)
@@ -63,7 +64,7 @@ CONFIGS = {
 }
 # FullyFusedMLP configurations the tile engine trains (engine "fused"); the rest run layer by layer
 TILE = {"oneblob_w64_h2", "oneblob16_w64_h2", "hashgrid_w128_h4", "identity_w64_h3", "oneblob_w64_h5", "hashgrid_w128_h2",
-        "oneblob_as_file_w128_h5", "oneblob_w128_h4", "hashgrid_w128_h5"}
+        "oneblob_as_file_w128_h5", "oneblob_w128_h4", "hashgrid_w128_h5", "identity_w32_h3"}
 # the same shapes with the tile engine switched off run on the layer-wise engine
 LAYERED_AB = ["oneblob_as_file_w128_h5", "hashgrid_w128_h4"]
 

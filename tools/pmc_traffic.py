@@ -4,7 +4,9 @@ Correction (/opt/skills/guides/MI355X_MICROARCH.md, HBM section): on gfx950 FETC
 the bytes of wide (16 B/lane) coalesced streaming reads, so reads are doubled; WRITE_SIZE is exact
 for 16 B/lane streaming stores. Both counters are in KiB per dispatch; Infinity-Cache hits are
 counted as fabric requests. Gathers (4 B/lane) are uncalibrated -- the doubled figure is reported
-as an upper bound. Usage: python tools/pmc_traffic.py gpurun_out/pmc_run out.json
+as an upper bound. Usage: python tools/pmc_traffic.py gpurun_out/pmc_run out.json [workload tag]
+The workload tag (bench.py --print-workload with the same arguments as the profiled bench) keys the
+file for bench.py's roofline.traffic lookup.
 """
 import csv
 import collections
@@ -13,7 +15,9 @@ import json
 import os
 import sys
 
-KERNELS = {"k_fused_train_grid": "k_fused_train_grid", "k_grid_bwd_lds": "k_grid_bwd_lds", "k_adam": "k_adam"}
+KERNELS = {"k_fused_train_grid": "k_fused_train_grid", "k_grid_bwd_lds": "k_grid_bwd_lds", "k_adam": "k_adam",
+           "k_mlp_tile_train": "k_mlp_tile_train", "k_mlp_tile_infer": "k_mlp_tile_infer", "k_grid_fwd": "k_grid_fwd",
+           "k_grid_bin": "k_grid_bin", "k_grid_acc": "k_grid_acc"}
 
 
 def load(run_dir):
@@ -40,8 +44,10 @@ def main():
         for c in ("TCC_HIT_sum", "TCC_MISS_sum"):
             if c in d:
                 res[k][c] = sum(d[c]) / len(d[c])
-    json.dump({"correction": "reads x2 (gfx950 FETCH_SIZE = half of 16B-streaming bytes), writes as counted",
-               "kernels": res}, open(out, "w"), indent=1)
+    doc = {"correction": "reads x2 (gfx950 FETCH_SIZE = half of 16B-streaming bytes), writes as counted", "kernels": res}
+    if len(sys.argv) > 3:
+        doc["workload"] = sys.argv[3]
+    json.dump(doc, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
 
