@@ -127,6 +127,11 @@ struct ModuleNWIE : ModuleBase {
 		check_batch(n);
 		auto c = std::make_unique<NwieCtx>();
 		c->pool = pool;
+		if (std::getenv("TCNN_NO_FORWARD_KEEP")) {  // A/B switch (read per call): the backward recomputes the forward
+			model.inference(st, ws, n, in, params, out);
+			c->layout = NetworkHost::KEEP_NONE;
+			return c;
+		}
 		c->keep = pool->get();
 		c->layout = model.forward_keep(st, ws, n, in, params, out, prep, *c->keep);
 		c->in = in;

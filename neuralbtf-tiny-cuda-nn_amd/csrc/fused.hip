@@ -94,9 +94,9 @@ static void launch_fused_e(hipStream_t st, const FusedTrainArgs& args, uint32_t 
 template <int W, int IN, int NH, uint32_t D, HashType H, Act A>
 static void launch_fused_t(hipStream_t st, const FusedTrainArgs& args, uint32_t n_blocks) {
 	if (args.enc) {
-		// the encoding comes from memory: one instantiation serves every D / hash (Module backward)
-		TCNN_CHECK(args.dout, "fused train: a kept encoding is used with an external dL/d(output) only");
-		launch_fused_e<W, IN, NH, 2, HashType::CoherentPrime, A, true, true>(st, args, n_blocks);
+		// the encoding comes from memory: one instantiation serves every D / hash
+		if (args.dout) launch_fused_e<W, IN, NH, 2, HashType::CoherentPrime, A, true, true>(st, args, n_blocks);
+		else launch_fused_e<W, IN, NH, 2, HashType::CoherentPrime, A, false, true>(st, args, n_blocks);
 	} else if (args.dout) {
 		launch_fused_e<W, IN, NH, D, H, A, true>(st, args, n_blocks);
 	} else {

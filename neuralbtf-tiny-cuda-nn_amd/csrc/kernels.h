@@ -138,7 +138,7 @@ void launch_fused_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, ui
                         const float* pos, const float* target, void* out16, void* dLdenc_pairs,
                         float* wgrad_partial, float* loss_partial, const LevelInfo* levels, bool hash_grid,
                         Interp interp, uint32_t n_blocks, const void* dout16, const void* wimage, uint32_t loss_l2 = 0, bool inrange_index = false,
-                        const void* enc16 = nullptr);  // enc16: the forward's encoding, SoA [IN][B] (with dout16 only)
+                        const void* enc16 = nullptr);  // enc16: the encoding read from memory, SoA [IN][B] (no gathers)
 // LDS weight image of the fused kernels, built once per parameter update.
 size_t fused_weight_image_bytes(uint32_t W, uint32_t IN, uint32_t NH);
 void launch_pack_weights(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, const void* params16, void* image);

@@ -148,6 +148,31 @@ __device__ __forceinline__ h8 lds_wtfrag16(const _Float16* M, int rs, int col0, 
 
 __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+// Per-wave staging buffers [32 samples][64 halves] of the fused kernel's backward (activations, deltas,
+// dL/dy), with the 8-byte chunks of every row XOR-swizzled: chunk ch of row r lives at chunk
+// ch ^ stg_g(r), stg_g = the row's bits (r3 r1 r2 r0). Against the MI355X bank rules (64 banks for
+// ds_read_b64 / _tr_b16 in 32-lane halves, 32 banks for ds_write_b64 in 16-lane groups) every access
+// of the slice is then conflict-free: the h4 stores (16 rows, one chunk per 16-lane group), the
+// transposed reads (rows 8q + 0..3 and + 4, chunks 4t + 0..3) and the row reads (16 rows, chunks
+// 8s + q and + 4). The unswizzled [32][W + 8] rows were 2-way on the stores and transposed reads
+// (r02: SQ_LDS_BANK_CONFLICT 4.57 M cycles per launch).
+__device__ __forceinline__ int stg_g(int r) { return (((r >> 3) & 1) << 3) | (((r >> 1) & 1) << 2) | (((r >> 2) & 1) << 1) | (r & 1); }
+__device__ __forceinline__ int stg_off(int r, int ch) { return r * 64 + ((ch ^ stg_g(r)) << 2); }
+// store 4 consecutive features col .. col+3 (col % 4 == 0) of sample row r
+__device__ __forceinline__ void stg_put(_Float16* S, int r, int col, h4 v) { *(h4*)(S + stg_off(r, col >> 2)) = v; }
+// lds_afrag on a staging buffer: S[r][col0 .. +3] and S[r][col0 + 16 .. +19]
+__device__ __forceinline__ h8 stg_afrag(const _Float16* S, int r, int col0) {
+	return cat8(*(const h4*)(S + stg_off(r, col0 >> 2)), *(const h4*)(S + stg_off(r, (col0 >> 2) + 4)));
+}
+// lds_trfrag on a staging buffer: lane (c, q) receives S[8q + e][16 tile + c], e = 0..7
+__device__ __forceinline__ h8 stg_trfrag(const _Float16* S, int q, int c, int tile) {
+	typedef __attribute__((address_space(3))) s4 lds_s4;
+	const int r = 8 * q + (c >> 2), ch = 4 * tile + (c & 3);
+	const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(S + stg_off(r, ch)));
+	const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(S + stg_off(r + 4, ch)));
+	return cat8(__builtin_bit_cast(h4, lo), __builtin_bit_cast(h4, hi));
+}
+
 
 template <int W, int IN, int NH>
 struct FusedLayout {
@@ -155,7 +180,8 @@ struct FusedLayout {
 	static constexpr int NT = W / 16, KW = W / 32, NTI = IN / 16, KI = IN / 32;
 	static constexpr int NHM = NH - 1;  // hidden WxW matrices
 	static constexpr int RSI = IN + 8, RSW = W + 8;
-	static constexpr int RSS = (W > IN ? W : IN) + 8;
+	static_assert(W <= 64 && IN <= 64, "fused MLP: staging rows hold 64 halves");
+	static constexpr int RSS = 64;  // staging row: 16 XOR-swizzled 8-byte chunks (stg_off)
 	// weight image (row-major, padded rows): W0 [W][RSI] | Wh [NHM][W][RSW] | Wo [16][RSW]
 	static constexpr int oW0 = 0;
 	static constexpr int oWh = oW0 + W * RSI;
@@ -375,15 +401,15 @@ __device__ __forceinline__ void fused_slice(const FusedTrainArgs& a, uint32_t ba
 	// output layer: dWout += G * act[NH-1]^T
 #pragma unroll
 	for (int tau = 0; tau < 2; ++tau) {
-		*(h4*)(bufD + (16 * tau + c) * L::RSS + 4 * q) = G[tau];
+		stg_put(bufD, 16 * tau + c, 4 * q, G[tau]);
 #pragma unroll
-		for (int t = 0; t < NT; ++t) *(h4*)(bufA + (16 * tau + c) * L::RSS + 16 * t + 4 * q) = act[NH - 1][tau][t];
+		for (int t = 0; t < NT; ++t) stg_put(bufA, 16 * tau + c, 16 * t + 4 * q, act[NH - 1][tau][t]);
 	}
 	lds_fence();
 	{
-		const h8 ga = lds_trfrag(bufD, L::RSS, q, c, 0);
+		const h8 ga = stg_trfrag(bufD, q, c, 0);
 #pragma unroll
-		for (int nt = 0; nt < NT; ++nt) acc.Wo[nt] = mfma16(ga, lds_trfrag(bufA, L::RSS, q, c, nt), acc.Wo[nt]);
+		for (int nt = 0; nt < NT; ++nt) acc.Wo[nt] = mfma16(ga, stg_trfrag(bufA, q, c, nt), acc.Wo[nt]);
 	}
 	h4 dl[2][NT];
 #pragma unroll
@@ -399,18 +425,18 @@ __device__ __forceinline__ void fused_slice(const FusedTrainArgs& a, uint32_t ba
 		for (int tau = 0; tau < 2; ++tau) {
 #pragma unroll
 			for (int t = 0; t < NT; ++t) {
-				*(h4*)(bufD + (16 * tau + c) * L::RSS + 16 * t + 4 * q) = dl[tau][t];
-				*(h4*)(bufA + (16 * tau + c) * L::RSS + 16 * t + 4 * q) = act[j - 1][tau][t];
+				stg_put(bufD, 16 * tau + c, 16 * t + 4 * q, dl[tau][t]);
+				stg_put(bufA, 16 * tau + c, 16 * t + 4 * q, act[j - 1][tau][t]);
 			}
 		}
 		lds_fence();
 		{
 			h8 bf[NT];
 #pragma unroll
-			for (int nt = 0; nt < NT; ++nt) bf[nt] = lds_trfrag(bufA, L::RSS, q, c, nt);
+			for (int nt = 0; nt < NT; ++nt) bf[nt] = stg_trfrag(bufA, q, c, nt);
 #pragma unroll
 			for (int mt = 0; mt < NT; ++mt) {
-				const h8 ad = lds_trfrag(bufD, L::RSS, q, c, mt);
+				const h8 ad = stg_trfrag(bufD, q, c, mt);
 #pragma unroll
 				for (int nt = 0; nt < NT; ++nt) acc.H[j - 1][mt][nt] = mfma16(ad, bf[nt], acc.H[j - 1][mt][nt]);
 			}
@@ -423,8 +449,8 @@ __device__ __forceinline__ void fused_slice(const FusedTrainArgs& a, uint32_t ba
 #pragma unroll
 			for (int s = 0; s < KW; ++s) {
 				const h8 af = lds_wtfrag(Wm, L::RSW, 32 * s, 16 * t, q, c);
-				acc0 = mfma16(af, lds_afrag(bufD, L::RSS, c, 32 * s + 4 * q), acc0);
-				acc1 = mfma16(af, lds_afrag(bufD, L::RSS, 16 + c, 32 * s + 4 * q), acc1);
+				acc0 = mfma16(af, stg_afrag(bufD, c, 32 * s + 4 * q), acc0);
+				acc1 = mfma16(af, stg_afrag(bufD, 16 + c, 32 * s + 4 * q), acc1);
 			}
 			dl[0][t] = act_bwd<ACT>(act[j - 1][0][t], acc0);
 			dl[1][t] = act_bwd<ACT>(act[j - 1][1][t], acc1);
@@ -436,18 +462,18 @@ __device__ __forceinline__ void fused_slice(const FusedTrainArgs& a, uint32_t ba
 #pragma unroll
 	for (int tau = 0; tau < 2; ++tau) {
 #pragma unroll
-		for (int t = 0; t < NT; ++t) *(h4*)(bufD + (16 * tau + c) * L::RSS + 16 * t + 4 * q) = dl[tau][t];
+		for (int t = 0; t < NT; ++t) stg_put(bufD, 16 * tau + c, 16 * t + 4 * q, dl[tau][t]);
 #pragma unroll
-		for (int u = 0; u < NTI; ++u) *(h4*)(bufA + (16 * tau + c) * L::RSS + 16 * u + 4 * q) = xt[tau][u];
+		for (int u = 0; u < NTI; ++u) stg_put(bufA, 16 * tau + c, 16 * u + 4 * q, xt[tau][u]);
 	}
 	lds_fence();
 	{
 		h8 bf[NTI];
 #pragma unroll
-		for (int u = 0; u < NTI; ++u) bf[u] = lds_trfrag(bufA, L::RSS, q, c, u);
+		for (int u = 0; u < NTI; ++u) bf[u] = stg_trfrag(bufA, q, c, u);
 #pragma unroll
 		for (int mt = 0; mt < NT; ++mt) {
-			const h8 ad = lds_trfrag(bufD, L::RSS, q, c, mt);
+			const h8 ad = stg_trfrag(bufD, q, c, mt);
 #pragma unroll
 			for (int u = 0; u < NTI; ++u) acc.W0[mt][u] = mfma16(ad, bf[u], acc.W0[mt][u]);
 		}
@@ -459,8 +485,8 @@ __device__ __forceinline__ void fused_slice(const FusedTrainArgs& a, uint32_t ba
 #pragma unroll
 		for (int s = 0; s < KW; ++s) {
 			const h8 af = lds_wtfrag(sW0, L::RSI, 32 * s, 16 * u, q, c);
-			acc0 = mfma16(af, lds_afrag(bufD, L::RSS, c, 32 * s + 4 * q), acc0);
-			acc1 = mfma16(af, lds_afrag(bufD, L::RSS, 16 + c, 32 * s + 4 * q), acc1);
+			acc0 = mfma16(af, stg_afrag(bufD, c, 32 * s + 4 * q), acc0);
+			acc1 = mfma16(af, stg_afrag(bufD, 16 + c, 32 * s + 4 * q), acc1);
 		}
 		const h4 d0 = __builtin_convertvector(acc0, h4);
 		const h4 d1 = __builtin_convertvector(acc1, h4);

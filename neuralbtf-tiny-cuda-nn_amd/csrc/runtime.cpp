@@ -902,7 +902,15 @@ void TrainerHost::training_step(hipStream_t st, uint32_t B, const float* input, 
 void TrainerHost::training_step_overlapped(hipStream_t st, uint32_t B, const float* input, const float* target, bool run_optimizer) {
 	NetworkHost& m = *model;
 	mark(st, 0);
-	m.fused_kernel(st, ws, B, input, target, n_output_dims, loss_scale, w16.p, false);
+	const void* enc_soa = nullptr;
+	if (std::getenv("TCNN_SPLIT_ENCODE")) {  // A/B experiment: the encoding as its own pass, read by the fused kernel
+		const GridEncodingHost& g = *m.grid;
+		ws.enc16.reserve((size_t)m.mlp.n_input * B * 2);
+		launch_grid_fwd(st, g.desc.n_pos_dims, g.desc.n_features_per_level, g.desc.hash_type, B, g.desc.n_levels, input, g.desc.n_pos_dims,
+		                (const uint8_t*)w16.p + n_mlp * 2, ws.enc16.p, true, 0, g.dev_levels(), g.hash_grid(), g.desc.interp);
+		enc_soa = ws.enc16.p;
+	}
+	m.fused_kernel(st, ws, B, input, target, n_output_dims, loss_scale, w16.p, false, nullptr, nullptr, enc_soa);
 	mark(st, 1);
 	if (run_optimizer) ++adam_step;
 	GridBwdEpilogue ep{};

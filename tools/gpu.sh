@@ -8,6 +8,7 @@
 #   pmc[:<groups file>]    PMC passes over a short bench (tools/gpu_pmc.sh) + HBM traffic summary;
 #                          BENCH_EXTRA / PMC_FILTER pass through
 #   spread                 tools/render_spread.py (render PSNR per seed pair)
+#   profpy:<script> [args] rocprofv3 --kernel-trace --stats of a python tool (-> $OUT/profpyN)
 #   py:<script> [args]     any python tool under tools/ (120 s budget unless PY_TIMEOUT)
 # Output: gpurun_out/$OUT (default gpurun_out/job).
 set -o pipefail
@@ -48,6 +49,12 @@ for step in "$@"; do
     spread)
       timeout -k 10 600 python -u tools/render_spread.py "$D/render_spread.json" > "$log" 2>&1 || { echo SPREAD_FAILED; tail -20 "$log"; exit 1; }
       tail -25 "$log" ;;
+    profpy)
+      # rocprofv3 kernel stats of a python tool: profpy:<script> [args]
+      rm -rf "$D/profpy$n"
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$D/profpy$n" -o run -- python3 $arg > "$log" 2>&1 \
+        || { echo PROFPY_FAILED; tail -20 "$log"; exit 1; }
+      python3 tools/prof_top.py "$D/profpy$n" | head -12 ;;
     py)
       timeout -k 10 ${PY_TIMEOUT:-120} python -u $arg > "$log" 2>&1 || { echo "PY_FAILED $arg"; tail -20 "$log"; exit 1; }
       tail -${PY_TAIL:-15} "$log" ;;

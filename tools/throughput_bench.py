@@ -64,19 +64,24 @@ def main():
                          "rtx3090_samples_per_s": PUBLISHED_3090.get(("train", W, B))})
             s = timed(lambda: t.inference(pos), it)
             rows.append({"config": f"config_oneblob W{W} H{cfg['network']['n_hidden_layers']}", "mode": "infer", "batch": B,
-                         "engine": t.engine, "s_per_call": s, "samples_per_s": B / s,
+                         "engine": t.inference_engine, "s_per_call": s, "samples_per_s": B / s,
                          "rtx3090_samples_per_s": PUBLISHED_3090.get(("infer", W, B))})
             print(json.dumps(rows[-2]), flush=True)
             print(json.dumps(rows[-1]), flush=True)
         del t
     cfg = json.load(open(os.path.join(REPO, "tests", "golden", "config_hash.json")))
-    t = Trainer(2, 3, cfg, seed=1337)
-    for lb in (18, 21):
-        B = 1 << lb
-        pos = torch.rand(B, 2, device="cuda")
-        s = timed(lambda: t.inference(pos), args.iters)
-        rows.append({"config": "config_hash", "mode": "infer", "batch": B, "engine": t.engine, "s_per_call": s, "samples_per_s": B / s})
-        print(json.dumps(rows[-1]), flush=True)
+    cfg3 = copy.deepcopy(cfg)  # BASELINE configs[3]: HashGrid + W128/H4
+    cfg3["network"]["n_neurons"], cfg3["network"]["n_hidden_layers"] = 128, 4
+    for name, c in (("config_hash", cfg), ("configs3 HashGrid W128 H4", cfg3)):
+        t = Trainer(2, 3, c, seed=1337)
+        for lb in (18, 21):
+            B = 1 << lb
+            pos = torch.rand(B, 2, device="cuda")
+            s = timed(lambda: t.inference(pos), args.iters)
+            rows.append({"config": name, "mode": "infer", "batch": B, "engine": t.inference_engine, "s_per_call": s,
+                         "samples_per_s": B / s})
+            print(json.dumps(rows[-1]), flush=True)
+        del t
     if args.out:
         with open(args.out, "w") as f:
             json.dump({"device": torch.cuda.get_device_name(0), "rows": rows}, f, indent=1)
