@@ -157,9 +157,13 @@ def main():
                     help="strong: shard the global batch over ranks (configs[4]); weak: a full batch per rank")
     ap.add_argument("--allreduce-dtype", choices=["fp32", "fp16"], default="fp32")
     ap.add_argument("--no-overlap", action="store_true", help="all-reduce after the whole backward")
-    ap.add_argument("--optimizer", choices=["sharded", "replicated"], default="sharded",
-                    help="N > 1: sharded = reduce-scatter the gradient sums, Adam on 1/N of the parameters, "
-                         "all-gather the fp16 parameters; replicated = all-reduce, Adam everywhere")
+    ap.add_argument("--optimizer", choices=["sharded", "replicated"], default="replicated",
+                    help="N > 1: replicated = all-reduce of the gradient sums, Adam everywhere (default: the schedule "
+                         "with the plainest collective; no multi-GPU RCCL run of either is recorded yet); sharded = "
+                         "reduce-scatter, Adam on 1/N of the parameters, all-gather of the fp16 parameters")
+    ap.add_argument("--exchange", choices=["torch", "engine"], default="torch",
+                    help="N > 1: torch = torch.distributed collectives driven from Python; engine = RCCL issued by "
+                         "the training step itself (tcnn_trainer_set_dp: one call per step, hipGraph-capturable)")
     ap.add_argument("--graph", action="store_true", help="replay the single-GPU training step as a hipGraph")
     ap.add_argument("--all-ranks-on-device0", action="store_true",
                     help="rehearse N>1 on a 1-GPU box (gloo); never used for measurements")
@@ -216,8 +220,9 @@ def main():
 
     from tinycudann.parallel import DataParallelTrainer
     sharded = world > 1 and args.optimizer == "sharded" and args.allreduce_dtype == "fp32"
+    exchange = args.exchange if args.allreduce_dtype == "fp32" else "torch"
     dp = DataParallelTrainer(trainer, overlap=not args.no_overlap, allreduce_dtype=args.allreduce_dtype,
-                             shard_optimizer=sharded)
+                             shard_optimizer=sharded, exchange=exchange)
     if args.graph:
         trainer.set_graph(True)
 
@@ -283,7 +288,8 @@ def main():
             "parallelism": "dp1" if world == 1 else (f"dp{world} batch-sharded ({B_global}/{world} points per rank)" if args.scaling == "strong"
                             else f"dp{world} ({B} points per rank)") +
                            ((", fp32 reduce-scatter + Adam on 1/N of the parameters + fp16 all-gather (sharded optimizer)" if sharded else
-                             f", {args.allreduce_dtype} all-reduce" + ("" if args.no_overlap else " overlapped with the grid backward"))
+                             f", {args.allreduce_dtype} all-reduce" + ("" if args.no_overlap else " overlapped with the grid backward")) +
+                            (", RCCL issued by the engine's step" if exchange == "engine" else ", torch.distributed from Python")
                             if world > 1 else ""),
         },
         "step_graph": bool(args.graph),

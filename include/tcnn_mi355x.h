@@ -129,6 +129,25 @@ int tcnn_trainer_optimizer_step(tcnn_trainer* t, void* stream);
  * optimizer: each rank updates its shard of the reduce-scattered gradient sums; the caller then
  * all-gathers the fp16 parameters). Not in the reference, which has no multi-GPU path. */
 int tcnn_trainer_optimizer_step_range(tcnn_trainer* t, void* stream, uint64_t begin, uint64_t end);
+/* ---- data-parallel exchange inside the engine (not in the reference, which has no multi-GPU path;
+ * SURVEY.md §5, §8(e)) ----
+ * One process per GPU. Rank 0 creates a unique id, the caller broadcasts its TCNN_DP_ID_BYTES bytes
+ * (e.g. over torch.distributed), every rank creates its communicator (RCCL over xGMI, loaded on first
+ * use) on its current device and attaches it to its trainer. From then on every
+ * tcnn_trainer_training_step(run_optimizer = 1) is the whole data-parallel step in one call on
+ * `stream` (hipGraph-capturable): this rank's forward / backward, the fp32 gradient sum across ranks
+ * on the communicator's stream (the network part overlapped with the grid backward), then Adam with
+ * gradient scale 1/N -- on every parameter (sharded = 0), or on this rank's 1/N shard of the
+ * reduce-scattered sum followed by an all-gather of the fp16 parameters (sharded = 1; the fp32
+ * masters and Adam state then stay current on the shard only: tcnn_trainer_dp_gather_state before
+ * serialize(with_optimizer)). The communicator must outlive its attachment (attach NULL to detach). */
+#define TCNN_DP_ID_BYTES 128
+typedef struct tcnn_dp_comm tcnn_dp_comm;
+int tcnn_dp_unique_id(void* id);
+tcnn_dp_comm* tcnn_dp_comm_create(const void* id, int nranks, int rank);
+void tcnn_dp_comm_destroy(tcnn_dp_comm* c);
+int tcnn_trainer_set_dp(tcnn_trainer* t, tcnn_dp_comm* c, int sharded);
+int tcnn_trainer_dp_gather_state(tcnn_trainer* t, void* stream);
 /* Trainer::loss(stream, ctx) of the last training step (trainer.h:205-207); synchronises `stream`. */
 float tcnn_trainer_loss(tcnn_trainer* t, void* stream);
 /* Device pointer to the last step's loss sum (fp32 scalar), for graph-friendly readback. */
@@ -143,6 +162,9 @@ float* tcnn_trainer_params_fp32(tcnn_trainer* t);
 void* tcnn_trainer_params(tcnn_trainer* t);
 void* tcnn_trainer_param_gradients(tcnn_trainer* t);
 float* tcnn_trainer_gradients_fp32(tcnn_trainer* t);
+/* Adam state buffers (adam.h:128-148): first / second moments fp32 and per-parameter step counts
+ * uint32, [n_params] each (device pointers owned by the trainer). */
+int tcnn_trainer_optimizer_state(tcnn_trainer* t, float** first_moments, float** second_moments, uint32_t** steps);
 /* Data-parallel support: Adam reads grad_fp32 * grad_scale (set 1/N after a sum all-reduce). */
 int tcnn_trainer_set_gradient_scale(tcnn_trainer* t, float scale);
 /* hipGraph replay of the single-GPU training step (the reference Trainer's CUDA graph,

@@ -256,6 +256,9 @@ struct tcnn_context {
 struct tcnn_trainer {
 	std::unique_ptr<TrainerHost> t;
 };
+struct tcnn_dp_comm {
+	std::unique_ptr<DpComm> c;
+};
 
 extern "C" {
 
@@ -423,6 +426,23 @@ int tcnn_trainer_optimizer_step(tcnn_trainer* t, void* stream) {
 int tcnn_trainer_optimizer_step_range(tcnn_trainer* t, void* stream, uint64_t begin, uint64_t end) {
 	return guard([&] { t->t->optimizer_step_range((hipStream_t)stream, begin, end); });
 }
+int tcnn_dp_unique_id(void* id) {
+	return guard([&] { dp_unique_id(id); });
+}
+tcnn_dp_comm* tcnn_dp_comm_create(const void* id, int nranks, int rank) {
+	return guard_ptr<tcnn_dp_comm>([&] {
+		auto* r = new tcnn_dp_comm;
+		r->c = std::make_unique<DpComm>(id, nranks, rank);
+		return r;
+	});
+}
+void tcnn_dp_comm_destroy(tcnn_dp_comm* c) { delete c; }
+int tcnn_trainer_set_dp(tcnn_trainer* t, tcnn_dp_comm* c, int sharded) {
+	return guard([&] { t->t->set_dp(c ? c->c.get() : nullptr, sharded != 0); });
+}
+int tcnn_trainer_dp_gather_state(tcnn_trainer* t, void* stream) {
+	return guard([&] { t->t->dp_gather_state((hipStream_t)stream); });
+}
 float tcnn_trainer_loss(tcnn_trainer* t, void* stream) {
 	float v = -1.0f;
 	if (guard([&] { v = t->t->loss((hipStream_t)stream); }) != 0) return -1.0f;
@@ -440,6 +460,12 @@ float* tcnn_trainer_params_fp32(tcnn_trainer* t) { return t->t->w32.as<float>();
 void* tcnn_trainer_params(tcnn_trainer* t) { return t->t->w16.p; }
 void* tcnn_trainer_param_gradients(tcnn_trainer* t) { return t->t->g16.p; }
 float* tcnn_trainer_gradients_fp32(tcnn_trainer* t) { return t->t->g32.as<float>(); }
+int tcnn_trainer_optimizer_state(tcnn_trainer* t, float** m1, float** m2, uint32_t** steps) {
+	if (m1) *m1 = t->t->m1.as<float>();
+	if (m2) *m2 = t->t->m2.as<float>();
+	if (steps) *steps = t->t->steps.as<uint32_t>();
+	return 0;
+}
 int tcnn_trainer_set_gradient_scale(tcnn_trainer* t, float s) {
 	t->t->grad_scale = s;
 	return 0;
@@ -473,6 +499,14 @@ int tcnn_trainer_update_hyperparams(tcnn_trainer* t, const char* params_json) {
 	return guard([&] {
 		const json p = json::parse(params_json);
 		if (p.count("optimizer")) t->t->adam.update(p["optimizer"]);  // Trainer::update_hyperparams, trainer.h:213-216
+		// the reference forwards "loss" to Loss::update_hyperparams, which holds no hyperparameters
+		// (relative_l2.h, l2.h): the loss type is fixed at construction there too -- say so instead of
+		// ignoring a request to change it
+		if (p.count("loss") && p["loss"].is_object() && p["loss"].count("otype")) {
+			const std::string o = p["loss"]["otype"].get<std::string>();
+			TCNN_CHECK(ieq(o, t->t->loss_otype), "update_hyperparams: the loss type is fixed at construction ('" + t->t->loss_otype +
+			                                         "'), cannot change it to '" + o + "'");
+		}
 	});
 }
 const char* tcnn_trainer_hyperparams(tcnn_trainer* t) {

@@ -50,32 +50,52 @@ constexpr int tile_halves(int W, int IN, int NH, int NS) {
 // layers; with 5 its weight-gradient accumulators (>= 164 registers) spill at 256 registers per wave,
 // so it runs 4 waves (1 per SIMD, 512 registers incl. AGPRs, two row tiles each); W64 4; W32 2 (one
 // row tile each)
-constexpr int tile_waves(int W, int NH) { return W == 128 && NH < 5 ? 8 : (W == 32 ? 2 : 4); }
+//
+// Register-resident variant (RA): every hidden matrix's A fragments -- forward (the wave's output
+// rows) and backward (the wave's input features, from the transposed copy) -- are loaded once per
+// launch into registers and stay there; no hidden matrix is staged in LDS and no A operand is read
+// from it. W64: 4 waves of one row tile each, two workgroups per CU (IN 128 with 5 hidden layers would
+// spill at 256 registers). W128: 4 waves (one per SIMD, two row tiles each, up to 512 registers:
+// 64 per hidden matrix for the fragments + the weight-gradient accumulators), for IN <= 32 and at most
+// 3 hidden layers -- with 4 the kernel spills 24 registers and measured 2 % slower than the 8-wave
+// LDS-staged kernel (profiles/r03_tile_ra_ab.json); measured 1.03-1.06x faster on the W64 configs and
+// HashGrid + W128/H3.
+constexpr bool tile_ra_ok(int W, int IN, int NH) {
+	return NH > 1 && ((W == 64 && !(IN > 64 && NH > 4)) || (W == 128 && IN <= 32 && NH <= 3));
+}
+constexpr int tile_waves(int W, int NH, bool RA = false) { return W == 128 && NH < 5 && !RA ? 8 : (W == 32 ? 2 : 4); }
 constexpr int tile_lds_limit() { return 160 * 1024; }
 // fewest streamed hidden matrices that let the rest of the network + the tile's activations fit
-constexpr int tile_n_streamed(int W, int IN, int NH) {
+// (RA: all of them, from registers)
+constexpr int tile_n_streamed(int W, int IN, int NH, bool RA = false) {
+	if (RA) return NH - 1;
 	int ns = 0;
 	while (ns < NH - 1 && tile_halves(W, IN, NH, ns) * 2 + tile_waves(W, NH) * 4 > tile_lds_limit()) ++ns;
 	return ns;
 }
-// workgroups per CU the launch aims for: two waves per SIMD where the LDS allows
-constexpr int tile_train_wg_per_cu(int W, int IN, int NH) {
-	return tile_imax(1, tile_imin(8 / tile_waves(W, NH), tile_lds_limit() / (tile_halves(W, IN, NH, tile_n_streamed(W, IN, NH)) * 2 + tile_waves(W, NH) * 4)));
+// workgroups per CU the launch aims for: two waves per SIMD where the LDS (and, for W128 RA, the
+// registers) allow
+constexpr int tile_train_wg_per_cu(int W, int IN, int NH, bool RA = false) {
+	return W == 128 && RA ? 1
+	                      : tile_imax(1, tile_imin(8 / tile_waves(W, NH, RA),
+	                                               tile_lds_limit() / (tile_halves(W, IN, NH, tile_n_streamed(W, IN, NH, RA)) * 2 + tile_waves(W, NH, RA) * 4)));
 }
 
-template <int WR, int IN, int NH>
+template <int WR, int IN, int NH, bool RA = false>
 struct TileLayout {
 	static constexpr int W = tile_kw(WR);
 	static_assert(W == 32 || W == 64 || W == 128, "tile engine: W in {16, 32, 64, 128}");
 	static_assert(IN % 16 == 0 && IN <= 128, "tile engine: IN a multiple of 16, <= 128");
+	static_assert(!RA || tile_ra_ok(W, IN, NH), "register-resident variant: shape out of its register budget");
 	static constexpr int KP0 = (IN + 31) / 32 * 32;  // K of the first layer, padded to the MFMA depth
 	static constexpr int RS0 = KP0 + 8, RSW = W + 8, RSG = 24;
-	static constexpr int WAVES = tile_waves(W, NH), NTHR = WAVES * 64;
+	static constexpr int WAVES = tile_waves(W, NH, RA), NTHR = WAVES * 64;
 	static constexpr int MT = W / 16, MTW = MT / WAVES;  // output-row tiles per matrix / per wave
 	static constexpr int KT0 = IN / 16;              // feature tiles of the input
 	// hidden matrices 1..NS are not staged: their forward A fragments come from the fp16 parameters
 	// (L2-resident, every workgroup reads the same 32 KB), their backward ones from a transposed copy
-	static constexpr int NS = tile_n_streamed(W, IN, NH);
+	// (RA: loaded once into registers)
+	static constexpr int NS = tile_n_streamed(W, IN, NH, RA);
 	static_assert(NS == 0 || W == WR, "streamed matrices only for unpadded widths");
 	static constexpr int oW0 = 0, oWh = oW0 + W * RS0, oWo = oWh + (NH - 1 - NS) * W * RSW;
 	static constexpr int oX = oWo + 16 * RSW;                 // slot 0: the tile's input [32][RS0]
@@ -84,7 +104,7 @@ struct TileLayout {
 	static constexpr int HALVES = oG + 32 * RSG;
 	static constexpr int BYTES = HALVES * 2 + WAVES * 4;       // + per-wave loss
 	static constexpr int N_MLP = WR * IN + (NH - 1) * WR * WR + 16 * WR;  // parameters (unpadded)
-	static constexpr int WG_PER_CU = tile_train_wg_per_cu(W, IN, NH);
+	static constexpr int WG_PER_CU = tile_train_wg_per_cu(W, IN, NH, RA);
 	// waves per SIMD the launch runs (amdgpu_waves_per_eu: caps the registers so they fit)
 	static constexpr int WAVES_PER_EU = tile_imax(1, WG_PER_CU * WAVES / 4);
 	static_assert(HALVES == tile_halves(W, IN, NH, NS), "layout");
@@ -125,14 +145,14 @@ __device__ __forceinline__ h4 out_act_fwd(int a, f4 y) {
 }
 
 // launch bounds as plain function calls (a template-id's commas would split the macro arguments)
-constexpr int tile_train_nthr(int WR, int NH) { return tile_waves(tile_kw(WR), NH) * 64; }
-constexpr int tile_train_weu(int WR, int IN, int NH) {
-	return tile_imax(1, tile_train_wg_per_cu(tile_kw(WR), IN, NH) * tile_waves(tile_kw(WR), NH) / 4);
+constexpr int tile_train_nthr(int WR, int NH, bool RA) { return tile_waves(tile_kw(WR), NH, RA) * 64; }
+constexpr int tile_train_weu(int WR, int IN, int NH, bool RA) {
+	return tile_imax(1, tile_train_wg_per_cu(tile_kw(WR), IN, NH, RA) * tile_waves(tile_kw(WR), NH, RA) / 4);
 }
 
-template <int WR, int IN, int NH, Act ACT>
-__global__ __launch_bounds__(tile_train_nthr(WR, NH), tile_train_weu(WR, IN, NH)) void k_mlp_tile_train(const TileTrainArgs a) {
-	using L = TileLayout<WR, IN, NH>;
+template <int WR, int IN, int NH, Act ACT, bool RA>
+__global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN, NH, RA)) void k_mlp_tile_train(const TileTrainArgs a) {
+	using L = TileLayout<WR, IN, NH, RA>;
 	constexpr int W = L::W;
 	constexpr int MTW = L::MTW, KT0 = L::KT0, RS0 = L::RS0, RSW = L::RSW, RSG = L::RSG;
 	constexpr int WAVES = L::WAVES, NTHR = L::NTHR;
@@ -178,6 +198,22 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH), tile_train_weu(WR, IN, NH)
 	f4 dW0[MTW][KT0];
 	f4 dWh[NH > 1 ? NH - 1 : 1][MTW][L::MT];
 	f4 dWo[NTW];
+	// RA: the hidden matrices' forward / backward A fragments, loaded once (rows resp. input features
+	// 16 (wave MTW + i) + c, K columns 32 s + 8 q ..+7)
+	constexpr int NRA = RA ? NH - 1 : 1;
+	h8 pag[NRA][MTW][W / 32], pagT[NRA][MTW][W / 32];
+	if constexpr (RA) {
+#pragma unroll
+		for (int j = 0; j < NH - 1; ++j)
+#pragma unroll
+			for (int i = 0; i < MTW; ++i)
+#pragma unroll
+				for (int s = 0; s < W / 32; ++s) {
+					const size_t o = (size_t)j * W * W + (size_t)(16 * (wave * MTW + i) + c) * W + 32 * s + 8 * q;
+					pag[j][i][s] = *(const h8*)(a.params + (size_t)W * IN + o);
+					pagT[j][i][s] = *(const h8*)(a.wT + o);
+				}
+	}
 #pragma unroll
 	for (int i = 0; i < MTW; ++i) {
 #pragma unroll
@@ -241,7 +277,12 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH), tile_train_weu(WR, IN, NH)
 #pragma unroll
 			for (int i = 0; i < MTW; ++i) acc[i][0] = acc[i][1] = fz;
 			h8 ag[MTW][W / 32];  // a streamed layer's A fragments, all loads issued before the first MFMA
-			if (streamed(m)) {
+			if (RA && streamed(m)) {
+#pragma unroll
+				for (int i = 0; i < MTW; ++i)
+#pragma unroll
+					for (int s = 0; s < W / 32; ++s) ag[i][s] = pag[m >= 1 ? m - 1 : 0][i][s];
+			} else if (streamed(m)) {
 				const _Float16* Wg = a.params + (size_t)W * IN + (size_t)(m - 1) * W * W;
 #pragma unroll
 				for (int i = 0; i < MTW; ++i)
@@ -347,7 +388,12 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH), tile_train_weu(WR, IN, NH)
 			// a streamed matrix's transposed A fragments (A[feature][neuron] = M^T rows of this wave's
 			// tiles), loaded ahead so the latency hides behind the weight-gradient MFMAs
 			h8 agT[MTW][W / 32];
-			if (streamed(m)) {
+			if (RA && streamed(m)) {
+#pragma unroll
+				for (int i = 0; i < MTW; ++i)
+#pragma unroll
+					for (int s = 0; s < W / 32; ++s) agT[i][s] = pagT[m >= 1 ? m - 1 : 0][i][s];
+			} else if (streamed(m)) {
 				const _Float16* WgT = a.wT + (size_t)(m - 1) * W * W;
 #pragma unroll
 				for (int i = 0; i < MTW; ++i)
@@ -633,9 +679,14 @@ __global__ __launch_bounds__(tile_infer_nthr(WR), tile_infer_weu(WR, IN, NH)) vo
 	X(w, 128, 1) X(w, 128, 2) X(w, 128, 3) X(w, 128, 4) X(w, 128, 5)
 
 struct TileShapeInfo {
-	uint32_t lds_bytes, n_streamed, wg_per_cu, waves;  // training
+	uint32_t lds_bytes, n_streamed, wg_per_cu, waves;  // training (the variant tile_ra_selected picks)
 	uint32_t infer_lds_bytes, infer_wg_per_cu, infer_tile;
+	uint32_t reg_a;                                    // 1: the register-resident training variant
 };
+
+// whether the training launch of a shape with tile_ra_ok takes the register-resident variant (its
+// default policy, TCNN_TILE_REG_A=0/1 overrides; read once per process)
+bool tile_ra_selected(uint32_t W, uint32_t IN, uint32_t NH);
 
 // per-width entry points (one translation unit per width); false if (IN, NH) is not instantiated
 bool tile_shape_w16(uint32_t IN, uint32_t NH, TileShapeInfo* info);
@@ -651,14 +702,39 @@ bool tile_infer_w32(hipStream_t st, uint32_t IN, uint32_t NH, int act, uint32_t 
 bool tile_infer_w64(hipStream_t st, uint32_t IN, uint32_t NH, int act, uint32_t blocks, const TileInferArgs& a);
 bool tile_infer_w128(hipStream_t st, uint32_t IN, uint32_t NH, int act, uint32_t blocks, const TileInferArgs& a);
 
+template <int WR, int IN, int NH>
+inline void tile_info_fill(TileShapeInfo* info) {
+	using L = TileLayout<WR, IN, NH>;
+	using LI = TileInferLayout<WR, IN, NH>;
+	*info = TileShapeInfo{(uint32_t)L::BYTES, (uint32_t)L::NS, (uint32_t)L::WG_PER_CU, (uint32_t)L::WAVES,
+	                      (uint32_t)LI::BYTES, (uint32_t)LI::WG_PER_CU, (uint32_t)LI::T, 0u};
+	if constexpr (tile_ra_ok(tile_kw(WR), IN, NH)) {
+		if (tile_ra_selected(WR, IN, NH)) {
+			using LR = TileLayout<WR, IN, NH, true>;
+			info->lds_bytes = LR::BYTES, info->n_streamed = LR::NS, info->wg_per_cu = LR::WG_PER_CU, info->waves = LR::WAVES;
+			info->reg_a = 1u;
+		}
+	}
+}
+
 // the definitions of one width's entry points (used once per mlp_tile_w*.hip)
 #define TCNN_TILE_WIDTH_TU(w)                                                                                                    \
+	template <int IN, int NH, Act A, bool RA>                                                                                    \
+	static void tile_train_launch_v_##w(hipStream_t st, uint32_t blocks, const TileTrainArgs& a) {                               \
+		using L = TileLayout<w, IN, NH, RA>;                                                                                     \
+		static uint64_t done = 0;                                                                                                \
+		set_dyn_lds((const void*)k_mlp_tile_train<w, IN, NH, A, RA>, L::BYTES, done);                                            \
+		hipLaunchKernelGGL((k_mlp_tile_train<w, IN, NH, A, RA>), dim3(blocks), dim3(L::NTHR), L::BYTES, st, a);                 \
+	}                                                                                                                            \
 	template <int IN, int NH, Act A>                                                                                             \
 	static void tile_train_launch_##w(hipStream_t st, uint32_t blocks, const TileTrainArgs& a) {                                 \
-		using L = TileLayout<w, IN, NH>;                                                                                         \
-		static uint64_t done = 0;                                                                                                \
-		set_dyn_lds((const void*)k_mlp_tile_train<w, IN, NH, A>, L::BYTES, done);                                                \
-		hipLaunchKernelGGL((k_mlp_tile_train<w, IN, NH, A>), dim3(blocks), dim3(L::NTHR), L::BYTES, st, a);                     \
+		if constexpr (tile_ra_ok(tile_kw(w), IN, NH)) {                                                                          \
+			if (tile_ra_selected(w, IN, NH)) {                                                                                   \
+				tile_train_launch_v_##w<IN, NH, A, true>(st, blocks, a);                                                         \
+				return;                                                                                                          \
+			}                                                                                                                    \
+		}                                                                                                                        \
+		tile_train_launch_v_##w<IN, NH, A, false>(st, blocks, a);                                                                \
 	}                                                                                                                            \
 	template <int IN, int NH, Act A>                                                                                             \
 	static void tile_infer_launch_##w(hipStream_t st, uint32_t blocks, const TileInferArgs& a) {                                 \
@@ -682,10 +758,7 @@ bool tile_infer_w128(hipStream_t st, uint32_t IN, uint32_t NH, int act, uint32_t
 
 #define TCNN_TILE_INFO_X(w, in, nh)                                                                                              \
 	if (IN == in && NH == nh) {                                                                                                  \
-		using L = TileLayout<w, in, nh>;                                                                                         \
-		using LI = TileInferLayout<w, in, nh>;                                                                                   \
-		*info = TileShapeInfo{(uint32_t)L::BYTES, (uint32_t)L::NS, (uint32_t)L::WG_PER_CU, (uint32_t)L::WAVES,                  \
-		                      (uint32_t)LI::BYTES, (uint32_t)LI::WG_PER_CU, (uint32_t)LI::T};                                    \
+		tile_info_fill<w, in, nh>(info);                                                                                         \
 		return true;                                                                                                             \
 	}
 #define TCNN_TILE_TRAIN_X(w, in, nh)                                                                                             \

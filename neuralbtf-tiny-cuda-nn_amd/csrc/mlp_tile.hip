@@ -6,6 +6,17 @@
 
 namespace tcnn_amd {
 
+// Register-resident training variant (mlp_tile.h, tile_ra_ok): the default for every eligible shape;
+// TCNN_TILE_REG_A=0 selects the LDS-staged kernel instead (A/B switch).
+bool tile_ra_selected(uint32_t W, uint32_t IN, uint32_t NH) {
+	static const int env = [] {
+		const char* e = std::getenv("TCNN_TILE_REG_A");
+		return e ? (std::atoi(e) != 0 ? 1 : 0) : -1;
+	}();
+	if (!tile_ra_ok((int)tile_kw((int)W), (int)IN, (int)NH)) return false;
+	return env != 0;
+}
+
 static bool tile_shape(uint32_t W, uint32_t IN, uint32_t NH, TileShapeInfo* info) {
 	switch (W) {
 		case 16: return tile_shape_w16(IN, NH, info);

@@ -876,6 +876,11 @@ void TrainerHost::training_step(hipStream_t st, uint32_t B, const float* input, 
 		timer.sampling = (timer.counter++ % timer.every) == 0;
 		if (timer.sampling) timer.marks.push_back({-1, -1, -1, -1, -1});
 	}
+	if (dp && run_optimizer) {
+		if (use_graph && !timer.enabled && !adam.adabound && training_step_graph(st, B, input, target)) return;
+		training_step_dp(st, B, input, target);
+		return;
+	}
 	if (overlapped_ok()) {
 		if (use_graph && run_optimizer && !timer.enabled && !adam.adabound && training_step_graph(st, B, input, target)) return;
 		training_step_overlapped(st, B, input, target, run_optimizer);
@@ -1010,7 +1015,8 @@ std::vector<uint64_t> TrainerHost::graph_key(uint32_t B, const float* input, con
 	                           (uint64_t)(uintptr_t)ws.loss_partial.p, (uint64_t)(uintptr_t)ws.wimage.p,
 	                           (uint64_t)(uintptr_t)ws.gbw.partial.p, (uint64_t)(uintptr_t)ws.gbw.recs.p,
 	                           (uint64_t)(uintptr_t)ws.gbw.dir.p, (uint64_t)(uintptr_t)ws.gbw.dysum.p, ws.n_fused_blocks,
-	                           ws.gbw.n_chunks, (uint64_t)overlapped_ok()};
+	                           ws.gbw.n_chunks, (uint64_t)overlapped_ok(), (uint64_t)(uintptr_t)dp, (uint64_t)dp_sharded, dp_per,
+	                           (uint64_t)(uintptr_t)ws.enc16.p};
 	// every scalar the step's kernels take from the trainer (AdamArgs holds no pointer here)
 	const AdamArgs a = adam_args();
 	const size_t n = sizeof(AdamArgs) / 8 + 1;
@@ -1029,7 +1035,7 @@ std::vector<uint64_t> TrainerHost::graph_key(uint32_t B, const float* input, con
 }
 
 bool TrainerHost::training_step_graph(hipStream_t st, uint32_t B, const float* input, const float* target) {
-	if (adam_step + 1 >= GRAPH_STEPS || !ws.wimage_valid) return false;  // first step packs the weights eagerly
+	if (adam_step + 1 >= GRAPH_STEPS || (!dp && !ws.wimage_valid)) return false;  // first step packs the weights eagerly
 	if (ftable_valid < GRAPH_STEPS || ftable_b1 != adam.beta1 || ftable_b2 != adam.beta2)
 		(void)adam_args_table(st, GRAPH_STEPS, GRAPH_STEPS);
 	if (!graph) graph = std::make_unique<StepGraph>();
@@ -1037,7 +1043,8 @@ bool TrainerHost::training_step_graph(hipStream_t st, uint32_t B, const float* i
 	hipGraphExec_t exec = graph->find(key);
 	if (!exec) {
 		// eager step first (sizes every workspace for this B, so the capture allocates nothing)
-		training_step_overlapped(st, B, input, target, true);
+		if (dp) training_step_dp(st, B, input, target);
+		else training_step_overlapped(st, B, input, target, true);
 		key = graph_key(B, input, target);
 		TCNN_HIP_CHECK(hipStreamSynchronize(st));
 		TCNN_HIP_CHECK(hipStreamSynchronize(graph->cs));
@@ -1046,15 +1053,17 @@ bool TrainerHost::training_step_graph(hipStream_t st, uint32_t B, const float* i
 			graph->execs.erase(graph->execs.begin());
 		}
 		const uint32_t step0 = adam_step, ftv0 = ftable_valid, lb0 = last_B;
-		const bool wv0 = ws.wimage_valid;
+		const bool wv0 = ws.wimage_valid, dps0 = dp_state_partial;
 		hipGraph_t g = nullptr;
 		TCNN_HIP_CHECK(hipStreamBeginCapture(graph->cs, hipStreamCaptureModeThreadLocal));
-		training_step_overlapped(graph->cs, B, input, target, true);
+		if (dp) training_step_dp(graph->cs, B, input, target);
+		else training_step_overlapped(graph->cs, B, input, target, true);
 		TCNN_HIP_CHECK(hipStreamEndCapture(graph->cs, &g));
 		adam_step = step0;  // the capture ran nothing
 		ftable_valid = ftv0;
 		last_B = lb0;
 		ws.wimage_valid = wv0;
+		dp_state_partial = dps0;
 		hipGraphExec_t e = nullptr;
 		const hipError_t err = hipGraphInstantiate(&e, g, nullptr, nullptr, 0);
 		(void)hipGraphDestroy(g);
@@ -1068,9 +1077,10 @@ bool TrainerHost::training_step_graph(hipStream_t st, uint32_t B, const float* i
 	TCNN_HIP_CHECK(hipGraphLaunch(exec, graph->cs));
 	TCNN_HIP_CHECK(hipEventRecord(graph->e1, graph->cs));
 	TCNN_HIP_CHECK(hipStreamWaitEvent(st, graph->e1, 0));
-	// the host-side effects of training_step_overlapped
+	// the host-side effects of training_step_overlapped / training_step_dp
 	++adam_step;
-	ws.wimage_valid = true;
+	ws.wimage_valid = !dp;  // the data-parallel step leaves the weight image to be packed by the next step
+	if (dp && dp_sharded) dp_state_partial = true;
 	last_B = B;
 	++graph_replays;
 	return true;

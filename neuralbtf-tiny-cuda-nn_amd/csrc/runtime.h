@@ -267,6 +267,25 @@ struct PhaseTimer {
 	~PhaseTimer();
 };
 
+// One RCCL communicator of a data-parallel job (dp.cpp): rank `rank` of `nranks`, one process per
+// GPU; collectives run on its own stream `cs`, joined to the trainer's stream with events.
+struct DpComm {
+	void* comm = nullptr;  // ncclComm_t
+	int nranks = 1, rank = 0;
+	hipStream_t cs = nullptr;
+	hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+	DpComm(const void* unique_id, int nranks, int rank);
+	~DpComm();
+	DpComm(const DpComm&) = delete;
+	DpComm& operator=(const DpComm&) = delete;
+	void all_reduce_f32(float* buf, size_t n, hipStream_t st);
+	// in place: rank r receives the sum of [r per, (r + 1) per) at buf + r per
+	void reduce_scatter_f32(float* buf, size_t per, hipStream_t st);
+	// in place: rank r's [r per, (r + 1) per) elements of elem_bytes (2 or 4) to every rank
+	void all_gather(void* buf, size_t per_elems, int elem_bytes, hipStream_t st);
+};
+void dp_unique_id(void* id128);  // ncclGetUniqueId (one rank; the caller broadcasts it)
+
 struct TrainerHost {
 	uint32_t n_input_dims, n_output_dims;
 	PhaseTimer timer;
@@ -300,6 +319,15 @@ struct TrainerHost {
 	void training_step(hipStream_t st, uint32_t B, const float* input, const float* target, bool run_optimizer);
 	void training_step_part(hipStream_t st, uint32_t B, const float* input, const float* target, int part);
 	void optimizer_step(hipStream_t st);
+	// data-parallel exchange inside the step (dp.cpp): with a communicator attached every
+	// training_step(run_optimizer = true) sums the gradients across the ranks (all-reduce, or
+	// reduce-scatter + Adam on this rank's shard + all-gather of the fp16 parameters when sharded)
+	DpComm* dp = nullptr;
+	bool dp_sharded = false, dp_state_partial = false;
+	uint64_t dp_per = 0;  // parameters per shard (sharded: buffers padded to nranks * dp_per)
+	void set_dp(DpComm* c, bool sharded);
+	void training_step_dp(hipStream_t st, uint32_t B, const float* input, const float* target);
+	void dp_gather_state(hipStream_t st);
 	// Adam on parameters [begin, end) only (data-parallel sharded optimizer: each rank updates its
 	// shard of the reduce-scattered gradient, then the fp16 parameters are all-gathered)
 	void optimizer_step_range(hipStream_t st, uint64_t begin, uint64_t end);

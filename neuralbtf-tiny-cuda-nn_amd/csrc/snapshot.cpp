@@ -223,6 +223,9 @@ MsgValue from_json_text(const json& j) {
 }  // namespace
 
 std::vector<uint8_t> TrainerHost::serialize(bool with_optimizer) {
+	TCNN_CHECK(!(with_optimizer && dp_sharded && dp_state_partial),
+	           "serialize(optimizer): the sharded data-parallel optimizer state is current only on each rank's shard; "
+	           "gather it first (tcnn_trainer_dp_gather_state)");
 	TCNN_HIP_CHECK(hipDeviceSynchronize());
 	const size_t n = n_params;
 	MsgWriter w;

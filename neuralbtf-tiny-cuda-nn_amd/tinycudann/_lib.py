@@ -74,6 +74,12 @@ _SIGS = {
     "tcnn_trainer_hyperparams": (c_char_p, [c_void_p]),
     "tcnn_trainer_initialize_params": (c_int, [c_void_p, c_uint32]),
     "tcnn_trainer_engine": (c_char_p, [c_void_p]),
+    "tcnn_trainer_optimizer_state": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "tcnn_dp_unique_id": (c_int, [c_void_p]),
+    "tcnn_dp_comm_create": (c_void_p, [c_void_p, c_int, c_int]),
+    "tcnn_dp_comm_destroy": (None, [c_void_p]),
+    "tcnn_trainer_set_dp": (c_int, [c_void_p, c_void_p, c_int]),
+    "tcnn_trainer_dp_gather_state": (c_int, [c_void_p, c_void_p]),
     "tcnn_trainer_inference_engine": (c_char_p, [c_void_p]),
     "tcnn_module_engine": (c_char_p, [c_void_p]),
     "tcnn_module_inference_engine": (c_char_p, [c_void_p]),

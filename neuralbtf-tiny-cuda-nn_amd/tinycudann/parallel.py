@@ -20,19 +20,28 @@ to fp16 (the reference's gradient buffer is __half, trainer.h:327), the fp16 sum
 collective, and Adam reads it with scale 1. The default fp32 exchange keeps the single-GPU
 numerics (one fp16 rounding of the reduced sum).
 
-shard_optimizer=True (ZeRO-1 style; the default of bench.py for N > 1): instead of the all-reduce,
+exchange="engine": the same exchange runs inside the engine instead (EngineComm, tcnn_trainer_set_dp):
+one RCCL communicator created from a unique id broadcast over torch.distributed, the collectives
+issued by the training step itself on its stream (network part overlapped with the grid backward),
+so a data-parallel step is one C-ABI call that a hipGraph can capture. exchange="torch" (default)
+drives torch.distributed collectives from Python -- also the gloo rehearsal on CPU.
+
+shard_optimizer=True (ZeRO-1 style): instead of the all-reduce,
 the fp32 gradient sums are reduce-scattered (each rank receives the sum of one contiguous 1/N of the
 parameter vector), each rank runs Adam on its shard only (Trainer.optimizer_step_range, grad scale
 1/N), and the updated fp16 parameters -- what the next step's kernels read -- are all-gathered.
 Per step that moves (N-1)/N of 4 + 2 bytes per parameter instead of 2 (N-1)/N of 4, and Adam, whose
 cost does not shrink with the per-rank batch (36 B per parameter), runs on 1/N of the parameters.
-The fp32 master weights and Adam moments stay sharded (each rank's are current on its own shard);
-gather_master() all-gathers the fp32 master weights, e.g. before a snapshot. For two ranks the
-result is bit-identical to the all-reduce schedule (a + b is the same sum either way).
+The fp32 master weights and Adam state stay sharded (each rank's are current on its own shard);
+gather_state() all-gathers the fp32 masters, both Adam moments and the per-parameter step counts,
+and the trainer refuses serialize(optimizer=True) until it has run. For two ranks the result is
+bit-identical to the all-reduce schedule (a + b is the same sum either way).
 
 Batch sharding: strong scaling splits one global batch into contiguous shards (shard_bounds);
 weak scaling gives every rank its own full batch. Both use the same step.
 """
+import ctypes
+
 import torch
 import torch.distributed as dist
 
@@ -57,19 +66,52 @@ def shard(x, rank, world):
     return x[lo:hi]
 
 
+class EngineComm:
+    """An engine data-parallel communicator (tcnn_dp_comm_create, RCCL over xGMI) for the ranks of
+    `group`: rank 0 draws the unique id, torch.distributed broadcasts it (any backend), every rank
+    creates its communicator on its current device."""
+
+    def __init__(self, group=None):
+        from tinycudann import _lib as L
+        self._L = L
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        uid = torch.zeros(128, dtype=torch.uint8)
+        if self.rank == 0:
+            L.check(L.lib().tcnn_dp_unique_id(ctypes.c_void_p(uid.data_ptr())))
+        on_gpu = dist.get_backend(group) == "nccl"
+        t = uid.cuda() if on_gpu else uid
+        dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        uid = t.cpu().contiguous()
+        self.h = L.check_ptr(L.lib().tcnn_dp_comm_create(ctypes.c_void_p(uid.data_ptr()), self.world, self.rank))
+
+    def __del__(self):
+        try:
+            self._L.lib().tcnn_dp_comm_destroy(self.h)
+        except Exception:
+            pass
+
+
 class DataParallelTrainer:
     """Wraps tinycudann.Trainer: training_step = local fwd/bwd, all-reduce (overlapped), Adam."""
 
-    def __init__(self, trainer, group=None, overlap=True, allreduce_dtype="fp32", shard_optimizer=False):
+    def __init__(self, trainer, group=None, overlap=True, allreduce_dtype="fp32", shard_optimizer=False, exchange="torch"):
         assert allreduce_dtype in ("fp32", "fp16")
+        assert exchange in ("torch", "engine")
         assert not (shard_optimizer and allreduce_dtype == "fp16"), "the sharded optimizer exchanges fp32 gradient sums"
+        assert not (exchange == "engine" and allreduce_dtype == "fp16"), "the engine exchange sums fp32 gradients"
         self.trainer = trainer
         self.group = group
         self.overlap = overlap
         self.dtype = allreduce_dtype
         self.shard_optimizer = shard_optimizer
+        self.exchange = exchange
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        if self.world > 1 and shard_optimizer:
+        self.comm = None
+        if self.world > 1 and exchange == "engine":
+            self.comm = EngineComm(group)
+            trainer.set_dp(self.comm, sharded=shard_optimizer)
+        elif self.world > 1 and shard_optimizer:
             self.rank = dist.get_rank(group)
             n = trainer.n_params
             self._per = (n + self.world - 1) // self.world
@@ -113,23 +155,36 @@ class DataParallelTrainer:
             self._wshard[:self._hi - self._lo].copy_(self._w16[self._lo:self._hi])
         dist.all_gather_into_tensor(self._wpad, self._wshard, group=self.group)
         self._w16.copy_(self._wpad[:n])
+        self.trainer._dp_state_partial = True
 
-    def gather_master(self):
-        """All-gather the fp32 master weights (sharded under shard_optimizer) so every rank holds
-        the full vector, e.g. before serialize()."""
+    def _gather(self, v):
+        """all-gather this rank's shard [lo, hi) of the trainer buffer view v into every rank's v"""
+        n = self.trainer.n_params
+        buf = torch.zeros(self._per * self.world, dtype=v.dtype, device=v.device)
+        mine = torch.zeros(self._per, dtype=v.dtype, device=v.device)
+        if self._hi > self._lo:
+            mine[:self._hi - self._lo].copy_(v[self._lo:self._hi])
+        dist.all_gather_into_tensor(buf, mine, group=self.group)
+        v.copy_(buf[:n])
+
+    def gather_state(self):
+        """All-gather the sharded optimizer state -- fp32 master weights, both Adam moments and the
+        per-parameter step counts -- so every rank holds the full vectors, e.g. before
+        serialize(optimizer=True) (which refuses to run until then)."""
         if self.world == 1 or not self.shard_optimizer:
             return
-        n = self.trainer.n_params
-        w32 = self.trainer.params_fp32()
-        buf = torch.zeros(self._per * self.world, dtype=torch.float32, device=w32.device)
-        mine = torch.zeros(self._per, dtype=torch.float32, device=w32.device)
-        if self._hi > self._lo:
-            mine[:self._hi - self._lo].copy_(w32[self._lo:self._hi])
-        dist.all_gather_into_tensor(buf, mine, group=self.group)
-        w32.copy_(buf[:n])
+        if self.exchange == "engine":
+            self.trainer.dp_gather_state()
+            return
+        m1, m2, steps = self.trainer.optimizer_state()
+        for v in (self.trainer.params_fp32(), m1, m2, steps):
+            self._gather(v)
+        self.trainer._dp_state_partial = False
+
+    gather_master = gather_state  # the round-2 name (it gathered only the masters)
 
     def training_step(self, input, target):
-        if self.world == 1:
+        if self.world == 1 or self.exchange == "engine":
             self.trainer.training_step(input, target, run_optimizer=True)
             return
         if self.shard_optimizer:

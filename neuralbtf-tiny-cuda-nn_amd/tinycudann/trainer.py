@@ -90,6 +90,9 @@ class Trainer:
 
     def serialize(self, optimizer=False):
         """Trainer::serialize as the reference's msgpack snapshot bytes (trainer.h:275-288)."""
+        if optimizer and getattr(self, "_dp_state_partial", False):
+            raise L.TcnnError("serialize(optimizer=True): the sharded data-parallel optimizer state is current only on each "
+                              "rank's shard; call DataParallelTrainer.gather_state() first")
         n = ctypes.c_uint64(0)
         L.check(L.lib().tcnn_trainer_serialize(self.h, int(optimizer), None, 0, ctypes.byref(n)))
         buf = ctypes.create_string_buffer(n.value)
@@ -138,6 +141,26 @@ class Trainer:
     def gradients_fp32(self):
         import torch
         return self._view(L.lib().tcnn_trainer_gradients_fp32(self.h), self.n_params, torch.float32)
+
+    def optimizer_state(self):
+        """(first moments fp32, second moments fp32, per-parameter step counts int32) views (adam.h:128-148)"""
+        import torch
+        m1, m2, st = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        L.check(L.lib().tcnn_trainer_optimizer_state(self.h, ctypes.byref(m1), ctypes.byref(m2), ctypes.byref(st)))
+        return (self._view(m1.value, self.n_params, torch.float32), self._view(m2.value, self.n_params, torch.float32),
+                self._view(st.value, self.n_params, torch.int32))
+
+    def set_dp(self, comm, sharded=False):
+        """Attach an engine data-parallel communicator (tinycudann.parallel.EngineComm; None detaches):
+        every training_step(run_optimizer=True) then sums the gradients across the ranks inside the
+        step (tcnn_trainer_set_dp)."""
+        L.check(L.lib().tcnn_trainer_set_dp(self.h, comm.h if comm is not None else None, int(bool(sharded))))
+        self._dp_comm = comm  # the communicator must outlive the attachment
+
+    def dp_gather_state(self, stream=None):
+        """All-gather the sharded optimizer state (fp32 masters, Adam moments, steps) of an attached
+        engine communicator (tcnn_trainer_dp_gather_state), e.g. before serialize(optimizer=True)."""
+        L.check(L.lib().tcnn_trainer_dp_gather_state(self.h, _stream(stream)))
 
 
 def create_from_config(n_input_dims, n_output_dims, config, seed=1337):

@@ -110,6 +110,7 @@ def lib():
         _lib.orc_hfma.restype = ctypes.c_uint16
         _lib.orc_hfma.argtypes = [ctypes.c_uint16] * 3
         _lib.orc_set_mimic.argtypes = [ctypes.c_int]
+        _lib.orc_set_abs_wgrad.argtypes = [ctypes.c_int]
         _lib.orc_act_bwd_output.argtypes = [ctypes.c_uint32, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
     return _lib
 
@@ -379,6 +380,21 @@ def act_code(name):
 def set_mimic(on):
     """reference-mimic fp16 accumulation on / off, process-wide"""
     lib().orc_set_mimic(1 if on else 0)
+
+
+def mlp_wgrad_magnitude(W, IN, NH, OUTP, params16, x16, hidden16, dout16, input_soa=True, activation=1, n_threads=1,
+                        want_dinput=False):
+    """sum_i |delta_i| |a_i| per MLP weight, the deltas propagated through |W| with the forward's
+    activation masks (abs-backprop): the per-element scale of the weight gradient's tolerance
+    (tests/helpers.assert_wgrad_per_element). want_dinput: also the abs-backprop dL/dinput (fp16), the
+    scale of a dL/dinput element's tolerance. Returns wg, or (wg, dinput) with want_dinput."""
+    lib().orc_set_abs_wgrad(1)
+    try:
+        wg, din = mlp_bwd(W, IN, NH, OUTP, params16, x16, hidden16, dout16, input_soa=input_soa, activation=activation,
+                          want_dinput=want_dinput, n_threads=n_threads)
+    finally:
+        lib().orc_set_abs_wgrad(0)
+    return (wg, din) if want_dinput else wg
 
 
 def act_bwd_output(act, out16, g16):

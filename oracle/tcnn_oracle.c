@@ -366,6 +366,18 @@ void orc_grid_fwd(const orc_grid* g, uint32_t B, const float* pos_in, const uint
  * (tests/golden/oracle_render.json). */
 static int g_mimic = 0;
 void orc_set_mimic(int on) { g_mimic = on; }
+/* Magnitude mode of the MLP weight gradient (tests only): orc_mlp_bwd accumulates sum_i |delta_i a_i|
+ * per weight instead of sum_i delta_i a_i (the deltas themselves are propagated as usual). It sizes
+ * the per-element tolerance of a weight gradient: a perturbation of every term by e ulps moves the sum
+ * by at most e 2^-10 times this magnitude. */
+static int g_abs_wgrad = 0;
+void orc_set_abs_wgrad(int on) { g_abs_wgrad = on; }
+#define WTERM(x) (g_abs_wgrad ? fabsf(x) : (x))
+/* magnitude mode also propagates the deltas through |W| (abs-backprop with the same ReLU masks), so
+ * that the magnitude of a delta or of dL/dinput bounds what a one-ulp change of any upstream fp16
+ * delta can move it, cancellation included */
+#define DTERM(w, d) (g_abs_wgrad ? fabsf(w) * fabsf(d) : (w) * (d))
+#define DABS(x) (g_abs_wgrad ? fabsf(x) : (x))
 static inline float hround(float x) { return orc_h2f(orc_f2h(x)); }
 /* fp16 running sum update after k products (chunked), see g_mimic */
 #define MIMIC_STEP(acc, part, k, chunk, K) \
@@ -760,14 +772,14 @@ static void mlp_bwd_sample(const mlp_view* v, uint32_t act, const float* x, cons
 		float* gWo = wgrad + v->off[NH];
 		for (uint32_t o = 0; o < OUTP; ++o) {
 			if (g[o] == 0.0f) continue;
-			for (uint32_t k = 0; k < W; ++k) gWo[(size_t)o * W + k] += g[o] * hl[k];
+			for (uint32_t k = 0; k < W; ++k) gWo[(size_t)o * W + k] += WTERM(g[o] * hl[k]);
 		}
 	}
 	for (uint32_t k = 0; k < W; ++k) {
 		float acc = 0.0f, part = 0.0f;
-		for (uint32_t o = 0; o < OUTP; ++o) { part += Wo[(size_t)o * W + k] * g[o]; MIMIC_STEP(acc, part, o, 16, OUTP); }
+		for (uint32_t o = 0; o < OUTP; ++o) { part += DTERM(Wo[(size_t)o * W + k], g[o]); MIMIC_STEP(acc, part, o, 16, OUTP); }
 		if (!g_mimic) acc = part;
-		d_cur[k] = act_bwd(act, acc, hl[k]);
+		d_cur[k] = DABS(act_bwd(act, acc, hl[k]));
 	}
 	if (deltas) memcpy(deltas + (size_t)(NH - 1) * W, d_cur, sizeof(float) * W);
 	/* hidden layers, from the last to the first hidden matmul */
@@ -779,14 +791,14 @@ static void mlp_bwd_sample(const mlp_view* v, uint32_t act, const float* x, cons
 			for (uint32_t n = 0; n < W; ++n) {
 				float dn = d_cur[n];
 				if (dn == 0.0f) continue;
-				for (uint32_t k = 0; k < W; ++k) gWl[(size_t)n * W + k] += dn * hin[k];
+				for (uint32_t k = 0; k < W; ++k) gWl[(size_t)n * W + k] += WTERM(dn * hin[k]);
 			}
 		}
 		for (uint32_t k = 0; k < W; ++k) {
 			float acc = 0.0f, part = 0.0f;
-			for (uint32_t n = 0; n < W; ++n) { part += Wl[(size_t)n * W + k] * d_cur[n]; MIMIC_STEP(acc, part, n, 16, W); }
+			for (uint32_t n = 0; n < W; ++n) { part += DTERM(Wl[(size_t)n * W + k], d_cur[n]); MIMIC_STEP(acc, part, n, 16, W); }
 			if (!g_mimic) acc = part;
-			d_nxt[k] = act_bwd(act, acc, hin[k]);
+			d_nxt[k] = DABS(act_bwd(act, acc, hin[k]));
 		}
 		float* t = d_cur; d_cur = d_nxt; d_nxt = t;
 		if (deltas) memcpy(deltas + (size_t)(l - 1) * W, d_cur, sizeof(float) * W);
@@ -798,13 +810,13 @@ static void mlp_bwd_sample(const mlp_view* v, uint32_t act, const float* x, cons
 		for (uint32_t n = 0; n < W; ++n) {
 			float dn = d_cur[n];
 			if (dn == 0.0f) continue;
-			for (uint32_t k = 0; k < IN; ++k) gW0[(size_t)n * IN + k] += dn * x[k];
+			for (uint32_t k = 0; k < IN; ++k) gW0[(size_t)n * IN + k] += WTERM(dn * x[k]);
 		}
 	}
 	if (dx) {
 		for (uint32_t k = 0; k < IN; ++k) {
 			float acc = 0.0f, part = 0.0f;
-			for (uint32_t n = 0; n < W; ++n) { part += W0[(size_t)n * IN + k] * d_cur[n]; MIMIC_STEP(acc, part, n, 8, W); }
+			for (uint32_t n = 0; n < W; ++n) { part += DTERM(W0[(size_t)n * IN + k], d_cur[n]); MIMIC_STEP(acc, part, n, 8, W); }
 			if (!g_mimic) acc = part;
 			dx[k] = orc_h2f(orc_f2h(acc));
 		}

@@ -104,6 +104,8 @@ void orc_grid_bwd_bwd(const orc_grid* g, uint32_t B, const float* pos, const uin
 uint32_t orc_mlp_n_params(uint32_t W, uint32_t IN, uint32_t NH, uint32_t OUTP);
 /* reference-mimic fp16 accumulation on (1) / off (0, default): see g_mimic in tcnn_oracle.c */
 void orc_set_mimic(int on);
+/* orc_mlp_bwd's wgrad = sum_i |delta_i a_i| (on) / sum_i delta_i a_i (off, default): tolerance sizing */
+void orc_set_abs_wgrad(int on);
 /* in-place output-activation transfer of dL/dout given the network output (bits 8-15 of act) */
 void orc_act_bwd_output(uint32_t act, size_t n, const uint16_t* out16, uint16_t* g16);
 void orc_mlp_fwd(uint32_t W, uint32_t IN, uint32_t NH, uint32_t OUTP, uint32_t activation,

@@ -81,3 +81,100 @@ def assert_within_fp16_ulps(got, ref, n_ulp=4):
     ulp = float(np.spacing(np.float16(scale)))
     err = float(np.abs(np.asarray(got, np.float64) - np.asarray(ref, np.float64)).max())
     assert err <= n_ulp * ulp, (err, ulp, scale)
+
+
+def assert_wgrad_per_element(got, ref, mag, ulps=8, fp16_out=False, floor_rel=1e-6):
+    """Per-element bound of an MLP weight gradient dW = sum_i delta_i a_i. Between the HIP kernels
+    (fp32 MFMA) and the oracle (fp32 CPU order) a term's fp16 activation or delta can round to the
+    neighbouring fp16 value, so each term may differ by a few fp16 ulps (2^-10 relative):
+    |got - ref| <= ulps * 2^-10 * mag + floor_rel * max|ref| (+ 2^-11 |ref| when got was rounded to
+    fp16), mag = sum_i |delta_i a_i| (oracle.mlp_wgrad_magnitude). The fp32 summation error of either
+    side (K * 2^-24 relative) is far below this."""
+    got, ref, mag = (np.asarray(v, np.float64) for v in (got, ref, mag))
+    bound = ulps * 2.0 ** -10 * mag + floor_rel * np.abs(ref).max()
+    if fp16_out:
+        bound += 2.0 ** -11 * np.abs(ref) + 2.0 ** -25  # fp16 rounding (subnormals: half the smallest step)
+    r = np.abs(got - ref) / bound
+    k = int(np.argmax(r))
+    assert r[k] <= 1.0, (float(r[k]), k, got[k], ref[k], mag[k])
+    return float(r[k])
+
+
+def relu_margin_ok(W, IN, NH, params16, x_rows, tau=2.0 ** -11, check_output=False):
+    """Per sample: True when no hidden pre-activation of the ReLU MLP lies within tau * sum_k |w_k a_k|
+    of zero. At such a boundary fp32-MFMA and CPU summation orders may legitimately take different
+    ReLU branches (a discrete difference no rounding bound covers); per-element gradient checks run on
+    batches of samples clear of it, the aggregate checks on every sample. tau = 2^-11 covers one fp16
+    ulp of difference in any single input term (|w_k| ulp(a_k) <= 2^-11 |w_k a_k|) plus the fp32
+    summation-order noise. check_output (loss-driven steps): also False when the output's fp16 rounding
+    is within 2^-18 sum |w a| of a rounding boundary. x_rows: float [B][IN] (the fp16 encoded input values)."""
+    p = O.h2f(np.asarray(params16, np.uint16)).astype(np.float64)
+    mats, off, k = [], 0, IN
+    for _ in range(NH):
+        mats.append(p[off:off + W * k].reshape(W, k))
+        off += W * k
+        k = W
+    a = np.asarray(x_rows, np.float64)
+    ok = np.ones(a.shape[0], bool)
+    for Wm in mats:
+        z = a @ Wm.T
+        mag = np.abs(a) @ np.abs(Wm).T
+        ok &= np.all(np.abs(z) >= tau * mag, axis=1)
+        a = np.maximum(z, 0.0).astype(np.float16).astype(np.float64)  # the fp16 post-activation
+    if not check_output:
+        return ok
+    # the output's fp16 rounding: both sides must round to the same value, else the loss gradient
+    # 2 (p - t) / (p^2 + 0.01) of a sample with a small error p - t changes by a large factor
+    Wo = p[off:off + 16 * k].reshape(16, k)
+    y, ymag = a @ Wo.T, np.abs(a) @ np.abs(Wo).T
+    eps = 2.0 ** -18 * ymag
+    ok &= np.all((y - eps).astype(np.float16) == (y + eps).astype(np.float16), axis=1)
+    return ok
+
+
+def relu_safe_grid_batch(cfg, params16, B, seed=1337, step=0):
+    """A B-point batch (make_batch order) of samples clear of the ReLU boundaries (relu_margin_ok) for
+    the grid-encoded network of cfg at params16."""
+    W, NH = cfg["network"]["n_neurons"], cfg["network"]["n_hidden_layers"]
+    g = O.grid_cfg(cfg["encoding"], 2)
+    IN = g.n_levels * g.n_features_per_level
+    nm = O.mlp_n_params(W, IN, NH, 16)
+    p16 = np.asarray(params16, np.uint16)
+    pos, tgt = make_batch(4 * B, seed=seed, step=step)
+    enc = O.h2f(O.grid_fwd(g, pos, p16[nm:])).T  # [B][IN]
+    ok = relu_margin_ok(W, IN, NH, p16[:nm], enc, check_output=True)
+    assert ok.sum() >= B, ok.sum()
+    idx = np.nonzero(ok)[0][:B]
+    return np.ascontiguousarray(pos[idx]), np.ascontiguousarray(tgt[idx])
+
+
+def trainer_grad_bounds(cfg, params16, pos, tgt, n_threads=4):
+    """The oracle's intermediates of one training step on (pos, tgt) with parameters params16 (grid
+    encoding + FullyFusedMLP, RelativeL2): returns (mlp magnitude, grid bound) for per-element checks of
+    the trainer's fp32 gradient sums. Grid bound = the grid backward's own bound for the oracle's
+    dL/d(encoding) (oracle.grid_grad_tolerance) + 8 fp16 ulps of every update's abs-backprop magnitude
+    (the GPU's dL/d(encoding) comes from its own MLP backward: an fp16 delta upstream that rounds to
+    its neighbouring value moves it by up to an ulp of that magnitude, cancellation included)."""
+    enc_cfg, net = cfg["encoding"], cfg["network"]
+    W, NH = net["n_neurons"], net["n_hidden_layers"]
+    g = O.grid_cfg(enc_cfg, pos.shape[1])
+    IN = g.n_levels * g.n_features_per_level
+    nm = O.mlp_n_params(W, IN, NH, 16)
+    p16 = np.asarray(params16, np.uint16)
+    enc = O.grid_fwd(g, pos, p16[nm:])
+    out16, hidden = O.mlp_fwd(W, IN, NH, 16, p16[:nm], enc, n_threads=n_threads)
+    _, dout, _ = O.relative_l2(out16, tgt)
+    mag, denc_abs = O.mlp_wgrad_magnitude(W, IN, NH, 16, p16[:nm], enc, hidden, dout, n_threads=n_threads, want_dinput=True)
+    _, denc = O.mlp_bwd(W, IN, NH, 16, p16[:nm], enc, hidden, dout, n_threads=n_threads)
+    ref_grid = O.grid_bwd(g, pos, denc)
+    absum, _ = O.grid_bwd_stats(g, pos, denc_abs)
+    grid_bound = O.grid_grad_tolerance(g, pos, denc, ref_grid) + 8 * 2.0 ** -10 * absum.astype(np.float64)
+    return mag, grid_bound
+
+
+def assert_trainer_grads_per_element(g32, ref32, n_mlp, mag, grid_bound):
+    assert_wgrad_per_element(g32[:n_mlp], ref32[:n_mlp], mag)
+    got, ref = np.asarray(g32[n_mlp:], np.float64), np.asarray(ref32[n_mlp:], np.float64)
+    r = np.abs(got - ref) / (grid_bound + 1e-30)
+    k = int(np.argmax(r))
+    assert r[k] <= 1.0, (float(r[k]), k, got[k], ref[k], grid_bound[k])

@@ -120,6 +120,9 @@ class _FakeShardTrainer(_FakeTrainer):
         self.n_params = n
         self.w16 = torch.zeros(n, dtype=torch.float16)
         self.w32 = torch.zeros(n, dtype=torch.float32)
+        self.m1 = torch.zeros(n, dtype=torch.float32)
+        self.m2 = torch.zeros(n, dtype=torch.float32)
+        self.steps = torch.zeros(n, dtype=torch.int32)
         self.ranges = []
 
     def params(self):
@@ -128,10 +131,16 @@ class _FakeShardTrainer(_FakeTrainer):
     def params_fp32(self):
         return self.w32
 
+    def optimizer_state(self):
+        return self.m1, self.m2, self.steps
+
     def optimizer_step_range(self, lo, hi):
         self.ranges.append((lo, hi))
         self.w32[lo:hi] = self.g[lo:hi] * self.scale
         self.w16[lo:hi] = self.w32[lo:hi].half()
+        self.m1[lo:hi] = self.w32[lo:hi] * 0.1
+        self.m2[lo:hi] = self.w32[lo:hi] * 0.01
+        self.steps[lo:hi] += 1
 
 
 def _sched_worker(rank, world, port, out_q):
@@ -154,8 +163,10 @@ def _sched_worker(rank, world, port, out_q):
     dp = DataParallelTrainer(t, shard_optimizer=True)
     dp.training_step(None, None)
     w16 = t.w16.clone()
-    dp.gather_master()
-    res["zero"] = (w16.float().numpy(), t.w32.numpy(), t.ranges)
+    partial = t._dp_state_partial
+    dp.gather_state()
+    res["zero"] = (w16.float().numpy(), t.w32.numpy(), t.ranges, t.m1.numpy(), t.m2.numpy(), t.steps.numpy(), partial,
+                   t._dp_state_partial)
     x = torch.arange(10 * 3).reshape(10, 3)
     res["shard"] = shard(x, rank, world).numpy()
     out_q.put((rank, res))
@@ -191,11 +202,17 @@ def test_two_rank_exchange_schedule_and_sharding():
         np.testing.assert_array_equal(g16, (h[0] + h[1]).astype(np.float32))
     np.testing.assert_array_equal(np.concatenate([res[0]["shard"], res[1]["shard"]]), np.arange(30).reshape(10, 3))
     # sharded optimizer over 41 parameters (padded to 42): rank 0 updates [0, 21), rank 1 [21, 41);
-    # afterwards every rank holds the whole fp16 vector and, after gather_master, the fp32 one
+    # afterwards every rank holds the whole fp16 vector and, after gather_state, the fp32 one and the Adam state
     idx41 = np.arange(41, dtype=np.float32)
     mean41 = ((idx41 + 1) * np.float32(0.37) + (idx41 + 1) * 2 * np.float32(0.37)) / 2
     for r in range(world):
-        w16, w32, ranges = res[r]["zero"]
+        w16, w32, ranges, m1, m2, steps, partial, partial_after = res[r]["zero"]
         assert ranges == [(0, 21)] if r == 0 else ranges == [(21, 41)]
         np.testing.assert_allclose(w32, mean41, rtol=1e-6)
         np.testing.assert_array_equal(w16, w32.astype(np.float16).astype(np.float32))
+        # gather_state: the Adam moments and step counts of every shard reach every rank, and the
+        # serialize(optimizer=True) guard is lifted
+        np.testing.assert_array_equal(m1, w32 * np.float32(0.1))
+        np.testing.assert_array_equal(m2, w32 * np.float32(0.01))
+        np.testing.assert_array_equal(steps, np.ones(41, np.int32))
+        assert partial and not partial_after

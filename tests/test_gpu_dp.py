@@ -50,7 +50,7 @@ def _worker(rank, world, port, B, q):
             pos_s, tgt_s = make_batch(B, step=s)
             dp.training_step(torch.from_numpy(pos_s[lo:hi]).cuda(), torch.from_numpy(tgt_s[lo:hi]).cuda())
         if gather:
-            dp.gather_master()
+            dp.gather_state()
         torch.cuda.synchronize()
         a = trainer_arrays(tr2)
         return a["w32"], a["w16"]

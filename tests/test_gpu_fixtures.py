@@ -6,9 +6,13 @@ Tolerances:
   * F3 grid forward: bit-exact (same fp16 FMA chain and index math)
   * F4 grid backward: per element, |gpu - ref| <= the fixture's bound (fixed-point step x updates +
     the oracle's fp32 summation error) + fp16 rounding of the output (2^-11 relative)
-  * F5 MLP (Network module on the layer-wise engine, fp32 MFMA accumulation): output within 4 fp16
-    ulp of the output scale; weight gradients (fp16) and dL/dinput rel L2 <= 1e-3 (5e-3 for the
-    5-hidden-layer net, see tests/test_fixtures.py)
+  * F5 MLP (Network module = Identity + FullyFusedMLP: the tile engine's fused inference and training
+    kernels, fp32 MFMA accumulation): output within 4 fp16 ulp of the output scale; weight gradients
+    (fp16) per element within 8 fp16 ulps of the sum of their terms' magnitudes
+    (helpers.assert_wgrad_per_element) and rel L2 <= 1e-3; dL/dinput rel L2 <= 1e-3. The 5-hidden-layer
+    IN = 128 net keeps 5e-3 for the aggregate measures: its gradient moves 2.4e-3 (rel L2) under 1-ulp
+    flips of 1 % of its forward activations (float64 backward passes on either side's activations,
+    tests/test_fixtures.py), which the per-element bound already covers term by term
   * F7 20 training steps of config_hash at B=4096: per-step loss within 3e-2 relative, final
     parameter norms within 1e-2 (trajectories of fp32-MFMA vs CPU summation orders)
 """
@@ -20,7 +24,8 @@ import sys
 import numpy as np
 import pytest
 
-from helpers import CONFIG_HASH, GOLD, make_batch, trainer_arrays
+from helpers import CONFIG_HASH, GOLD, assert_wgrad_per_element, make_batch, relu_margin_ok, trainer_arrays
+from oracle import oracle as O
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "tools"))
@@ -124,6 +129,29 @@ def test_f5_mlp_module(torch_mod, shape):
     wg = grad.float().cpu().numpy().astype(np.float64)
     ew = np.linalg.norm(wg - f["wgrad"]) / np.linalg.norm(f["wgrad"])
     assert ew <= lim, ew
+    # per element against the live oracle, the fixture's weights on 512 fresh inputs clear of the ReLU
+    # boundaries (helpers.relu_margin_ok)
+    rng = np.random.default_rng(W + H + IN)
+    xc = O.f2h(rng.uniform(-1.0, 1.0, (8192, IN)).astype(np.float32))
+    dc = O.f2h(rng.uniform(-1.0, 1.0, (8192, 16)).astype(np.float32))
+    idx = np.nonzero(relu_margin_ok(W, IN, H, params, O.h2f(xc)))[0][:512]
+    assert idx.size == 512, idx.size
+    xs, ds = np.ascontiguousarray(xc[idx]), np.ascontiguousarray(dc[idx])
+    m = L.check_ptr(lib.tcnn_create_network(IN, 16, json.dumps(net).encode()))
+    Bs = idx.size
+    xin = torch.from_numpy(xs.view(np.float16).astype(np.float32)).cuda()
+    out = torch.empty(Bs, 16, dtype=torch.float16, device="cuda")
+    ctx = L.check_ptr(lib.tcnn_module_forward(m, None, Bs, _vp(xin), _vp(out), _vp(p16), 0))
+    d_d = torch.from_numpy(ds.view(np.float16)).cuda()
+    grad = torch.empty(n, dtype=torch.float16, device="cuda")
+    L.check(lib.tcnn_module_backward(m, None, ctx, Bs, None, _vp(d_d), _vp(grad), _vp(xin), _vp(out), _vp(p16)))
+    torch.cuda.synchronize()
+    lib.tcnn_context_destroy(ctx)
+    lib.tcnn_module_destroy(m)
+    _, hidden = O.mlp_fwd(W, IN, H, 16, params, xs, input_soa=False)
+    ref, _ = O.mlp_bwd(W, IN, H, 16, params, xs, hidden, ds, input_soa=False, want_dinput=False)
+    mag = O.mlp_wgrad_magnitude(W, IN, H, 16, params, xs, hidden, ds, input_soa=False)
+    assert_wgrad_per_element(grad.float().cpu().numpy(), ref, mag, fp16_out=True)
     rdx = f["dinput"].view(np.float16).astype(np.float64)
     ed = np.linalg.norm(dx.cpu().numpy() - rdx) / np.linalg.norm(rdx)
     assert ed <= lim, ed

@@ -51,8 +51,21 @@ def test_graph_replay_bit_identical(torch_mod):
     a, b = trainer_arrays(eager), trainer_arrays(graph)
     for k in ("w32", "w16", "g16"):
         assert np.array_equal(a[k], b[k]), k
+    for name, x, y in zip(("m1", "m2", "steps"), eager.optimizer_state(), graph.optimizer_state()):
+        assert torch.equal(x, y), name  # the Adam moments and per-parameter step counts too
     assert losses["eager"] == losses["graph"]
     captures, replays = graph.graph_stats()
     # captures: first B (after the weight-packing first step), the learning-rate change, the new B
     assert captures >= 3 and replays >= 4, (captures, replays)
     assert graph.optimizer_step_count == eager.optimizer_step_count == 10
+
+
+def test_update_hyperparams_rejects_loss_type_change(torch_mod):
+    """The loss type is fixed at construction (the reference's Loss::update_hyperparams holds no
+    hyperparameters): a request to change it fails loudly instead of being ignored."""
+    from tinycudann import _lib as L
+    from tinycudann import Trainer
+    t = Trainer(2, 3, CONFIG_HASH, seed=1337)
+    L.check(L.lib().tcnn_trainer_update_hyperparams(t.h, json.dumps({"loss": {"otype": "RelativeL2"}}).encode()))
+    with pytest.raises(RuntimeError, match="loss type is fixed"):
+        L.check(L.lib().tcnn_trainer_update_hyperparams(t.h, json.dumps({"loss": {"otype": "L2"}}).encode()))

@@ -242,10 +242,19 @@ def test_trainer_log2t19_gradients(torch_mod, B):
     # network gradients: fp32 MFMA vs fp32 CPU order -> relative L2 (as test_gpu_parity)
     from helpers import rel_err
     assert rel_err(a["g32"][:nm], om.grad32[:nm]) <= 1e-3
-    # grid gradients: the per-element bound covers the grid backward for a given dL/d(encoding)
-    # (Module tests above); here dL/d(encoding) itself comes from each side's MLP backward (fp32
-    # MFMA vs fp32 CPU order, then fp16), so the comparison is relative L2 like test_gpu_parity
     assert rel_err(a["g32"][nm:], om.grad32[nm:]) <= 1e-3
+    # per element: dL/d(encoding) comes from each side's MLP backward, so the grid bound adds 8 fp16
+    # ulps of every update to the grid backward's own bound (helpers.trainer_grad_bounds)
+    # (on a batch clear of the ReLU boundaries, helpers.relu_margin_ok)
+    from helpers import assert_trainer_grads_per_element, relu_safe_grid_batch, trainer_grad_bounds
+    t2 = _t19_trainer(torch)
+    om2 = O.OracleModel(CONFIG_T19, 2, 3, seed=1337)
+    pos, tgt = relu_safe_grid_batch(CONFIG_T19, om2.w16, B)
+    t2.training_step(torch.from_numpy(pos).cuda(), torch.from_numpy(tgt).cuda(), run_optimizer=False)
+    om2.train_step(pos, tgt, run_optimizer=False)
+    a2 = trainer_arrays(t2)
+    mag, gb = trainer_grad_bounds(CONFIG_T19, a2["w16"], pos, tgt)
+    assert_trainer_grads_per_element(a2["g32"], om2.grad32, nm, mag, gb)
 
 
 def test_trainer_log2t19_adam_step(torch_mod):

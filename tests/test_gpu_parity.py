@@ -12,7 +12,8 @@ import json
 import numpy as np
 import pytest
 
-from helpers import CONFIG_HASH, assert_within_fp16_ulps, make_batch, rel_err, trainer_arrays
+from helpers import (CONFIG_HASH, assert_trainer_grads_per_element, assert_wgrad_per_element, assert_within_fp16_ulps, make_batch,
+                     rel_err, relu_margin_ok, relu_safe_grid_batch, trainer_arrays, trainer_grad_bounds)
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -77,6 +78,17 @@ def test_fused_step_gradients_and_loss(torch_mod, B):
     e_grid = rel_err(a["g32"][nm:], om.grad32[nm:])
     assert e_mlp <= 1e-3, e_mlp
     assert e_grid <= 1e-3, e_grid
+
+    # per element, on a batch clear of the ReLU boundaries (helpers.relu_margin_ok): every term of
+    # each sum within 8 fp16 ulps (helpers.trainer_grad_bounds)
+    t2 = Trainer(2, 3, CONFIG_HASH, seed=1337)
+    om2 = O.OracleModel(CONFIG_HASH, 2, 3, seed=1337)
+    pos, tgt = relu_safe_grid_batch(CONFIG_HASH, om2.w16, B)
+    t2.training_step(torch.from_numpy(pos).cuda(), torch.from_numpy(tgt).cuda(), run_optimizer=False)
+    om2.train_step(pos, tgt, run_optimizer=False)
+    a2 = trainer_arrays(t2)
+    mag, gb = trainer_grad_bounds(CONFIG_HASH, a2["w16"], pos, tgt)
+    assert_trainer_grads_per_element(a2["g32"], om2.grad32, nm, mag, gb)
 
 
 def test_fused_step_positions_outside_unit_square(torch_mod):
@@ -169,7 +181,14 @@ def test_module_backward_matches_oracle(torch_mod):
     L.check(lib.tcnn_module_initialize_params(m, 42, ctypes.c_void_p(p32.data_ptr()), 1.0))
     p16 = p32.half().contiguous()
     B = 1024
-    pos, _ = make_batch(B, seed=11)
+    pos, _ = make_batch(4 * B, seed=11)
+    # a batch clear of the ReLU boundaries, so the per-element bounds below apply (helpers.relu_margin_ok)
+    g0 = O.grid_cfg(enc, 2)
+    p0 = p16.cpu().numpy().view(np.uint16)
+    nm0 = O.mlp_n_params(64, 32, 2, 16)
+    ok = relu_margin_ok(64, 32, 2, p0[:nm0], O.h2f(O.grid_fwd(g0, pos, p0[nm0:])).T)
+    pos = np.ascontiguousarray(pos[np.nonzero(ok)[0][:B]])
+    assert pos.shape[0] == B
     pos_d = torch.from_numpy(pos).cuda()
     out = torch.empty(B, 16, dtype=torch.float16, device="cuda")
     ctx = L.check_ptr(lib.tcnn_module_forward(m, None, B, ctypes.c_void_p(pos_d.data_ptr()), ctypes.c_void_p(out.data_ptr()),
@@ -189,11 +208,21 @@ def test_module_backward_matches_oracle(torch_mod):
     encv = O.grid_fwd(g, pos, params16[nm:])
     outr, hidden = O.mlp_fwd(64, 32, 2, 16, params16[:nm], encv)
     assert_within_fp16_ulps(O.h2f(out.cpu().numpy().view(np.uint16)), O.h2f(outr))
-    wg, denc = O.mlp_bwd(64, 32, 2, 16, params16[:nm], encv, hidden, dout16.cpu().numpy().view(np.uint16))
+    d16 = dout16.cpu().numpy().view(np.uint16)
+    wg, denc = O.mlp_bwd(64, 32, 2, 16, params16[:nm], encv, hidden, d16)
     gg = O.grid_bwd(g, pos, denc)
     ref = np.concatenate([wg, gg])
     got = grad.float().cpu().numpy()
-    assert rel_err(got, ref) <= 1e-3, rel_err(got, ref)
+    assert rel_err(got, ref) <= 1e-3, (rel_err(got, ref), int(np.isnan(got[:nm]).sum()), int(np.isnan(got[nm:]).sum()),
+                                       int(np.isnan(ref).sum()), np.nonzero(np.isnan(got))[0][:8])
+    # per element: network weights by the term-magnitude bound, grid by its own bound (fp16 outputs)
+    assert_wgrad_per_element(got[:nm], wg, O.mlp_wgrad_magnitude(64, 32, 2, 16, params16[:nm], encv, hidden, d16), fp16_out=True)
+    _, denc_abs = O.mlp_wgrad_magnitude(64, 32, 2, 16, params16[:nm], encv, hidden, d16, want_dinput=True)
+    absum, _ = O.grid_bwd_stats(g, pos, denc_abs)  # abs-backprop magnitude of every update (helpers.trainer_grad_bounds)
+    gbound = O.grid_grad_tolerance(g, pos, denc, gg) + 8 * 2.0 ** -10 * absum + 2.0 ** -11 * np.abs(gg) + 2.0 ** -25
+    r = np.abs(got[nm:] - gg) / gbound
+    k = int(np.argmax(r))
+    assert r[k] <= 1.0, (float(r[k]), k, got[nm + k], gg[k], gbound[k])
     lib.tcnn_context_destroy(ctx)
     lib.tcnn_module_destroy(m)
 
