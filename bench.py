@@ -122,6 +122,36 @@ def workload_tag(cfg, B):
             f"{cfg.get('optimizer', {}).get('otype', 'Adam')}, B={bs}")
 
 
+GRID_BWD_SLOTS = 32768  # int32 accumulators of one LDS item (grid_bwd_lds.h: 128 KiB)
+
+
+def grid_binned_params(cfg, D=2):
+    """Grid parameters of the levels the engine's binned backward takes (runtime.cpp: from the first
+    level whose one feature exceeds an LDS item on; their Adam runs inside k_grid_acc). Level sizes
+    as GridEncodingTemplated (grid.h:668-730) in float32."""
+    import numpy as np
+    e = cfg.get("encoding", {})
+    if e.get("otype", "").lower() not in ("hashgrid", "grid", "densegrid", "tiledgrid"):
+        return 0
+    L, F = e.get("n_levels", 16), e.get("n_features_per_level", 2)
+    log2T, base = e.get("log2_hashmap_size", 19), e.get("base_resolution", 16)
+    gtype = e.get("type", "Hash" if e["otype"].lower() in ("hashgrid", "grid") else ("Tiled" if e["otype"].lower() == "tiledgrid" else "Dense"))
+    ls = np.log2(np.float32(e.get("per_level_scale", 2.0)))
+    sizes = []
+    for l in range(L):
+        scale = np.float32(np.exp2(np.float32(l) * ls)) * np.float32(base) - np.float32(1.0)
+        res = int(np.ceil(scale)) + 1
+        n = min(res ** D, 0xffffffff // 2)
+        n = (n + 7) // 8 * 8
+        if gtype.lower() == "hash":
+            n = min(n, 1 << log2T)
+        elif gtype.lower() == "tiled":
+            n = min(n, base ** D)
+        sizes.append(n)
+    first = next((l for l in range(L) if sizes[l] > GRID_BWD_SLOTS), L)
+    return sum(sizes[first:]) * F
+
+
 def pmc_traffic(kernel, tag):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary measured on the SAME
     workload (profiles/*_pmc_traffic*.json whose "workload" equals `tag`; files without the key
@@ -308,10 +338,22 @@ def main():
         else:
             # the grid backward launch also carries the network-gradient reduction + Adam on the
             # network parameters (16 extra workgroups); their bytes are < 1 % of the grid's
-            achieved = GRID_BWD_BYTES_PER_SAMPLE * B / (t_gbwd * 1e-3) / 1e9
-            res["roofline"] = {"kernel": "k_grid_bwd_lds", "bound": "hbm", "achieved": achieved,
-                               "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
-                               "traffic": pmc_traffic("k_grid_bwd_lds", tag)}
+            nb = grid_binned_params(cfg)
+            if nb == 0:
+                achieved = GRID_BWD_BYTES_PER_SAMPLE * B / (t_gbwd * 1e-3) / 1e9
+                res["roofline"] = {"kernel": "k_grid_bwd_lds", "bound": "hbm", "achieved": achieved,
+                                   "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
+                                   "traffic": pmc_traffic("k_grid_bwd_lds", tag)}
+            else:
+                # binned levels (e.g. log2T 19): the phase is k_grid_bwd_lds + k_grid_bin + k_grid_acc,
+                # and k_grid_acc applies Adam to the binned parameters: algorithmic bytes = the grid
+                # backward's per sample + Adam's per binned parameter; traffic = the three kernels'
+                achieved = (GRID_BWD_BYTES_PER_SAMPLE * B + ADAM_BYTES_PER_PARAM * nb) / (t_gbwd * 1e-3) / 1e9
+                parts = [pmc_traffic(k, tag) for k in ("k_grid_bwd_lds", "k_grid_bin", "k_grid_acc")]
+                res["roofline"] = {"kernel": "grid backward phase: k_grid_bwd_lds + k_grid_bin + k_grid_acc (incl. Adam of "
+                                             f"{nb} binned parameters)", "bound": "hbm", "achieved": achieved,
+                                   "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
+                                   "traffic": sum(parts) if all(p is not None for p in parts) else None}
     if world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(cfg)
     print(json.dumps(res))
