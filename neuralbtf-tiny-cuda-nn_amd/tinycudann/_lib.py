@@ -7,7 +7,8 @@ import ctypes
 import os
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_PKG, "lib", "libtcnn_mi355x.so")
+# TCNN_LIB_PATH: another build of the same library (A/B timing of two builds in one job)
+LIB_PATH = os.environ.get("TCNN_LIB_PATH") or os.path.join(_PKG, "lib", "libtcnn_mi355x.so")
 
 _lib = None
 
