@@ -272,10 +272,7 @@ __device__ __forceinline__ void grid_bwd_mlp_tail(const GridBwdEpilogue& ep, uin
 	if (g == 0) {
 		__syncthreads();
 		const float l = block_sum_fixed(ep.lpart, ep.n_wparts, lds);
-		if (threadIdx.x == 0) {
-			*ep.d_loss = l;
-			if (ep.apply_adam && ep.factor_out) *ep.factor_out = adam_bias_factor(ep.adam_mlp, ep.factor_step);
-		}
+		if (threadIdx.x == 0) *ep.d_loss = l;
 	}
 }
 

@@ -118,8 +118,6 @@ struct GridBwdEpilogue {
 	uint32_t n_wparts, n_mlp;
 	const float* lpart;      // loss partials [n_wparts]
 	float* d_loss;
-	float* factor_out;       // receives the bias-correction factor of step adam_mlp's current step
-	uint32_t factor_step;
 	// fused weight image (mlp_fused.h FusedLayout): W0 rows of RSI halves at 0, hidden rows of RSW
 	// at oWh, output rows of RSW at oWo
 	_Float16* wimage;
@@ -233,8 +231,6 @@ void launch_mlp_tile_infer(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH,
 
 // generate_random_uniform<float> (random.h:57-70) from pcg32 {state, inc} (not advanced here)
 void launch_generate_uniform(hipStream_t st, uint64_t n, uint64_t state, uint64_t inc, float* out, float lo, float hi);
-// factor_table[t - 1] = adam_bias_factor(a, t) for t in (lo, hi]
-void launch_fill_bias_factors(hipStream_t st, const AdamArgs& a, float* table, uint32_t lo, uint32_t hi);
 void launch_adam(hipStream_t st, const AdamArgs& a, float* w32, void* w16, const float* grad32, void* grad16,
                  float* m1, float* m2, uint32_t* steps);
 

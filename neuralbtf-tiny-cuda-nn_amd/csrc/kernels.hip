@@ -143,16 +143,6 @@ void launch_generate_uniform(hipStream_t st, uint64_t n, uint64_t state, uint64_
 	TCNN_HIP_CHECK(hipGetLastError());
 }
 
-__global__ __launch_bounds__(256) void k_fill_bias_factors(const AdamArgs a, float* __restrict__ table, uint32_t lo, uint32_t hi) {
-	const uint32_t t = lo + 1 + blockIdx.x * blockDim.x + threadIdx.x;
-	if (t <= hi) table[t - 1] = adam_bias_factor(a, t);
-}
-
-void launch_fill_bias_factors(hipStream_t st, const AdamArgs& a, float* table, uint32_t lo, uint32_t hi) {
-	if (hi <= lo) return;
-	hipLaunchKernelGGL(k_fill_bias_factors, dim3(div_round_up(hi - lo, 256)), dim3(256), 0, st, a, table, lo, hi);
-	TCNN_HIP_CHECK(hipGetLastError());
-}
 
 // reference optimizers/adam.h:47-119 (per-parameter update in adam_device.h)
 __global__ __launch_bounds__(256) void k_adam(const AdamArgs a, float* __restrict__ w32, _Float16* __restrict__ w16,

@@ -921,21 +921,15 @@ void TrainerHost::training_step_overlapped(hipStream_t st, uint32_t B, const flo
 	GridBwdEpilogue ep{};
 	ep.enabled = 1;
 	ep.apply_adam = run_optimizer ? 1 : 0;
-	// bias factors of earlier steps from the table; this step's entry is written by the launch's
-	// workgroup 0 (grid_bwd_mlp_tail) for the Adam launches that follow
-	ep.adam_mlp = run_optimizer ? adam_args_table(st, adam_step - 1, adam_step) : adam_args();
+	ep.adam_mlp = run_optimizer ? adam_args_table(st, adam_step) : adam_args();
 	ep.adam_mlp.n = (uint32_t)n_mlp;
 	ep.buf = AdamBuffers{w32.as<float>(), w16.as<_Float16>(), g32.as<float>(), g16.as<_Float16>(), m1.as<float>(), m2.as<float>(),
 	                     steps.as<uint32_t>()};
 	ep.n_mlp_groups = MLP_TAIL_GROUPS;
 	ep.n_mlp = (uint32_t)n_mlp;
 	ep.d_loss = d_loss.as<float>();
-	// this step's bias factor, unless the table already holds it (always, under graph replay)
-	ep.factor_out = (run_optimizer && ftable_valid < adam_step) ? d_ftable.as<float>() + (adam_step - 1) : nullptr;
-	ep.factor_step = ep.factor_out ? adam_step : 0u;
 	TCNN_CHECK(n_mlp % 4 == 0, "network parameter count must be a multiple of 4");
 	m.grid_backward(st, ws, B, input, &ep);
-	if (run_optimizer) ftable_valid = std::max(ftable_valid, adam_step);
 	GridEncodingHost& g = *m.grid;
 	if (run_optimizer) {
 		// binned levels: Adam applied by the accumulate pass; LDS levels: Adam summing their slabs
@@ -1194,11 +1188,18 @@ AdamArgs TrainerHost::adam_args_table(hipStream_t st, uint32_t upto, uint32_t re
 		d_ftable.reserve((size_t)ftable_cap * 4);
 		ftable_valid = 0;
 	}
-	if (upto > ftable_valid) {
-		// the factors depend only on t and the betas: fill 1024 steps ahead, so the fill kernel runs
-		// once per 1024 steps instead of once per step
-		const uint32_t ahead = std::min(ftable_cap, (upto + 1023u) / 1024u * 1024u);
-		launch_fill_bias_factors(st, a, d_ftable.as<float>(), ftable_valid, ahead);
+	if (std::max(upto, reserve) > ftable_valid) {
+		// the factors depend only on t and the betas, sqrt(1 - b2^t) / (1 - b1^t) (adam.h:110-113),
+		// computed 1024 steps ahead on the host with the C library's powf / sqrtf -- one libm for
+		// every step, the same one the CPU restatement uses, so the Adam update is bit-exact against it
+		// (a device powf differs from glibc's in the last bit for some t)
+		const uint32_t ahead = std::min(ftable_cap, (std::max(upto, reserve) + 1023u) / 1024u * 1024u);
+		h_ftable.resize(ahead);
+		for (uint32_t t = ftable_valid + 1; t <= ahead; ++t)
+			h_ftable[t - 1] = std::sqrt(1.0f - std::pow(adam.beta2, (float)t)) / (1.0f - std::pow(adam.beta1, (float)t));
+		TCNN_HIP_CHECK(hipMemcpyAsync(d_ftable.as<float>() + ftable_valid, h_ftable.data() + ftable_valid, (size_t)(ahead - ftable_valid) * 4,
+		                              hipMemcpyHostToDevice, st));
+		TCNN_HIP_CHECK(hipStreamSynchronize(st));  // h_ftable may grow (reallocate) before the next fill
 		ftable_valid = ahead;
 	}
 	a.factor_table = d_ftable.as<float>();

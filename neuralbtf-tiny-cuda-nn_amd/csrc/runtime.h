@@ -298,9 +298,10 @@ struct TrainerHost {
 	// Adam bias-correction factors of steps 1 .. ftable_valid (AdamArgs::factor_table), for the betas
 	// they were computed with; grown by doubling
 	DevBuf d_ftable;
+	std::vector<float> h_ftable;  // host staging of the table (computed on the host, see adam_args_table)
 	uint32_t ftable_cap = 0, ftable_valid = 0;
 	float ftable_b1 = 0.0f, ftable_b2 = 0.0f;
-	// makes the table cover steps 1 .. upto (launching the fill kernel for what is missing) and
+	// makes the table cover steps 1 .. upto (computing what is missing, 1024 steps ahead) and
 	// returns args with factor_table / factor_n set
 	// (capacity for at least `reserve` entries)
 	AdamArgs adam_args_table(hipStream_t st, uint32_t upto, uint32_t reserve = 0);

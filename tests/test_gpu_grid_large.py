@@ -270,9 +270,8 @@ def test_trainer_log2t19_adam_step(torch_mod):
     m2 = np.zeros_like(m1)
     steps = np.zeros(om.n_params, np.uint32)
     O.adam_step(om.m.adam, om.n_mlp_params, 128.0, 1, w32, w16, a["g16"], m1, m2, steps)
-    assert np.mean(a["w32"] == w32) >= 0.999
-    from helpers import rel_err
-    assert rel_err(a["w32"], w32) <= 1e-5
+    np.testing.assert_array_equal(a["w32"], w32)  # bit for bit (the binned levels' Adam runs in k_grid_acc)
+    np.testing.assert_array_equal(a["w16"], w16)
 
 
 def test_trainer_log2t19_sequential_equals_overlapped(torch_mod):
