@@ -107,7 +107,14 @@ public:
 	// trainer.h:213-224
 	void update_hyperparams(const json& params) {
 		if (params.count("optimizer")) m_optimizer->update_hyperparams(params["optimizer"]);
-		if (params.count("loss")) m_loss->update_hyperparams(params["loss"]);
+		if (params.count("loss")) {
+			// the engine's loss is fixed at construction: it refuses an otype change instead of
+			// silently training on with the old loss (tcnn_trainer_update_hyperparams)
+			json l = json::object();
+			l["loss"] = params["loss"];
+			detail::check_rc(tcnn_trainer_update_hyperparams(m_h, l.dump().c_str()));
+			m_loss->update_hyperparams(params["loss"]);
+		}
 	}
 	json hyperparams() const { return json::parse(tcnn_trainer_hyperparams(m_h)); }
 

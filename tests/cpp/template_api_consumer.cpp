@@ -137,6 +137,15 @@ int main(int argc, char** argv) {
 		EXPECT(std::fabs(model.optimizer->learning_rate() - 1e-3f) < 1e-9f);
 		model.trainer->update_hyperparams({{"optimizer", {{"learning_rate", 2e-3f}}}});
 		EXPECT(std::fabs(model.trainer->hyperparams()["optimizer"]["learning_rate"].get<float>() - 2e-3f) < 1e-9f);
+		// the loss type is fixed at construction: a change is refused, not silently ignored
+		model.trainer->update_hyperparams({{"loss", {{"otype", "RelativeL2"}}}});
+		bool refused = false;
+		try {
+			model.trainer->update_hyperparams({{"loss", {{"otype", "L2"}}}});
+		} catch (const std::runtime_error&) {
+			refused = true;
+		}
+		EXPECT(refused);
 
 		// parameters: set_params_full_precision round trip, snapshot round trip
 		std::vector<float> p(model.trainer->n_params());

@@ -53,12 +53,12 @@ def _worker(rank, world, port, B, q):
             dp.gather_state()
         torch.cuda.synchronize()
         a = trainer_arrays(tr2)
-        return a["w32"], a["w16"]
-    w_over = run()[0]                         # two-part step, network all-reduce overlapping the grid backward
+        return a["w32"], a["w16"], bytes(tr2.serialize(optimizer=True))
+    w_over, h_over, snap_over = run()         # two-part step, network all-reduce overlapping the grid backward
     w_plain = run(overlap=False)[0]           # whole backward, then the all-reduce
     w_half = run(allreduce_dtype="fp16")[0]   # pre-divided fp16 exchange
-    w_shard, h_shard = run(gather=True, shard_optimizer=True)  # reduce-scatter, Adam on 1/N, all-gather
-    q.put((rank, g_avg, w_over, w_plain, w_half, w_shard, h_shard, run()[1]))
+    w_shard, h_shard, snap_shard = run(gather=True, shard_optimizer=True)  # reduce-scatter, Adam on 1/N, all-gather
+    q.put((rank, g_avg, w_over, w_plain, w_half, w_shard, h_shard, h_over, snap_over, snap_shard))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -90,6 +90,10 @@ def test_two_rank_gpu_allreduce_matches_full_batch():
     for r in range(world):
         np.testing.assert_array_equal(res[r][6], res[r][7])
         np.testing.assert_array_equal(res[r][5], res[0][2])
+        # the snapshot with optimizer state after gather_state (Adam moments and step counts of every
+        # shard) is byte-identical to the replicated schedule's (a snapshot of a sharded
+        # trainer must not carry partial moments)
+        assert res[r][9] == res[r][8]
     from tinycudann import Trainer
     pos, tgt = make_batch(B)
     t = Trainer(2, 3, CONFIG_HASH, seed=1337)
