@@ -13,10 +13,11 @@ namespace tcnn_amd {
 // fused train step
 // =============================================================================================
 
+// (W64 with 3 hidden layers is not here: its dW accumulators spilled 126-216 registers at 256 and
+// it trained 1.45x slower than on the tile engine, profiles/r03_engine_choice_ab.json)
 #define TCNN_FUSED_SHAPES(X) \
 	X(64, 32, 2)             \
 	X(64, 32, 1)             \
-	X(64, 32, 3)             \
 	X(32, 32, 2)             \
 	X(32, 32, 1)
 

@@ -515,6 +515,7 @@ NetworkHost::NetworkHost(uint32_t n_in, uint32_t n_out, const json& e, const jso
 bool NetworkHost::fused_ok() const {
 	// CutlassMLP / "MLP" run on the layer-wise engine (the reference's separate GEMM-per-layer network)
 	const bool ff = ieq(mlp.otype, "FullyFusedMLP") || ieq(mlp.otype, "MegakernelMLP");
+	if (std::getenv("TCNN_NO_FUSED_GRID")) return false;  // A/B switch: the tile engine instead
 	return ff && grid && grid->n_to_pad == 0 && !grid->opts().active && mlp.output_activation == 0 &&
 	       (mlp.activation == ACT_NONE || mlp.activation == ACT_RELU) &&
 	       fused_train_supported(mlp.width, mlp.n_input, mlp.n_hidden_layers, grid->desc.n_pos_dims,

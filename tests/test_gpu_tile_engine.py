@@ -77,12 +77,14 @@ SMALL = {
     "oneblob16_w32_h3": _cfg({"otype": "OneBlob", "n_bins": 16}, 32, 3),
     "oneblob32_w32_h5": _cfg({"otype": "OneBlob", "n_bins": 32}, 32, 5),
     "hashgrid_w16_h2": _cfg(GRID, 16, 2),
+    # grid + W64/H3 trains on the tile engine since r03 (the register kernel spilled at H3)
+    "hashgrid_w64_h3": _cfg(GRID, 64, 3),
 }
 
 
 @pytest.mark.parametrize("name", list(SMALL))
 def test_small_width_training_step_matches_oracle(torch_mod, name):
-    """W16 (zero-padded to the W32 kernel) and W32 FullyFusedMLP on the fused tile engine."""
+    """W16 (zero-padded to the W32 kernel), W32 and grid + W64/H3 FullyFusedMLP on the fused tile engine."""
     torch = torch_mod
     from tinycudann import Trainer
     cfg = SMALL[name]
