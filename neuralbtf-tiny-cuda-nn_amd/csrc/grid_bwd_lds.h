@@ -264,7 +264,7 @@ __device__ __forceinline__ void grid_bwd_mlp_tail(const GridBwdEpilogue& ep, uin
 				o = ep.oWh + (k / ep.W) * ep.RSW + k % ep.W;  // rows of all hidden matrices are consecutive
 			} else {
 				const uint32_t k = i - nW0 - nWh;
-				o = ep.oWo + (k / ep.W) * ep.RSW + k % ep.W;
+				o = ep.oWo + (4 * ((k / ep.W) & 3) + (k / ep.W) / 4) * ep.RSW + k % ep.W;  // out_row (mlp_fused.h)
 			}
 			ep.wimage[o] = h;
 		}

@@ -211,19 +211,46 @@ __device__ __forceinline__ h2 encode_level_f2_inrange(const uint32_t* __restrict
 #pragma unroll
 	for (uint32_t d = 0; d < D; ++d) pos_fract(x[d], li.scale, Interp::Linear, pos[d], pg[d]);
 	constexpr uint32_t NC = 1u << D;
+	// grid_index_inrange per corner, with everything that does not depend on the corner hoisted to
+	// the level: per dimension the hash term pg*P and the dense term pg*res^d for both corner
+	// offsets ((pg + 1) * k = pg * k + k, also modulo 2^32). Under GridEncodingHost::inrange_index_ok
+	// a level whose index is used densely has res^D <= size (the stride loop never breaks), and its
+	// corner indices stay below 2 * size. The hashed / dense choice is per lane (lanes hold different
+	// levels), so it is a bit select on an opaque mask: written as a C select, the compiler sank the
+	// two index computations into divergent branches (exec-mask regions around every corner), which
+	// also kept it from issuing one level's gathers before the previous level's FMA chain.
+	uint32_t stride = 1;
+	bool brk = false;
+	uint32_t th[D][2], td[D][2];
+#pragma unroll
+	for (uint32_t d = 0; d < D; ++d) {
+		th[d][0] = pg[d] * hash_prime<H>(d);
+		th[d][1] = th[d][0] + hash_prime<H>(d);
+		td[d][0] = pg[d] * stride;
+		td[d][1] = td[d][0] + stride;
+		brk = brk || stride > li.size;  // the reference's stride loop (common_device.h:691-697)
+		stride = brk ? stride : stride * li.res;
+	}
+	uint32_t m = (hash_grid && li.size < stride) ? 0xffffffffu : 0u;
+	asm("" : "+v"(m));
+	const uint32_t hmask = li.size - 1, obytes = li.offset << 2;
 	uint32_t v[NC];
 	_Float16 w16[NC];
 #pragma unroll
 	for (uint32_t c = 0; c < NC; ++c) {
 		float w = 1.0f;
-		uint32_t local[D];
+		uint32_t h = 0, dn = 0;
 #pragma unroll
 		for (uint32_t d = 0; d < D; ++d) {
-			if ((c & (1u << d)) == 0) { w *= 1.0f - pos[d]; local[d] = pg[d]; }
-			else { w *= pos[d]; local[d] = pg[d] + 1; }
+			const uint32_t b = (c >> d) & 1u;
+			w *= b ? pos[d] : 1.0f - pos[d];
+			h ^= th[d][b];
+			dn += td[d][b];
 		}
+		const uint32_t dm = __builtin_elementwise_min(dn, dn - li.size);  // dn % size for dn < 2 size
+		const uint32_t idx = ((h & hmask) & m) | (dm & ~m);
 		w16[c] = (_Float16)w;  // as encode_level_f2
-		v[c] = table_u32[li.offset + grid_index_inrange<D, H>(hash_grid, li.size, li.res, local)];
+		v[c] = *(const uint32_t*)((const char*)table_u32 + (obytes + (idx << 2)));
 	}
 	h2 r = {(_Float16)0.0f, (_Float16)0.0f};
 #pragma unroll

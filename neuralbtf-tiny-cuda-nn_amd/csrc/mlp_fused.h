@@ -33,29 +33,57 @@ __device__ __forceinline__ f4 mfma16(h8 a, h8 b, f4 c) { return __builtin_amdgcn
 
 __device__ __forceinline__ h8 cat8(h4 lo, h4 hi) { return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7); }
 
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ h4 zero4() { return h4{(_Float16)0.0f, (_Float16)0.0f, (_Float16)0.0f, (_Float16)0.0f}; }
 
+// ReLU on the fp16-rounded accumulator, the reference's own order (relu<half> = __hmax(val, 0) on
+// the fp16 fragment, common_device.h:90-97): v_pk_max_f16 with 0 as the first operand, one packed
+// instruction per two values (max(0, -0) = +0 and max(0, NaN) = 0 on gfx950: tools/relu_probe.hip).
+// Rounding first then clamping equals clamping then rounding (the rounding is monotone and
+// fixes 0). As fp32 C code (v > 0 ? v : 0) the compiler emitted two v_max_f32 per value (a
+// canonicalising one first); as asm on the fp32 value it would read the MFMA result registers,
+// whose read-after-MFMA hazard the compiler does not pad for inline asm -- the cvt in between is an
+// ordinary instruction, so the asm here only reads VALU results.
+__device__ __forceinline__ uint32_t relu_pk_f16(uint32_t x) {
+	uint32_t r;
+	asm("v_pk_max_f16 %0, 0, %1" : "=v"(r) : "v"(x));
+	return r;
+}
 template <Act A>
 __device__ __forceinline__ h4 act_fwd(f4 v) {
+	h4 h = __builtin_convertvector(v, h4);
 	if constexpr (A == Act::ReLU) {
-		v[0] = v[0] > 0.0f ? v[0] : 0.0f; v[1] = v[1] > 0.0f ? v[1] : 0.0f;
-		v[2] = v[2] > 0.0f ? v[2] : 0.0f; v[3] = v[3] > 0.0f ? v[3] : 0.0f;
+		u32x2 b = __builtin_bit_cast(u32x2, h);
+		b[0] = relu_pk_f16(b[0]);
+		b[1] = relu_pk_f16(b[1]);
+		h = __builtin_bit_cast(h4, b);
 	}
-	return __builtin_convertvector(v, h4);
+	return h;
 }
 
 // activation transfer given the post-activation value (reference common_device.h:240-297).
 // ReLU: fwd > 0 ? g : 0. act_fwd only produces +0 or positive values (never -0 or NaN), so the test
-// is "fwd bits != 0", done on packed u16 lanes: mask = 0 - min(bits, 1) keeps both halves of a
-// register packed (per-half compares would unpack the activations into one VGPR per half).
-typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+// is "fwd bits != 0", done on packed u16 lanes: r * min(bits, 1) keeps both halves of a register
+// packed. Written as inline asm (two packed VALU per register): from the equivalent C the compiler
+// proves the operand is an fp16 value, turns "bits != 0" into an fp16 class test and lowers that
+// per half through ~10 SDWA compares + SALU mask ops (r03 ISA: 320 16-bit compares, ~40 % of the
+// fused kernel's MLP instructions).
+__device__ __forceinline__ uint32_t relu_mask_pk(uint32_t r, uint32_t fwd) {
+	uint32_t t;
+	asm("v_pk_min_u16 %0, %1, %2" : "=v"(t) : "v"(fwd), "s"(0x00010001u));
+	asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(r) : "v"(r), "v"(t));
+	return r;
+}
 template <Act A>
 __device__ __forceinline__ h4 act_bwd(h4 fwd, f4 g) {
 	h4 r = __builtin_convertvector(g, h4);
 	if constexpr (A == Act::ReLU) {
-		const u16x4 one = {1, 1, 1, 1}, zero = {0, 0, 0, 0};
-		const u16x4 m = zero - __builtin_elementwise_min(__builtin_bit_cast(u16x4, fwd), one);
-		r = __builtin_bit_cast(h4, __builtin_bit_cast(u16x4, r) & m);
+		const u32x2 f = __builtin_bit_cast(u32x2, fwd);
+		u32x2 v = __builtin_bit_cast(u32x2, r);
+		v[0] = relu_mask_pk(v[0], f[0]);
+		v[1] = relu_mask_pk(v[1], f[1]);
+		r = __builtin_bit_cast(h4, v);
 	}
 	return r;
 }
@@ -174,6 +202,14 @@ __device__ __forceinline__ h8 stg_trfrag(const _Float16* S, int q, int c, int ti
 }
 
 
+// Output rows of the fused weight image are stored transposed 4 x 4: network output o sits in image
+// row out_row(o) = 4 (o % 4) + o / 4 (an involution). The output-layer MFMA gives lane (c, q) the
+// image rows 4q + r (r = 0..3), i.e. outputs 4r + q, so the first four outputs land in register r = 0
+// of the four lane groups and the loss of a <= 4-output network (config_hash: 3) runs once per
+// 16-sample tile instead of once per r, with three of four lane groups busy instead of one (its
+// four IEEE divisions per element were ~30 % of the fused kernel's VALU instructions).
+__host__ __device__ constexpr int out_row(int o) { return 4 * (o & 3) + (o >> 2); }
+
 template <int W, int IN, int NH>
 struct FusedLayout {
 	static_assert(W % 32 == 0 && IN % 32 == 0 && NH >= 1, "fused MLP: W, IN multiples of 32");
@@ -225,7 +261,7 @@ __device__ __forceinline__ void load_weights_lds(_Float16* smem, const _Float16*
 		for (int idx = tid; idx < W * W; idx += nthreads) s[L::oWh + j * W * L::RSW + (idx / W) * L::RSW + idx % W] = p[idx];
 		p += W * W;
 	}
-	for (int idx = tid; idx < 16 * W; idx += nthreads) s[L::oWo + (idx / W) * L::RSW + idx % W] = p[idx];
+	for (int idx = tid; idx < 16 * W; idx += nthreads) s[L::oWo + out_row(idx / W) * L::RSW + idx % W] = p[idx];
 }
 
 // The LDS weight image is built once per step by k_pack_weights into global memory; every
@@ -360,15 +396,23 @@ __device__ __forceinline__ void slice_fwd_loss(const FusedTrainArgs& a, uint32_t
 		for (int tau = 0; tau < 2; ++tau) {
 			const uint32_t i = base + 16 * tau + c;
 			if constexpr (EXT_DOUT) {
-				G[tau] = Gext[tau];
+				// external dL/dy, read here rather than with the targets so it is not live across the
+				// forward (registers); register r of lane group q = output 4r + q (out_row)
+				(void)Gext;
+				const _Float16* dp = a.dout + (size_t)i * 16 + q;
+				G[tau] = h4{dp[0], dp[4], dp[8], dp[12]};
 				continue;
 			}
 			const h4 y = __builtin_convertvector(yacc[tau], h4);
-			if (a.out) *(h4*)(a.out + (size_t)i * 16 + 4 * q) = y;
+			if (a.out) {
+#pragma unroll
+				for (int r = 0; r < 4; ++r) a.out[(size_t)i * 16 + 4 * r + q] = y[r];  // image row 4q + r = output 4r + q
+			}
 			h4 g = zero4();
 #pragma unroll
 			for (int r = 0; r < 4; ++r) {
-				const uint32_t o = 4 * q + r;
+				if (4u * r >= a.dims) break;  // wave-uniform: r = 0 only for <= 4 outputs
+				const uint32_t o = 4 * r + q;
 				if (o < a.dims) {
 					const float p = (float)y[r];
 					const float pse = a.loss_l2 ? 1.0f : __builtin_fmaf(p, p, 0.01f);  // L2: pdf = 1
@@ -539,7 +583,7 @@ __device__ __forceinline__ void block_reduce_wgrad(WgradAcc<W, IN, NH>& acc, flo
 		for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
 			for (int r = 0; r < 4; ++r) {
-				float* p = &S[oO + (4 * q + r) * W + 16 * nt + c];
+				float* p = &S[oO + (4 * r + q) * W + 16 * nt + c];  // accumulator row 4q + r = output 4r + q
 				if (add) acc.Wo[nt][r] += *p; else *p = acc.Wo[nt][r];
 			}
 	};
@@ -606,13 +650,13 @@ __global__ __launch_bounds__(64 * FUSED_WAVES, 8 / FUSED_WAVES) void k_fused_tra
 			const uint32_t i = base + 16 * tau + c;
 #pragma unroll
 			for (int r = 0; r < 4; ++r) {
-				const uint32_t o = 4 * q + r;
+				const uint32_t o = 4 * r + q;  // out_row: register r of lane group q holds output 4r + q
 				tg[tau][r] = (!EXT_DOUT && o < a.dims) ? a.target[(size_t)i * a.dims + o] : 0.0f;
 			}
 		}
 #pragma unroll
 		for (int tau = 0; tau < 2; ++tau) {
-			if constexpr (EXT_DOUT) Gext[tau] = *(const h4*)(a.dout + (size_t)(base + 16 * tau + c) * 16 + 4 * q);
+			Gext[tau] = zero4();  // EXT_DOUT: read in slice_fwd_loss
 		}
 		if constexpr (ENC_MEM) {
 			// xt[tau][2s + (pp >> 1)][2 (pp & 1) + f] = feature f of level 16 s + 8 (pp >> 1) + 2 q + (pp & 1)
@@ -673,7 +717,7 @@ __global__ __launch_bounds__(64 * FUSED_WAVES, 8 / FUSED_WAVES) void k_fused_tra
 					}
 		}
 		if constexpr (PROF) { t1 = stamp(); ph[0] += t1 - t0; t0 = t1; }
-		auto target = [&](int tau, uint32_t o) { return tg[tau][o & 3]; };
+		auto target = [&](int tau, uint32_t o) { return tg[tau][o >> 2]; };
 		auto after_loss = [] {};
 		fused_slice<W, IN, NH, ACT, EXT_DOUT, PROF>(a, base, c, q, xt, target, after_loss, Gext, smem + L::oW0,
 		                                            smem + L::oWh, smem + L::oWo, bufA, bufD, acc, ph, t0);
@@ -746,7 +790,9 @@ __global__ __launch_bounds__(256, 2) void k_mlp_infer(uint32_t B, const _Float16
 		f4 y = fz;
 #pragma unroll
 		for (int s = 0; s < KW; ++s) y = mfma16(lds_afrag(sWo, L::RSW, c, 32 * s + 4 * q), cat8(act[2 * s], act[2 * s + 1]), y);
-		*(h4*)(out + (size_t)i * 16 + 4 * q) = __builtin_convertvector(y, h4);
+		const h4 yh = __builtin_convertvector(y, h4);
+#pragma unroll
+		for (int r = 0; r < 4; ++r) out[(size_t)i * 16 + 4 * r + q] = yh[r];  // out_row
 	}
 }
 
