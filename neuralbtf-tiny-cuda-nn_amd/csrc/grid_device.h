@@ -248,7 +248,10 @@ __device__ __forceinline__ h2 encode_level_f2_inrange(const uint32_t* __restrict
 			dn += td[d][b];
 		}
 		const uint32_t dm = __builtin_elementwise_min(dn, dn - li.size);  // dn % size for dn < 2 size
-		const uint32_t idx = ((h & hmask) & m) | (dm & ~m);
+		uint32_t idx = ((h & hmask) & m) | (dm & ~m);
+#ifdef TCNN_DIAG_GATHER_MASK  // diagnostic builds only (wrong results): gathers confined to a few cache lines
+		idx &= TCNN_DIAG_GATHER_MASK;
+#endif
 		w16[c] = (_Float16)w;  // as encode_level_f2
 		v[c] = *(const uint32_t*)((const char*)table_u32 + (obytes + (idx << 2)));
 	}
