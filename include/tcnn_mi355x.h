@@ -125,6 +125,24 @@ int tcnn_trainer_training_step(tcnn_trainer* t, void* stream, uint32_t n, const 
 int tcnn_trainer_training_step_part(tcnn_trainer* t, void* stream, uint32_t n, const float* input, const float* target, int part);
 /* Trainer::optimizer_step(stream, loss_scale) (trainer.h:155-157) */
 int tcnn_trainer_optimizer_step(tcnn_trainer* t, void* stream);
+/* Trainer::forward / backward (trainer.h:97-153): the halves of training_step with the reference's
+ * options. forward: data_pdf fp32 [n x n_out] or NULL; external_dL_dy fp16 [n x padded_output_width]
+ * (loss-scaled, i.e. already multiplied by tcnn_default_loss_scale) or NULL, in which case the loss
+ * is evaluated on target; prepare_input_gradients keeps what a dL/dinput backward needs. The context
+ * holds the output fp16 [n x padded_output_width] and dL/doutput. backward: gradients of the
+ * context's dL/doutput into gradients_fp32 (accumulate = 0: Overwrite, 1: Accumulate,
+ * GradientMode, common.h), optional dL/dinput fp32 [n x n_in]; then tcnn_trainer_optimizer_step. */
+typedef struct tcnn_trainer_context tcnn_trainer_context;  /* Trainer::ForwardContext (trainer.h:89-95) */
+tcnn_trainer_context* tcnn_trainer_forward(tcnn_trainer* t, void* stream, uint32_t n, const float* input, const float* target,
+                                           const float* data_pdf, const void* external_dL_dy, int prepare_input_gradients);
+int tcnn_trainer_backward(tcnn_trainer* t, void* stream, const tcnn_trainer_context* ctx, uint32_t n, const float* input,
+                          float* dL_dinput, int accumulate);
+/* Trainer::loss(stream, ctx) (trainer.h:205-211): synchronises stream; 0 for an external-dL/dy context */
+float tcnn_trainer_context_loss(tcnn_trainer* t, void* stream, const tcnn_trainer_context* ctx);
+const void* tcnn_trainer_context_output(const tcnn_trainer_context* ctx);
+const void* tcnn_trainer_context_doutput(const tcnn_trainer_context* ctx);
+void tcnn_trainer_context_destroy(tcnn_trainer_context* ctx);
+uint32_t tcnn_trainer_padded_output_width(const tcnn_trainer* t);
 /* Adam on parameters [begin, end) only, counting as one optimizer step (data-parallel sharded
  * optimizer: each rank updates its shard of the reduce-scattered gradient sums; the caller then
  * all-gathers the fp16 parameters). Not in the reference, which has no multi-GPU path. */

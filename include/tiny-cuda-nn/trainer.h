@@ -5,8 +5,10 @@
 // three launches on the caller's stream (neuralbtf-tiny-cuda-nn_amd/csrc/runtime.cpp,
 // TrainerHost::training_step_overlapped), so training_step() is one C-ABI call. The ForwardContext it
 // returns identifies the step; loss(ctx) reads that step's loss sum (trainer.h:205-211 reduces the
-// context's loss values). The separate forward()/backward() of the reference, data_pdf, external
-// dL/dy, dL/dinput and Accumulate gradients are not part of this engine's training step and throw.
+// context's loss values). With any of the reference's options (data_pdf, external dL/dy, dL/dinput,
+// Accumulate gradients) training_step runs as the reference's does: forward() (network output +
+// loss, or the caller's dL/dy) then backward() (tcnn_trainer_forward / _backward), then the optimizer;
+// loss(ctx) then reads the context's own loss.
 #pragma once
 
 #include <memory>
@@ -46,11 +48,72 @@ public:
 	Trainer(const Trainer&) = delete;
 	Trainer& operator=(const Trainer&) = delete;
 
-	// trainer.h:89-95
+	// trainer.h:89-95. A context made by forward() (or an optioned training_step) owns the engine's
+	// context: output and dL_doutput are views of its fp16 [padded_output_width x batch] buffers.
 	struct ForwardContext : public Context {
 		const Trainer* owner = nullptr;
 		uint64_t step = 0;
+		tcnn_trainer_context* h = nullptr;
+		GPUMatrix<COMPUTE_T> output, dL_doutput;
+		ForwardContext() = default;
+		ForwardContext(const ForwardContext&) = delete;
+		ForwardContext& operator=(const ForwardContext&) = delete;
+		~ForwardContext() { tcnn_trainer_context_destroy(h); }
 	};
+
+	uint32_t padded_output_width() const { return tcnn_trainer_padded_output_width(m_h); }
+
+	// trainer.h:97-144: network output + loss (or the caller's external dL/dy, loss-scaled)
+	std::unique_ptr<ForwardContext> forward(hipStream_t stream, const float loss_scale, const GPUMatrixDynamic<T>& input,
+	                                        const GPUMatrixDynamic<float>& target, const GPUMatrixDynamic<float>* data_pdf = nullptr,
+	                                        bool use_inference_params = false, bool prepare_input_gradients = false,
+	                                        const GPUMatrixDynamic<COMPUTE_T>* external_dL_dy = nullptr) {
+		(void)loss_scale;  // the engine's default_loss_scale<__half>() (common.h:232)
+		(void)use_inference_params;
+		const uint32_t n = input.n();
+		CHECK_THROW(input.m() == m_model->input_width());
+		CHECK_THROW(input.layout() == CM && input.is_contiguous());
+		if (external_dL_dy) {
+			CHECK_THROW(external_dL_dy->m() == padded_output_width());
+			CHECK_THROW(external_dL_dy->n() == n);
+		} else {
+			CHECK_THROW(target.m() == m_model->output_width());
+			CHECK_THROW(target.n() == n);
+		}
+		if (data_pdf) CHECK_THROW(data_pdf->m() == m_model->output_width() && data_pdf->n() == n);
+		auto ctx = std::make_unique<ForwardContext>();
+		ctx->owner = this;
+		ctx->step = ++m_n_steps;
+		ctx->h = tcnn_trainer_forward(m_h, stream, n, input.data(), external_dL_dy ? nullptr : target.data(),
+		                              data_pdf ? data_pdf->data() : nullptr, external_dL_dy ? external_dL_dy->data() : nullptr,
+		                              prepare_input_gradients ? 1 : 0);
+		if (!ctx->h) throw std::runtime_error{tcnn_last_error()};
+		const uint32_t w = padded_output_width();
+		ctx->output = GPUMatrix<COMPUTE_T>{(COMPUTE_T*)tcnn_trainer_context_output(ctx->h), w, n};
+		ctx->dL_doutput = GPUMatrix<COMPUTE_T>{(COMPUTE_T*)tcnn_trainer_context_doutput(ctx->h), w, n};
+		return ctx;
+	}
+	std::unique_ptr<ForwardContext> forward(const float loss_scale, const GPUMatrixDynamic<T>& input, const GPUMatrixDynamic<float>& target,
+	                                        const GPUMatrixDynamic<float>* data_pdf = nullptr, bool use_inference_params = false,
+	                                        bool prepare_input_gradients = false,
+	                                        const GPUMatrixDynamic<COMPUTE_T>* external_dL_dy = nullptr) {
+		return forward(nullptr, loss_scale, input, target, data_pdf, use_inference_params, prepare_input_gradients, external_dL_dy);
+	}
+
+	// trainer.h:146-153: parameter gradients (Overwrite or Accumulate) and optionally dL/dinput
+	void backward(hipStream_t stream, const ForwardContext& ctx, const GPUMatrixDynamic<T>& input, GPUMatrixDynamic<T>* dL_dinput = nullptr,
+	              bool use_inference_params = false, GradientMode param_gradients_mode = GradientMode::Overwrite) {
+		(void)use_inference_params;
+		if (!ctx.h || ctx.owner != this) throw std::runtime_error{"Trainer::backward: the context was not made by this trainer's forward()"};
+		if (param_gradients_mode == GradientMode::Ignore) throw std::runtime_error{"Trainer::backward: GradientMode::Ignore is not supported"};
+		if (dL_dinput) CHECK_THROW(dL_dinput->m() == m_model->input_width() && dL_dinput->n() == input.n() && dL_dinput->layout() == CM);
+		detail::check_rc(tcnn_trainer_backward(m_h, stream, ctx.h, input.n(), input.data(), dL_dinput ? dL_dinput->data() : nullptr,
+		                                       param_gradients_mode == GradientMode::Accumulate ? 1 : 0));
+	}
+	void backward(const ForwardContext& ctx, const GPUMatrixDynamic<T>& input, GPUMatrixDynamic<T>* dL_dinput = nullptr,
+	              bool use_inference_params = false, GradientMode param_gradients_mode = GradientMode::Overwrite) {
+		backward(nullptr, ctx, input, dL_dinput, use_inference_params, param_gradients_mode);
+	}
 
 	// trainer.h:68-87
 	void initialize_params() {
@@ -66,12 +129,19 @@ public:
 	                                              const GPUMatrixDynamic<COMPUTE_T>* external_dL_dy = nullptr) {
 		(void)use_inference_params;
 		CHECK_THROW(input.m() == m_model->input_width());
+		CHECK_THROW(input.n() % BATCH_SIZE_GRANULARITY == 0);
+		CHECK_THROW(input.layout() == CM && input.is_contiguous());
+		if (data_pdf || dL_dinput || external_dL_dy || param_gradients_mode != GradientMode::Overwrite) {
+			// trainer.h:163-203 as written: forward, backward, optimizer
+			auto ctx = forward(stream, default_loss_scale<PARAMS_T>(), input, target, data_pdf, use_inference_params, dL_dinput != nullptr,
+			                   external_dL_dy);
+			backward(stream, *ctx, input, dL_dinput, use_inference_params, param_gradients_mode);
+			if (run_optimizer) optimizer_step(stream, default_loss_scale<PARAMS_T>());
+			return ctx;
+		}
 		CHECK_THROW(target.m() == m_model->output_width());
 		CHECK_THROW(input.n() == target.n());
-		CHECK_THROW(input.n() % BATCH_SIZE_GRANULARITY == 0);
-		CHECK_THROW(input.layout() == CM && input.is_contiguous() && target.layout() == CM && target.is_contiguous());
-		if (data_pdf || dL_dinput || external_dL_dy || param_gradients_mode != GradientMode::Overwrite)
-			throw std::runtime_error{"Trainer::training_step: data_pdf / dL_dinput / external dL/dy / non-Overwrite gradients are not supported"};
+		CHECK_THROW(target.layout() == CM && target.is_contiguous());
 		detail::check_rc(tcnn_trainer_training_step(m_h, stream, input.n(), input.data(), target.data(), run_optimizer ? 1 : 0));
 		auto ctx = std::make_unique<ForwardContext>();
 		ctx->owner = this;
@@ -89,6 +159,11 @@ public:
 
 	// trainer.h:205-211: synchronises `stream`
 	float loss(hipStream_t stream, const ForwardContext& ctx) const {
+		if (ctx.h && ctx.owner == this) {  // a forward() context carries its own loss values
+			const float v = tcnn_trainer_context_loss(m_h, stream, ctx.h);
+			if (v < 0.0f) throw std::runtime_error{tcnn_last_error()};
+			return v;
+		}
 		if (ctx.owner != this || ctx.step != m_n_steps)
 			throw std::runtime_error{"Trainer::loss: only the loss of this trainer's most recent training step is retained"};
 		const float v = tcnn_trainer_loss(m_h, stream);

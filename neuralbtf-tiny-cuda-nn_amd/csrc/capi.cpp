@@ -423,6 +423,38 @@ int tcnn_trainer_training_step_part(tcnn_trainer* t, void* stream, uint32_t n, c
 int tcnn_trainer_optimizer_step(tcnn_trainer* t, void* stream) {
 	return guard([&] { t->t->optimizer_step((hipStream_t)stream); });
 }
+struct tcnn_trainer_context {
+	std::unique_ptr<TrainerFwdCtx> c;
+};
+tcnn_trainer_context* tcnn_trainer_forward(tcnn_trainer* t, void* stream, uint32_t n, const float* in, const float* target, const float* pdf,
+                                           const void* ext, int prep) {
+	tcnn_trainer_context* r = nullptr;
+	const int rc = guard([&] {
+		TCNN_CHECK(n > 0, "forward: empty batch");
+		auto c = t->t->forward((hipStream_t)stream, n, in, target, pdf, ext, prep != 0);
+		r = new tcnn_trainer_context{std::move(c)};
+	});
+	return rc == 0 ? r : nullptr;
+}
+int tcnn_trainer_backward(tcnn_trainer* t, void* stream, const tcnn_trainer_context* ctx, uint32_t n, const float* in, float* dL_din,
+                          int accumulate) {
+	return guard([&] {
+		TCNN_CHECK(ctx != nullptr, "backward: null context");
+		t->t->backward((hipStream_t)stream, *ctx->c, n, in, dL_din, accumulate != 0);
+	});
+}
+float tcnn_trainer_context_loss(tcnn_trainer* t, void* stream, const tcnn_trainer_context* ctx) {
+	float v = -1.0f;
+	guard([&] {
+		TCNN_CHECK(ctx != nullptr, "loss: null context");
+		v = t->t->ctx_loss((hipStream_t)stream, *ctx->c);
+	});
+	return v;
+}
+const void* tcnn_trainer_context_output(const tcnn_trainer_context* ctx) { return ctx ? ctx->c->out16.p : nullptr; }
+const void* tcnn_trainer_context_doutput(const tcnn_trainer_context* ctx) { return ctx ? ctx->c->dLdy() : nullptr; }
+void tcnn_trainer_context_destroy(tcnn_trainer_context* ctx) { delete ctx; }
+uint32_t tcnn_trainer_padded_output_width(const tcnn_trainer* t) { return t->t->model->mlp.padded_output; }
 int tcnn_trainer_optimizer_step_range(tcnn_trainer* t, void* stream, uint64_t begin, uint64_t end) {
 	return guard([&] { t->t->optimizer_step_range((hipStream_t)stream, begin, end); });
 }

@@ -259,7 +259,10 @@ void launch_wgrad(hipStream_t st, uint32_t B, uint32_t N, uint32_t K, const void
                   uint32_t n_chunks);
 uint32_t relative_l2_n_blocks(uint32_t B, uint32_t stride);
 void launch_relative_l2_partial(hipStream_t st, uint32_t B, uint32_t stride, uint32_t dims, float loss_scale, const void* pred16,
-                                const float* target, void* grads16, float* loss_partial, uint32_t loss_l2 = 0);
+                                const float* target, void* grads16, float* loss_partial, uint32_t loss_l2 = 0,
+                                const float* pdf = nullptr);
+// out[i] += in[i] (Accumulate-mode gradients)
+void launch_add_f32(hipStream_t st, const float* in, float* out, size_t n);
 
 // ---- OneBlob / Identity encodings (encodings.hip); output AoS fp16 [B][out_stride], padding = 1 ----
 void launch_oneblob_fwd(hipStream_t st, uint32_t B, uint32_t D, uint32_t n_bins, const float* x, uint32_t x_stride, void* out16,

@@ -219,6 +219,17 @@ void launch_relative_l2(hipStream_t st, uint32_t B, uint32_t stride, uint32_t di
 	TCNN_HIP_CHECK(hipGetLastError());
 }
 
+__global__ __launch_bounds__(256) void k_add_f32(const float* __restrict__ in, float* __restrict__ out, size_t n) {
+	const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+	if (i < n) out[i] += in[i];
+}
+
+void launch_add_f32(hipStream_t st, const float* in, float* out, size_t n) {
+	if (!n) return;
+	hipLaunchKernelGGL(k_add_f32, dim3((uint32_t)div_round_up(n, 256)), dim3(256), 0, st, in, out, n);
+	TCNN_HIP_CHECK(hipGetLastError());
+}
+
 __global__ __launch_bounds__(256) void k_sum(const float* __restrict__ in, uint32_t n, float* __restrict__ out) {
 	__shared__ float part[4];
 	float s = 0.0f;

@@ -386,7 +386,7 @@ void launch_wgrad(hipStream_t st, uint32_t B, uint32_t N, uint32_t K, const void
 __global__ __launch_bounds__(256) void k_relative_l2_partial(uint32_t l2, uint32_t n_elements, uint32_t stride, uint32_t dims, float loss_scale,
                                                               float n_total, const _Float16* __restrict__ pred,
                                                               const float* __restrict__ target, _Float16* __restrict__ grads,
-                                                              float* __restrict__ loss_partial) {
+                                                              float* __restrict__ loss_partial, const float* __restrict__ pdf) {
 	__shared__ float part[4];
 	float s = 0.0f;
 	for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n_elements; i += gridDim.x * 256) {
@@ -398,6 +398,12 @@ __global__ __launch_bounds__(256) void k_relative_l2_partial(uint32_t l2, uint32
 		const float p = (float)pred[i];
 		const float pse = l2 ? 1.0f : __builtin_fmaf(p, p, 0.01f);
 		const float d = p - target[inter * dims + intra];
+		if (pdf) {  // data_pdf (relative_l2.h:64-72, l2.h:63-71): values and gradient divided by the pdf
+			const float f = pdf[inter * dims + intra];
+			s += d * d / pse / f / n_total;
+			grads[i] = f16_rn(loss_scale * (2.0f * d / pse / f) / n_total);
+			continue;
+		}
 		s += d * d / pse / n_total;
 		const float gr = 2.0f * d / pse;
 		grads[i] = f16_rn(loss_scale * gr / n_total);
@@ -412,11 +418,11 @@ __global__ __launch_bounds__(256) void k_relative_l2_partial(uint32_t l2, uint32
 uint32_t relative_l2_n_blocks(uint32_t B, uint32_t stride) { return std::max(1u, std::min(div_round_up((uint64_t)B * stride, 256), 1024u)); }
 
 void launch_relative_l2_partial(hipStream_t st, uint32_t B, uint32_t stride, uint32_t dims, float loss_scale, const void* pred16,
-                                const float* target, void* grads16, float* loss_partial, uint32_t loss_l2) {
+                                const float* target, void* grads16, float* loss_partial, uint32_t loss_l2, const float* pdf) {
 	const uint32_t n = B * stride;
 	if (!n) return;
 	hipLaunchKernelGGL(k_relative_l2_partial, dim3(relative_l2_n_blocks(B, stride)), dim3(256), 0, st, loss_l2, n, stride, dims, loss_scale,
-	                   (float)((uint64_t)B * dims), (const _Float16*)pred16, target, (_Float16*)grads16, loss_partial);
+	                   (float)((uint64_t)B * dims), (const _Float16*)pred16, target, (_Float16*)grads16, loss_partial, pdf);
 	TCNN_HIP_CHECK(hipGetLastError());
 }
 

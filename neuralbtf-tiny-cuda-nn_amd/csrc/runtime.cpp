@@ -1215,6 +1215,49 @@ void TrainerHost::optimizer_step(hipStream_t st) {  // AdamOptimizer::step, adam
 	ws.wimage_valid = false;
 }
 
+std::unique_ptr<TrainerFwdCtx> TrainerHost::forward(hipStream_t st, uint32_t B, const float* input, const float* target, const float* pdf,
+                                                    const void* ext_dLdy16, bool prep_dinput) {
+	TCNN_CHECK(B % BATCH_GRANULARITY == 0, "forward: batch size must be a multiple of 256");
+	TCNN_CHECK(ext_dLdy16 || target, "forward: a target (or an external dL/dy) is required");
+	NetworkHost& m = *model;
+	const uint32_t OUTP = m.mlp.padded_output;
+	auto c = std::make_unique<TrainerFwdCtx>();
+	c->B = B;
+	c->out16.reserve((size_t)B * OUTP * 2);
+	c->layout = m.forward_keep(st, ws, B, input, w16.p, c->out16.p, prep_dinput, c->keep);
+	if (ext_dLdy16) {  // trainer.h:126-130: the caller's dL/dy replaces the loss
+		c->ext = ext_dLdy16;
+	} else {
+		c->dLdy16.reserve((size_t)B * OUTP * 2);
+		c->n_lpart = relative_l2_n_blocks(B, OUTP);
+		c->lpart.reserve((size_t)c->n_lpart * 4);
+		launch_relative_l2_partial(st, B, OUTP, n_output_dims, loss_scale, c->out16.p, target, c->dLdy16.p, c->lpart.as<float>(),
+		                           m.loss_l2, pdf);
+	}
+	ws.wimage_valid = false;  // forward_keep may have packed the image in place
+	return c;
+}
+
+void TrainerHost::backward(hipStream_t st, const TrainerFwdCtx& c, uint32_t B, const float* input, float* dL_dinput, bool accumulate) {
+	TCNN_CHECK(B == c.B, "backward: batch size differs from the forward's");
+	float* dst = g32.as<float>();
+	if (accumulate) {
+		g32_acc.reserve(n_params * 4);
+		dst = g32_acc.as<float>();
+	}
+	model->fwd_bwd(st, ws, B, input, nullptr, n_output_dims, 1.0f, w16.p, c.dLdy(), nullptr, dst, nullptr, dL_dinput,
+	               c.keep.p ? c.keep.p : nullptr, c.layout);
+	if (accumulate) launch_add_f32(st, dst, g32.as<float>(), n_params);
+	ws.wimage_valid = false;
+	last_B = B;
+}
+
+float TrainerHost::ctx_loss(hipStream_t st, const TrainerFwdCtx& c) {  // trainer.h:205-211
+	if (c.ext) return 0.0f;  // no loss was evaluated (the reference's L stays unwritten)
+	launch_sum(st, c.lpart.as<float>(), c.n_lpart, d_loss.as<float>());
+	return loss(st);
+}
+
 void TrainerHost::optimizer_step_range(hipStream_t st, uint64_t begin, uint64_t end) {
 	TCNN_CHECK(begin <= end && end <= n_params, "optimizer_step_range: range outside the parameter vector");
 	++adam_step;

@@ -286,6 +286,19 @@ struct DpComm {
 };
 void dp_unique_id(void* id128);  // ncclGetUniqueId (one rank; the caller broadcasts it)
 
+// Trainer::forward's context (reference trainer.h:89-95, 97-144): the network output, the loss-scaled
+// dL/d(output) (from the loss, or the caller's external dL/dy), the loss partial sums and the encoding
+// kept for the backward (NetworkHost::forward_keep).
+struct TrainerFwdCtx {
+	uint32_t B = 0;
+	DevBuf keep;
+	int layout = 0;
+	DevBuf out16, dLdy16, lpart;
+	const void* ext = nullptr;  // external dL/dy (not owned)
+	uint32_t n_lpart = 0;
+	const void* dLdy() const { return ext ? ext : dLdy16.p; }
+};
+
 struct TrainerHost {
 	uint32_t n_input_dims, n_output_dims;
 	PhaseTimer timer;
@@ -320,6 +333,16 @@ struct TrainerHost {
 	void training_step(hipStream_t st, uint32_t B, const float* input, const float* target, bool run_optimizer);
 	void training_step_part(hipStream_t st, uint32_t B, const float* input, const float* target, int part);
 	void optimizer_step(hipStream_t st);
+	// Trainer::forward / backward (trainer.h:97-153): the two halves of training_step with the
+	// reference's options -- data_pdf (fp32 [B][n_output_dims]), external dL/dy (fp16 [B][padded
+	// output], loss-scaled like the loss's own), dL/dinput (fp32 [B][n_input_dims]) and Accumulate
+	// gradients (added to gradients_fp32() instead of overwriting it). Gradients land in the buffer
+	// optimizer_step() reads.
+	std::unique_ptr<TrainerFwdCtx> forward(hipStream_t st, uint32_t B, const float* input, const float* target, const float* pdf,
+	                                       const void* ext_dLdy16, bool prep_dinput);
+	void backward(hipStream_t st, const TrainerFwdCtx& c, uint32_t B, const float* input, float* dL_dinput, bool accumulate);
+	float ctx_loss(hipStream_t st, const TrainerFwdCtx& c);
+	DevBuf g32_acc;  // Accumulate mode: this backward's gradients before they are added
 	// data-parallel exchange inside the step (dp.cpp): with a communicator attached every
 	// training_step(run_optimizer = true) sums the gradients across the ranks (all-reduce, or
 	// reduce-scatter + Adam on this rank's shard + all-gather of the fp16 parameters when sharded)

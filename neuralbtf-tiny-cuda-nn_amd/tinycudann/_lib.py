@@ -55,6 +55,13 @@ _SIGS = {
     "tcnn_trainer_destroy": (None, [c_void_p]),
     "tcnn_trainer_training_step": (c_int, [c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_int]),
     "tcnn_trainer_optimizer_step": (c_int, [c_void_p, c_void_p]),
+    "tcnn_trainer_forward": (c_void_p, [c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_int]),
+    "tcnn_trainer_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_int]),
+    "tcnn_trainer_context_loss": (c_float, [c_void_p, c_void_p, c_void_p]),
+    "tcnn_trainer_context_output": (c_void_p, [c_void_p]),
+    "tcnn_trainer_context_doutput": (c_void_p, [c_void_p]),
+    "tcnn_trainer_context_destroy": (None, [c_void_p]),
+    "tcnn_trainer_padded_output_width": (c_uint32, [c_void_p]),
     "tcnn_trainer_optimizer_step_range": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64]),
     "tcnn_trainer_training_step_part": (c_int, [c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_int]),
     "tcnn_trainer_loss": (c_float, [c_void_p, c_void_p]),

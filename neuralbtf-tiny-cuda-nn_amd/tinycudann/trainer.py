@@ -52,6 +52,29 @@ class Trainer:
     def optimizer_step(self, stream=None):
         L.check(L.lib().tcnn_trainer_optimizer_step(self.h, _stream(stream)))
 
+    @property
+    def padded_output_width(self):
+        return L.lib().tcnn_trainer_padded_output_width(self.h)
+
+    def forward(self, input, target=None, data_pdf=None, external_dL_dy=None, prepare_input_gradients=False, stream=None):
+        """Trainer::forward (trainer.h:97-144): network output + loss on target (optionally weighted by
+        data_pdf float32 [B, n_out]), or the caller's loss-scaled dL/dy (float16 [B, padded_output_width]).
+        Returns a ForwardContext for backward() / its loss()."""
+        for t in (input, target, data_pdf, external_dL_dy):
+            assert t is None or t.is_contiguous()
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr() if t is not None else 0)
+        h = L.lib().tcnn_trainer_forward(self.h, _stream(stream), input.shape[0], ptr(input), ptr(target), ptr(data_pdf),
+                                         ptr(external_dL_dy), int(prepare_input_gradients))
+        return ForwardContext(self, L.check_ptr(h), input.shape[0], (input, target, data_pdf, external_dL_dy))
+
+    def backward(self, ctx, input, dL_dinput=None, accumulate=False, stream=None):
+        """Trainer::backward (trainer.h:146-153): parameter gradients into gradients_fp32()
+        (Overwrite, or Accumulate with accumulate=True) and optionally dL/dinput (float32 [B, n_in])."""
+        assert ctx.trainer is self
+        L.check(L.lib().tcnn_trainer_backward(self.h, _stream(stream), ctx.h, input.shape[0], ctypes.c_void_p(input.data_ptr()),
+                                              ctypes.c_void_p(dL_dinput.data_ptr() if dL_dinput is not None else 0),
+                                              int(accumulate)))
+
     def optimizer_step_range(self, begin, end, stream=None):
         """Adam on parameters [begin, end) only (one optimizer step; data-parallel sharded optimizer)."""
         L.check(L.lib().tcnn_trainer_optimizer_step_range(self.h, _stream(stream), int(begin), int(end)))
@@ -166,3 +189,43 @@ class Trainer:
 def create_from_config(n_input_dims, n_output_dims, config, seed=1337):
     """TrainableModel equivalent: returns the Trainer (which owns loss, optimizer and network)."""
     return Trainer(n_input_dims, n_output_dims, config, seed)
+
+
+class ForwardContext:
+    """Trainer::ForwardContext (trainer.h:89-95): owns the engine's context (output, dL/doutput, loss)."""
+
+    def __init__(self, trainer, h, n, keepalive):
+        self.trainer, self.h, self.n = trainer, h, n
+        self._keep = keepalive  # the caller's tensors the queued kernels read
+
+    def __del__(self):
+        try:
+            L.lib().tcnn_trainer_context_destroy(self.h)
+        except Exception:
+            pass
+
+    def _view(self, ptr):
+        import torch
+
+        class _Dev:  # zero-copy view of engine memory (__cuda_array_interface__), cloned below
+            pass
+
+        w = self.trainer.padded_output_width
+        d = _Dev()
+        d.__cuda_array_interface__ = {"shape": (self.n, w), "typestr": "<f2", "data": (int(ptr), False), "version": 2}
+        return torch.as_tensor(d, device="cuda").clone()
+
+    @property
+    def output(self):
+        """fp16 [B, padded_output_width] copy of the network output."""
+        return self._view(L.lib().tcnn_trainer_context_output(self.h))
+
+    @property
+    def dL_doutput(self):
+        return self._view(L.lib().tcnn_trainer_context_doutput(self.h))
+
+    def loss(self, stream=None):
+        v = L.lib().tcnn_trainer_context_loss(self.trainer.h, _stream(stream), self.h)
+        if v < 0:
+            raise L.TcnnError(L.lib().tcnn_last_error().decode())
+        return v

@@ -125,6 +125,38 @@ int main(int argc, char** argv) {
 		EXPECT(std::isfinite(first) && last < 0.5f * first);
 		EXPECT(model.optimizer->step() == 200u);
 
+		// Trainer::forward / backward halves (trainer.h:97-153): Accumulate doubles the gradient, an
+		// external dL/dy equal to the loss's own gives the same gradient, dL/dinput is written
+		{
+			const size_t n = model.trainer->n_params();
+			auto fwd = model.trainer->forward(stream, 128.0f, batch, target);
+			model.trainer->backward(stream, *fwd, batch);
+			std::vector<float> g1(n), g2(n), g3(n);
+			HIP_CHECK_THROW(hipStreamSynchronize(stream));
+			HIP_CHECK_THROW(hipMemcpy(g1.data(), tcnn_trainer_gradients_fp32(model.trainer->handle()), n * 4, hipMemcpyDeviceToHost));
+			model.trainer->backward(stream, *fwd, batch, nullptr, false, GradientMode::Accumulate);
+			HIP_CHECK_THROW(hipStreamSynchronize(stream));
+			HIP_CHECK_THROW(hipMemcpy(g2.data(), tcnn_trainer_gradients_fp32(model.trainer->handle()), n * 4, hipMemcpyDeviceToHost));
+			auto ext = model.trainer->forward(stream, 128.0f, batch, target, nullptr, false, false, &fwd->dL_doutput);
+			model.trainer->backward(stream, *ext, batch);
+			HIP_CHECK_THROW(hipStreamSynchronize(stream));
+			HIP_CHECK_THROW(hipMemcpy(g3.data(), tcnn_trainer_gradients_fp32(model.trainer->handle()), n * 4, hipMemcpyDeviceToHost));
+			GPUMatrix<float> dx(2, B);
+			auto fwd_dx = model.trainer->forward(stream, 128.0f, batch, target, nullptr, false, true);
+			model.trainer->backward(stream, *fwd_dx, batch, &dx);
+			bool dbl = true, same = true;
+			for (size_t k = 0; k < n; ++k) {
+				dbl = dbl && g2[k] == 2.0f * g1[k];
+				same = same && g3[k] == g1[k];
+			}
+			EXPECT(dbl && same);
+			EXPECT(std::isfinite(model.trainer->loss(stream, *fwd)) && model.trainer->loss(stream, *ext) == 0.0f);
+			const std::vector<float> dxh = dx.to_cpu_vector();
+			float mx = 0.0f;
+			for (float v : dxh) mx = std::fmax(mx, std::fabs(v));
+			EXPECT(mx > 0.0f && std::isfinite(mx));
+		}
+
 		model.network->inference(stream, probe, probe_out);
 		HIP_CHECK_THROW(hipStreamSynchronize(stream));
 		const std::vector<float> out = probe_out.to_cpu_vector();
