@@ -110,6 +110,16 @@ int tcnn_module_initialize_params(tcnn_module* m, uint64_t seed, float* params_f
 const char* tcnn_module_hyperparams(tcnn_module* m);
 const char* tcnn_module_name(tcnn_module* m);
 
+/* ---- workspace arena (gpu_memory.h:426-754: GPUMemoryArena, allocate_workspace, free_gpu_memory_arena) ----
+ * One arena per stream (per device for the null stream): a virtual address range the size of the
+ * device memory with physical memory mapped at its end as it grows, so addresses stay valid across
+ * growth. Allocations are 128-byte aligned; free returns the interval to the stream's arena. */
+void* tcnn_workspace_allocate(void* stream, uint64_t n_bytes);
+int tcnn_workspace_free(void* stream, void* ptr);
+int tcnn_free_workspace_arena(void* stream);
+/* mapped bytes of the stream's arena; virtual_memory = 1 when it grows by mapping (VMM), 0 fallback */
+int tcnn_workspace_arena_info(void* stream, uint64_t* mapped_bytes, int* virtual_memory);
+
 /* ---- trainer: create_from_config + Trainer<float, __half, __half> (config.h:53-63, trainer.h) ---- */
 /* config_json holds {"loss", "optimizer", "encoding", "network"}; seed as Trainer(seed=1337). */
 tcnn_trainer* tcnn_trainer_create(uint32_t n_input_dims, uint32_t n_output_dims, const char* config_json, uint32_t seed);

@@ -122,9 +122,9 @@ inline uint32_t cuda_compute_capability(int device = -1) {
 	return v;
 }
 
-// gpu_memory.h:751-754: temporary device memory of the engine's workspaces
+// gpu_memory.h:751-754: temporary device memory of the engine's workspaces (free_gpu_memory_arena
+// of one stream: gpu_memory.h in this directory)
 inline void free_all_gpu_memory_arenas() { tcnn_free_temporary_memory(); }
-inline void free_gpu_memory_arena(hipStream_t) { tcnn_free_temporary_memory(); }
 
 // common.h:232: the loss scale of half-precision training
 template <typename T>

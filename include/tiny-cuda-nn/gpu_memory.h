@@ -1,10 +1,14 @@
 // tiny-cuda-nn/gpu_memory.h -- GPUMemory<T> (reference include/tiny-cuda-nn/gpu_memory.h:60-390):
-// an owning, move-only device array. The engine's own temporaries live in its workspaces (grow-only,
-// address-stable across steps), so the reference's stream arenas (gpu_memory.h:426-754) have no
-// counterpart here beyond free_all_gpu_memory_arenas() (common.h).
+// an owning, move-only device array; and the stream-ordered workspace arena (gpu_memory.h:426-754:
+// GPUMemoryArena::Allocation, allocate_workspace, allocate_workspace_and_distribute,
+// free_gpu_memory_arena) over the engine's arenas (tcnn_workspace_*, csrc/arena.cpp: one virtual
+// address range per stream with physical memory mapped at its end as it grows, so workspace
+// addresses survive growth).
 #pragma once
 
 #include <cstring>
+#include <tuple>
+#include <utility>
 #include <vector>
 
 #include "common.h"
@@ -109,5 +113,70 @@ private:
 	size_t m_size = 0;
 	bool m_managed = false;
 };
+
+// gpu_memory.h:426-754
+class GPUMemoryArena {
+public:
+	// a workspace interval of one stream's arena, returned to it on destruction (move-only)
+	class Allocation {
+	public:
+		Allocation() = default;
+		Allocation(hipStream_t stream, uint8_t* data) : m_stream{stream}, m_data{data} {}
+		~Allocation() {
+			if (m_data) tcnn_workspace_free(m_stream, m_data);
+		}
+		Allocation(const Allocation&) = delete;
+		Allocation& operator=(const Allocation&) = delete;
+		Allocation(Allocation&& other) { *this = std::move(other); }
+		Allocation& operator=(Allocation&& other) {
+			std::swap(m_stream, other.m_stream);
+			std::swap(m_data, other.m_data);
+			return *this;
+		}
+		uint8_t* data() { return m_data; }
+		const uint8_t* data() const { return m_data; }
+		hipStream_t stream() const { return m_stream; }
+
+	private:
+		hipStream_t m_stream = nullptr;
+		uint8_t* m_data = nullptr;
+	};
+};
+
+inline size_t align_to_cacheline(size_t bytes) { return (bytes + 127) / 128 * 128; }
+
+inline GPUMemoryArena::Allocation allocate_workspace(hipStream_t stream, size_t n_bytes) {
+	if (n_bytes == 0) return {};
+	void* p = tcnn_workspace_allocate(stream, n_bytes);
+	if (!p) throw std::runtime_error{tcnn_last_error()};
+	return GPUMemoryArena::Allocation{stream, (uint8_t*)p};
+}
+
+// one allocation split into cache-line aligned arrays (gpu_memory.h:726-741)
+namespace detail {
+template <typename... Types, size_t... I>
+std::tuple<Types*...> distribute(uint8_t* base, std::index_sequence<I...>, const size_t (&offsets)[sizeof...(Types)]) {
+	return std::tuple<Types*...>{(Types*)(base + offsets[I])...};
+}
+}  // namespace detail
+
+template <typename... Types, typename... Sizes>
+std::tuple<Types*...> allocate_workspace_and_distribute(hipStream_t stream, GPUMemoryArena::Allocation* alloc, Sizes... sizes) {
+	static_assert(sizeof...(Types) == sizeof...(Sizes), "allocate_workspace_and_distribute: one size per type");
+	const size_t bytes[] = {align_to_cacheline((size_t)sizes * sizeof(Types))...};
+	size_t offsets[sizeof...(Types)];
+	size_t total = 0;
+	for (size_t i = 0; i < sizeof...(Types); ++i) {
+		offsets[i] = total;
+		total += bytes[i];
+	}
+	*alloc = allocate_workspace(stream, total);
+	return detail::distribute<Types...>(alloc->data(), std::index_sequence_for<Types...>{}, offsets);
+}
+
+// gpu_memory.h:743-754: drops the stream's arena (it must hold no live allocation)
+inline void free_gpu_memory_arena(hipStream_t stream) {
+	if (tcnn_free_workspace_arena(stream) != 0) throw std::runtime_error{tcnn_last_error()};
+}
 
 }  // namespace tcnn

@@ -423,6 +423,21 @@ int tcnn_trainer_training_step_part(tcnn_trainer* t, void* stream, uint32_t n, c
 int tcnn_trainer_optimizer_step(tcnn_trainer* t, void* stream) {
 	return guard([&] { t->t->optimizer_step((hipStream_t)stream); });
 }
+void* tcnn_workspace_allocate(void* stream, uint64_t n_bytes) {
+	void* p = nullptr;
+	guard([&] { p = workspace_allocate((hipStream_t)stream, n_bytes); });
+	return p;
+}
+int tcnn_workspace_free(void* stream, void* ptr) {
+	return guard([&] { workspace_free((hipStream_t)stream, ptr); });
+}
+int tcnn_free_workspace_arena(void* stream) {
+	return guard([&] { workspace_arena_free((hipStream_t)stream); });
+}
+int tcnn_workspace_arena_info(void* stream, uint64_t* mapped_bytes, int* virtual_memory) {
+	return guard([&] { workspace_arena_info((hipStream_t)stream, mapped_bytes, virtual_memory); });
+}
+
 struct tcnn_trainer_context {
 	std::unique_ptr<TrainerFwdCtx> c;
 };

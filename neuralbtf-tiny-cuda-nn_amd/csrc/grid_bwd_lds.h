@@ -123,6 +123,60 @@ __device__ __forceinline__ void accum_point(const float (&x)[D], const float (&d
 	}
 }
 
+// One point's corner updates, D == 2, Linear interpolation, a whole level of kind HASH_POW2 or
+// DENSE (for DENSE: a position in [0, 1], so every corner index is below 2 size) -- accum_point's
+// arithmetic with the per-dimension hash / dense terms computed once per point and no control flow
+// per corner. (As generic code the per-corner index and `% size` paths became exec-mask branches
+// around every corner, as in the fused kernel's encode, r03.)
+template <uint32_t F, HashType H, int KIND, int MODE>
+__device__ __forceinline__ void accum_point_2d_fast(const float (&x)[2], const float (&dy)[F], const LevelInfo& li, uint32_t f0,
+                                                    uint32_t nf, int* acc) {
+	float p[2];
+	uint32_t g[2];
+	pos_fract(x[0], li.scale, Interp::Linear, p[0], g[0]);
+	pos_fract(x[1], li.scale, Interp::Linear, p[1], g[1]);
+	uint32_t t[2][2];
+	if constexpr (KIND == IDX_HASH_POW2) {
+		t[0][0] = g[0] * hash_prime<H>(0);
+		t[0][1] = t[0][0] + hash_prime<H>(0);
+		t[1][0] = g[1] * hash_prime<H>(1);
+		t[1][1] = t[1][0] + hash_prime<H>(1);
+	} else {
+		t[0][0] = g[0];
+		t[0][1] = g[0] + 1u;
+		t[1][0] = g[1] * li.res;
+		t[1][1] = t[1][0] + li.res;
+	}
+#pragma unroll
+	for (uint32_t c = 0; c < 4; ++c) {
+		const uint32_t bx = c & 1u, by = c >> 1;
+		const float w = (bx ? p[0] : 1.0f - p[0]) * (by ? p[1] : 1.0f - p[1]);
+		const float wh = (float)f16_rn(w);
+		uint32_t rel;
+		if constexpr (KIND == IDX_HASH_POW2) {
+			rel = (t[0][bx] ^ t[1][by]) & (li.size - 1u);
+		} else {
+			const uint32_t d = t[0][bx] + t[1][by];
+			rel = __builtin_elementwise_min(d, d - li.size);  // d % size for d < 2 size
+		}
+		if constexpr (MODE == 0) {
+			const int a = __float2int_rn(wh * dy[0]);
+			const int b = __float2int_rn(wh * dy[1]);
+			const unsigned long long pk = (unsigned long long)(((long long)b << 32) + (long long)a);
+			__hip_atomic_fetch_add((unsigned long long*)acc + rel, pk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+		} else {
+#pragma unroll
+			for (uint32_t f = 0; f < F; ++f) {
+				if constexpr (MODE == 1) {
+					if (f - f0 < nf) lds_add_i32(&acc[rel * nf + (f - f0)], wh * dy[f]);
+				} else {
+					lds_add_i32(&acc[rel * F + f], wh * dy[f]);
+				}
+			}
+		}
+	}
+}
+
 // Register-resident variant (D == 2, F <= 2, no grid options): the chunk's dL/dy bits were loaded
 // into dyb (GRID_BWD_PR points per thread, point i0 + threadIdx.x + p * blockDim.x in slot p) for the
 // scale pre-pass and are reused here; positions stream in batches of 8 with the next batch in flight.
@@ -145,6 +199,8 @@ __device__ __forceinline__ void grid_bwd_points_regs(const uint32_t (&dyb)[GRID_
                                                      Interp interp, uint32_t begin, uint32_t len, uint32_t f0, uint32_t nf,
                                                      uint32_t i0, uint32_t i1, float scale, int* acc, const GridOpts& o) {
 	constexpr uint32_t U = GRID_BWD_PU, NB = GRID_BWD_PR / U;
+	constexpr bool FAST_KIND = D == 2 && (KIND == IDX_HASH_POW2 || KIND == IDX_DENSE);
+	const bool fast = FAST_KIND && interp == Interp::Linear && begin == 0;  // whole levels (kind HASH_POW2 / DENSE)
 	float xs[2][U][D];
 #pragma unroll
 	for (uint32_t u = 0; u < U; ++u)
@@ -154,6 +210,28 @@ __device__ __forceinline__ void grid_bwd_points_regs(const uint32_t (&dyb)[GRID_
 	for (uint32_t k = 0; k < NB; ++k) {
 		if (i0 + threadIdx.x + k * U * blockDim.x >= i1) break;
 		if (k + 1 < NB) load_pos_batch<D>(pos, pstride, i0, i1, k + 1, xs[(k + 1) & 1]);
+		bool fast_b = fast;
+		if constexpr (FAST_KIND && KIND == IDX_DENSE) {  // dense corners below 2 size need positions in [0, 1]
+			bool inr = true;
+#pragma unroll
+			for (uint32_t u = 0; u < U; ++u)
+#pragma unroll
+				for (uint32_t d = 0; d < D; ++d) inr = inr && xs[k & 1][u][d] >= 0.0f && xs[k & 1][u][d] <= 1.0f;
+			fast_b = fast_b && __builtin_amdgcn_ballot_w64(!inr) == 0;
+		}
+		if (fast_b && i0 + threadIdx.x + (k * U + U - 1) * blockDim.x < i1) {  // the whole batch is inside the chunk
+			if constexpr (FAST_KIND) {
+#pragma unroll
+				for (uint32_t u = 0; u < U; ++u) {
+					const uint32_t p = k * U + u;
+					float dy[F];
+#pragma unroll
+					for (uint32_t f = 0; f < F; ++f) dy[f] = dy_bits_feature(dyb[p], f) * scale;
+					accum_point_2d_fast<F, H, KIND, MODE>(*(const float(*)[2]) & xs[k & 1][u][0], dy, li, f0, nf, acc);
+				}
+			}
+			continue;
+		}
 #pragma unroll
 		for (uint32_t u = 0; u < U; ++u) {
 			const uint32_t p = k * U + u;
@@ -178,6 +256,8 @@ __device__ __forceinline__ void grid_bwd_points(int layout, uint32_t B, const fl
                                                 int* acc, const GridOpts& o) {
 	constexpr uint32_t NF = F;
 	constexpr uint32_t U = 8;  // points in flight per thread
+	constexpr bool FAST_KIND = D == 2 && !OPTS && (KIND == IDX_HASH_POW2 || KIND == IDX_DENSE);
+	const bool fast = FAST_KIND && interp == Interp::Linear && begin == 0;  // accum_point_2d_fast
 	for (uint32_t base = i0 + threadIdx.x; base < i1; base += U * blockDim.x) {
 		float xs[U][D], dy[U][NF];
 #pragma unroll
@@ -200,6 +280,23 @@ __device__ __forceinline__ void grid_bwd_points(int layout, uint32_t B, const fl
 			}
 #pragma unroll
 			for (uint32_t f = 0; f < F; ++f) dy[u][f] = v[f] * scale;
+		}
+		if constexpr (FAST_KIND) {
+			bool fast_b = fast;
+			if constexpr (KIND == IDX_DENSE) {
+				bool inr = true;
+#pragma unroll
+				for (uint32_t u = 0; u < U; ++u)
+#pragma unroll
+					for (uint32_t d = 0; d < D; ++d) inr = inr && xs[u][d] >= 0.0f && xs[u][d] <= 1.0f;
+				fast_b = fast_b && __builtin_amdgcn_ballot_w64(!inr) == 0;
+			}
+			if (fast_b && base + (U - 1) * blockDim.x < i1) {
+#pragma unroll
+				for (uint32_t u = 0; u < U; ++u)
+					accum_point_2d_fast<F, H, KIND, MODE>(*(const float(*)[2]) & xs[u][0], dy[u], li, f0, nf, acc);
+				continue;
+			}
 		}
 #pragma unroll
 		for (uint32_t u = 0; u < U; ++u) {

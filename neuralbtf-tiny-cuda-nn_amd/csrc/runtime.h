@@ -299,6 +299,12 @@ struct TrainerFwdCtx {
 	const void* dLdy() const { return ext ? ext : dLdy16.p; }
 };
 
+// Stream-ordered workspace arena (arena.cpp; reference gpu_memory.h:426-754)
+void* workspace_allocate(hipStream_t st, size_t n_bytes);
+void workspace_free(hipStream_t st, void* p);
+void workspace_arena_free(hipStream_t st);
+void workspace_arena_info(hipStream_t st, uint64_t* mapped_bytes, int* vmm);
+
 struct TrainerHost {
 	uint32_t n_input_dims, n_output_dims;
 	PhaseTimer timer;

@@ -62,6 +62,10 @@ _SIGS = {
     "tcnn_trainer_context_doutput": (c_void_p, [c_void_p]),
     "tcnn_trainer_context_destroy": (None, [c_void_p]),
     "tcnn_trainer_padded_output_width": (c_uint32, [c_void_p]),
+    "tcnn_workspace_allocate": (c_void_p, [c_void_p, c_uint64]),
+    "tcnn_workspace_free": (c_int, [c_void_p, c_void_p]),
+    "tcnn_free_workspace_arena": (c_int, [c_void_p]),
+    "tcnn_workspace_arena_info": (c_int, [c_void_p, c_void_p, c_void_p]),
     "tcnn_trainer_optimizer_step_range": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64]),
     "tcnn_trainer_training_step_part": (c_int, [c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_int]),
     "tcnn_trainer_loss": (c_float, [c_void_p, c_void_p]),

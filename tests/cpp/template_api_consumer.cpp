@@ -5,6 +5,7 @@
 #include <tiny-cuda-nn/common_device.h>
 
 #include <tiny-cuda-nn/config.h>
+#include <tiny-cuda-nn/multi_stream.h>
 
 #include <cmath>
 #include <cstdio>
@@ -85,6 +86,59 @@ int main(int argc, char** argv) {
 			EXPECT(v.data() == a.data());
 			auto t = a.transposed();
 			EXPECT(t.m() == 512 && t.n() == 3 && t.layout() == RM);
+		}
+		// workspace arena (gpu_memory.h:426-754): addresses survive growth, contents too; aligned
+		// distribution; intervals are reused after free; SyncedMultiStream fork / join (multi_stream.h)
+		{
+			hipStream_t s;
+			HIP_CHECK_THROW(hipStreamCreate(&s));
+			uint64_t mapped0 = 0;
+			int vmm = 0;
+			{
+				auto a = allocate_workspace(s, 1000);
+				EXPECT(a.data() != nullptr && ((uintptr_t)a.data() % 128) == 0);
+				HIP_CHECK_THROW(hipMemsetAsync(a.data(), 0x5a, 1000, s));
+				tcnn_workspace_arena_info(s, &mapped0, &vmm);
+				uint8_t* p0 = a.data();
+				auto big = allocate_workspace(s, (size_t)3 << 30);  // grows the arena by 3 GiB
+				uint64_t mapped1 = 0;
+				tcnn_workspace_arena_info(s, &mapped1, &vmm);
+				EXPECT(mapped1 >= ((uint64_t)3 << 30) && big.data() != nullptr);
+				EXPECT(a.data() == p0);  // the first allocation did not move
+				std::vector<uint8_t> h(1000);
+				HIP_CHECK_THROW(hipMemcpyAsync(h.data(), a.data(), 1000, hipMemcpyDeviceToHost, s));
+				HIP_CHECK_THROW(hipStreamSynchronize(s));
+				bool kept = true;
+				for (uint8_t v : h) kept = kept && v == 0x5a;
+				EXPECT(kept);
+				GPUMemoryArena::Allocation d;
+				float* f;
+				uint16_t* u;
+				double* x;
+				std::tie(f, u, x) = allocate_workspace_and_distribute<float, uint16_t, double>(s, &d, 3, 5, 7);
+				EXPECT(((uintptr_t)f % 128) == 0 && ((uintptr_t)u % 128) == 0 && ((uintptr_t)x % 128) == 0);
+				EXPECT((uint8_t*)u - (uint8_t*)f == 128 && (uint8_t*)x - (uint8_t*)u == 128);
+			}
+			{
+				auto r = allocate_workspace(s, 1000);  // everything was freed: the first interval again
+				EXPECT(r.data() != nullptr);
+			}
+			free_gpu_memory_arena(s);
+			std::printf("arena vmm=%d\n", vmm);
+			// fork / join: four streams each fill a quarter, the parent reads the whole after the join
+			GPUMemory<float> buf(4096);
+			{
+				SyncedMultiStream ms{s, 4};
+				for (size_t k = 0; k < 4; ++k) HIP_CHECK_THROW(hipMemsetD32Async((hipDeviceptr_t)(buf.data() + 1024 * k), 0x3f800000u * (k % 2) + 0x40000000u * (1 - k % 2), 1024, ms.get(k)));
+			}
+			std::vector<float> hb(4096);
+			HIP_CHECK_THROW(hipMemcpyAsync(hb.data(), buf.data(), 4096 * 4, hipMemcpyDeviceToHost, s));
+			HIP_CHECK_THROW(hipStreamSynchronize(s));
+			bool ok = true;
+			for (size_t i = 0; i < 4096; ++i) ok = ok && hb[i] == ((i / 1024) % 2 ? 1.0f : 2.0f);
+			EXPECT(ok);
+			free_multi_streams(s);
+			HIP_CHECK_THROW(hipStreamDestroy(s));
 		}
 		// create_from_config -> training_step / loss / inference (config.h:53-63)
 		const uint32_t B = 1 << 16;
