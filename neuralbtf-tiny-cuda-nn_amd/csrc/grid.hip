@@ -117,12 +117,27 @@ __global__ __launch_bounds__(256) void k_grid_fwd_aos_f2(uint32_t B, const float
 	}
 	// all 64 points in [0, 1]: the branch-free index (see grid_index_inrange)
 	const bool fast = o.inrange_index && !o.active && __builtin_amdgcn_ballot_w64(!inr) == 0;
-	for (uint32_t level = wave; level < L; level += 4) {
+	if (fast) {
+		// four levels per wave at a time with all their gathers in flight together (a level past L
+		// encodes level 0 into a discarded register, so the body has no branch to split the batch)
+		for (uint32_t l0 = 0; l0 < L; l0 += 16) {
+			h2 r[4];
+#pragma unroll
+			for (uint32_t k = 0; k < 4; ++k) {
+				const uint32_t level = l0 + wave + 4 * k;
+				r[k] = encode_level_f2_inrange<D, H>(table, levels[level < L ? level : 0], hash_grid != 0, x);
+			}
+#pragma unroll
+			for (uint32_t k = 0; k < 4; ++k) {
+				const uint32_t level = l0 + wave + 4 * k;
+				if (level < L) tile[lane * 65 + level] = valid ? __builtin_bit_cast(uint32_t, r[k]) : 0u;
+			}
+		}
+	}
+	for (uint32_t level = fast ? L : wave; level < L; level += 4) {
 		const LevelInfo li = levels[level];
 		h2 r = {(_Float16)0.0f, (_Float16)0.0f};
-		if (fast) {
-			if (valid) r = encode_level_f2_inrange<D, H>(table, li, hash_grid != 0, x);
-		} else if (valid && !(o.active && (float)level >= grid_max_level(o, i, 2) + 1e-3f)) {  // masked: 0 (grid.h:75-91)
+		if (valid && !(o.active && (float)level >= grid_max_level(o, i, 2) + 1e-3f)) {  // masked: 0 (grid.h:75-91)
 			r = encode_level_f2<D, H>(table, li, hash_grid != 0, interp, x);
 		}
 		tile[lane * 65 + level] = __builtin_bit_cast(uint32_t, r);

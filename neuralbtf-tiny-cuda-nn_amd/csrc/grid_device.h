@@ -203,37 +203,60 @@ __device__ __forceinline__ uint32_t grid_index_inrange(bool hash_grid, uint32_t 
 	return hashed ? (h & (size - 1)) : dm;
 }
 
-template <uint32_t D, HashType H>
-__device__ __forceinline__ h2 encode_level_f2_inrange(const uint32_t* __restrict__ table_u32, const LevelInfo& li, bool hash_grid,
-                                                      const float* x) {
-	float pos[D];
-	uint32_t pg[D];
-#pragma unroll
-	for (uint32_t d = 0; d < D; ++d) pos_fract(x[d], li.scale, Interp::Linear, pos[d], pg[d]);
-	constexpr uint32_t NC = 1u << D;
-	// grid_index_inrange per corner, with everything that does not depend on the corner hoisted to
-	// the level: per dimension the hash term pg*P and the dense term pg*res^d for both corner
-	// offsets ((pg + 1) * k = pg * k + k, also modulo 2^32). Under GridEncodingHost::inrange_index_ok
-	// a level whose index is used densely has res^D <= size (the stride loop never breaks), and its
-	// corner indices stay below 2 * size. The hashed / dense choice is per lane (lanes hold different
-	// levels), so it is a bit select on an opaque mask: written as a C select, the compiler sank the
-	// two index computations into divergent branches (exec-mask regions around every corner), which
-	// also kept it from issuing one level's gathers before the previous level's FMA chain.
+// What encode_level_f2_inrange needs of a level, independent of the point: computed once per level
+// and shared by every point a lane encodes at that level (the fused kernel's two sample tiles).
+template <uint32_t D>
+struct LevelConsts {
+	float scale;
+	uint32_t size, hmask, obytes, m;  // m: all ones where the level is hashed (see below)
+	uint32_t sd[D];                   // dense stride of each dimension (res^d)
+};
+
+// grid_index_inrange with everything that does not depend on the corner hoisted: per dimension the
+// hash term pg*P and the dense term pg*res^d for both corner offsets ((pg + 1) * k = pg * k + k, also
+// modulo 2^32). Under GridEncodingHost::inrange_index_ok a level whose index is used densely has
+// res^D <= size (the stride loop never breaks), and its corner indices stay below 2 * size. The
+// hashed / dense choice is per lane (lanes hold different levels), so it is a bit select on an
+// opaque mask: written as a C select, the compiler sank the two index computations into divergent
+// branches (exec-mask regions around every corner), which also kept it from issuing one level's
+// gathers before the previous level's FMA chain.
+template <uint32_t D>
+__device__ __forceinline__ LevelConsts<D> level_consts(const LevelInfo& li, bool hash_grid) {
+	LevelConsts<D> c;
 	uint32_t stride = 1;
 	bool brk = false;
-	uint32_t th[D][2], td[D][2];
 #pragma unroll
 	for (uint32_t d = 0; d < D; ++d) {
-		th[d][0] = pg[d] * hash_prime<H>(d);
-		th[d][1] = th[d][0] + hash_prime<H>(d);
-		td[d][0] = pg[d] * stride;
-		td[d][1] = td[d][0] + stride;
+		c.sd[d] = stride;
 		brk = brk || stride > li.size;  // the reference's stride loop (common_device.h:691-697)
 		stride = brk ? stride : stride * li.res;
 	}
 	uint32_t m = (hash_grid && li.size < stride) ? 0xffffffffu : 0u;
 	asm("" : "+v"(m));
-	const uint32_t hmask = li.size - 1, obytes = li.offset << 2;
+	c.m = m;
+	c.scale = li.scale;
+	c.size = li.size;
+	c.hmask = li.size - 1;
+	c.obytes = li.offset << 2;
+	return c;
+}
+
+template <uint32_t D, HashType H>
+__device__ __forceinline__ h2 encode_level_f2_inrange(const uint32_t* __restrict__ table_u32, const LevelConsts<D>& lc, const float* x) {
+	float pos[D];
+	uint32_t pg[D];
+#pragma unroll
+	for (uint32_t d = 0; d < D; ++d) pos_fract(x[d], lc.scale, Interp::Linear, pos[d], pg[d]);
+	constexpr uint32_t NC = 1u << D;
+	uint32_t th[D][2], td[D][2];
+#pragma unroll
+	for (uint32_t d = 0; d < D; ++d) {
+		th[d][0] = pg[d] * hash_prime<H>(d);
+		th[d][1] = th[d][0] + hash_prime<H>(d);
+		td[d][0] = pg[d] * lc.sd[d];
+		td[d][1] = td[d][0] + lc.sd[d];
+	}
+	const uint32_t m = lc.m, hmask = lc.hmask, obytes = lc.obytes;
 	uint32_t v[NC];
 	_Float16 w16[NC];
 #pragma unroll
@@ -247,7 +270,7 @@ __device__ __forceinline__ h2 encode_level_f2_inrange(const uint32_t* __restrict
 			h ^= th[d][b];
 			dn += td[d][b];
 		}
-		const uint32_t dm = __builtin_elementwise_min(dn, dn - li.size);  // dn % size for dn < 2 size
+		const uint32_t dm = __builtin_elementwise_min(dn, dn - lc.size);  // dn % size for dn < 2 size
 		uint32_t idx = ((h & hmask) & m) | (dm & ~m);
 #ifdef TCNN_DIAG_GATHER_MASK  // diagnostic builds only (wrong results): gathers confined to a few cache lines
 		idx &= TCNN_DIAG_GATHER_MASK;
@@ -262,6 +285,12 @@ __device__ __forceinline__ h2 encode_level_f2_inrange(const uint32_t* __restrict
 		r = pk_fma_f16(wv, __builtin_bit_cast(h2, v[c]), r);
 	}
 	return r;
+}
+
+template <uint32_t D, HashType H>
+__device__ __forceinline__ h2 encode_level_f2_inrange(const uint32_t* __restrict__ table_u32, const LevelInfo& li, bool hash_grid,
+                                                      const float* x) {
+	return encode_level_f2_inrange<D, H>(table_u32, level_consts<D>(li, hash_grid), x);
 }
 
 // F fp16 features of one table entry / one point-level

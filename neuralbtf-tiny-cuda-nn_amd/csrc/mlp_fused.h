@@ -692,17 +692,20 @@ __global__ __launch_bounds__(64 * FUSED_WAVES, 8 / FUSED_WAVES) void k_fused_tra
 		// next slice's positions one slice ahead (no change)
 		if constexpr (ENC_MEM) {
 		} else if (a.inrange_index && __builtin_amdgcn_ballot_w64(!inr) == 0) {
+			// level constants once per level, shared by the lane's two samples
 #pragma unroll
-			for (int tau = 0; tau < 2; ++tau)
+			for (int s = 0; s < KI; ++s)
 #pragma unroll
-				for (int s = 0; s < KI; ++s)
+				for (int pp = 0; pp < 4; ++pp) {
+					const int level = 16 * s + 8 * (pp >> 1) + 2 * q + (pp & 1);
+					const LevelConsts<D> lc = level_consts<D>(sLvl[level], hash_grid);
 #pragma unroll
-					for (int pp = 0; pp < 4; ++pp) {
-						const int level = 16 * s + 8 * (pp >> 1) + 2 * q + (pp & 1);
-						const h2 e = encode_level_f2_inrange<D, H>(a.table, sLvl[level], hash_grid, xs[tau]);
+					for (int tau = 0; tau < 2; ++tau) {
+						const h2 e = encode_level_f2_inrange<D, H>(a.table, lc, xs[tau]);
 						xt[tau][2 * s + (pp >> 1)][2 * (pp & 1) + 0] = e[0];
 						xt[tau][2 * s + (pp >> 1)][2 * (pp & 1) + 1] = e[1];
 					}
+				}
 		} else {
 #pragma unroll
 			for (int tau = 0; tau < 2; ++tau)

@@ -163,6 +163,11 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 	const f4 fz = {0.0f, 0.0f, 0.0f, 0.0f};
 	float* wloss = (float*)(smem + L::HALVES);
 	const bool ext = a.dout != nullptr;
+	// OP: the output rows are stored transposed 4 x 4 (out_row, mlp_fused.h), so lane group q holds
+	// output 4r + q in register r and the loss of a <= 4-output network runs once per lane instead of
+	// once per r (waves 0, 1 compute it while the other waves wait at the next barrier). Not for the
+	// W128 / >= 4 hidden-layer kernels, which sit at their 256-register bound and spill with it.
+	constexpr bool OP = !(W >= 128 && NH >= 4);
 
 	// ---- weights -> LDS (rows padded; first-layer columns [IN, KP0) and W16's padded neurons zero) ----
 	{
@@ -181,7 +186,7 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 		p += (NH - 1) * WR * WR;
 		for (int idx = tid; idx < 16 * (W / 8); idx += NTHR) {
 			const int r = idx / (W / 8), c8 = idx % (W / 8);
-			*(h8*)(smem + L::oWo + r * RSW + 8 * c8) = 8 * c8 < WR ? *(const h8*)(p + (size_t)r * WR + 8 * c8) : zero8();
+			*(h8*)(smem + L::oWo + (OP ? out_row(r) : r) * RSW + 8 * c8) = 8 * c8 < WR ? *(const h8*)(p + (size_t)r * WR + 8 * c8) : zero8();
 		}
 		// zero the padded input columns of slot 0 once (the input loads never write them)
 		if (L::KP0 > IN)
@@ -257,7 +262,14 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 		if (wave < 2) {
 			const uint32_t i = base + 16 * wave + c;
 			if (ext) {
-				gext = *(const h4*)(a.dout + (size_t)i * 16 + 4 * q);
+				if constexpr (OP) {
+					const _Float16* dp = a.dout + (size_t)i * 16 + q;
+					gext = h4{dp[0], dp[4], dp[8], dp[12]};
+				} else {
+					gext = *(const h4*)(a.dout + (size_t)i * 16 + 4 * q);
+				}
+			} else if constexpr (OP) {  // register 0 only: outputs 4.. of a wider network are read in the loss
+				if (q < (int)a.dims) tg[0] = a.target[(size_t)i * a.dims + q];
 			} else {
 #pragma unroll
 				for (int r = 0; r < 4; ++r)
@@ -319,18 +331,27 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 				y = mfma16(*(const h8*)(smem + L::oWo + c * RSW + 32 * s + 8 * q), *(const h8*)(aN + (16 * tau + c) * RSW + 32 * s + 8 * q), y);
 			const uint32_t i = base + 16 * tau + c;
 			const h4 yh = out_act_fwd(a.out_act, y);
-			if (a.out) *(h4*)(a.out + (size_t)i * 16 + 4 * q) = yh;
+			if (a.out) {
+				if constexpr (OP) {
+#pragma unroll
+					for (int r = 0; r < 4; ++r) a.out[(size_t)i * 16 + 4 * r + q] = yh[r];
+				} else {
+					*(h4*)(a.out + (size_t)i * 16 + 4 * q) = yh;
+				}
+			}
 			h4 g = zero4();
 			if (ext) {
 				g = gext;
 			} else {
 #pragma unroll
 				for (int r = 0; r < 4; ++r) {
-					const uint32_t o = 4 * q + r;
+					if (OP && 4u * r >= a.dims) break;  // wave-uniform: r = 0 only for <= 4 outputs
+					const uint32_t o = OP ? 4 * r + q : 4 * q + r;
 					if (o < a.dims) {
 						const float p = (float)yh[r];
 						const float pse = a.loss_l2 ? 1.0f : __builtin_fmaf(p, p, 0.01f);  // relative_l2.h:67-75 / l2.h:66-74
-						const float d = p - tg[r];
+						const float t = (!OP || r == 0) ? tg[r] : a.target[(size_t)(base + 16 * tau + c) * a.dims + o];
+						const float d = p - t;
 						loss += d * d / pse / a.n_total;
 						g[r] = f16_rn(a.loss_scale * (2.0f * d / pse) / a.n_total);
 					}
@@ -487,7 +508,7 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 	for (int i = 0; i < NTW; ++i)
 #pragma unroll
 		for (int r = 0; r < 4; ++r)
-			if (16 * (wave * NTW + i) + c < WR) dst[WR * IN + (NH - 1) * WR * WR + (4 * q + r) * WR + 16 * (wave * NTW + i) + c] = dWo[i][r];
+			if (16 * (wave * NTW + i) + c < WR) dst[WR * IN + (NH - 1) * WR * WR + (OP ? 4 * r + q : 4 * q + r) * WR + 16 * (wave * NTW + i) + c] = dWo[i][r];
 #pragma unroll
 	for (int off = 32; off > 0; off >>= 1) loss += __shfl_xor(loss, off);
 	if (lane == 0) wloss[wave] = loss;
