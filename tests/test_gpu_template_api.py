@@ -25,12 +25,18 @@ def test_template_headers_declare_reference_interface():
         "config.h": ["struct TrainableModel", "create_from_config(uint32_t n_input_dims, uint32_t n_output_dims, json config)"],
         "trainer.h": ["class Trainer", "struct ForwardContext", "training_step(hipStream_t stream", "float loss(hipStream_t stream",
                       "void optimizer_step(hipStream_t stream, float loss_scale)", "params_full_precision()",
-                      "set_params_full_precision(", "void update_hyperparams(const json& params)", "void initialize_params()"],
+                      "set_params_full_precision(", "void update_hyperparams(const json& params)", "void initialize_params()",
+                      "std::unique_ptr<ForwardContext> forward(hipStream_t stream, const float loss_scale",
+                      "void backward(hipStream_t stream, const ForwardContext& ctx"],
         "network_with_input_encoding.h": ["class NetworkWithInputEncoding", "void inference(hipStream_t stream",
                                           "padded_output_width()", "size_t n_params()"],
         "gpu_matrix.h": ["class GPUMatrixDynamic", "class GPUMatrix : public GPUMatrixDynamic<T>", "uint32_t m() const",
                          "uint32_t n() const", "transposed()"],
-        "gpu_memory.h": ["class GPUMemory", "void copy_from_host(", "void copy_to_host(", "void resize(", "size_t get_bytes()"],
+        "gpu_memory.h": ["class GPUMemory", "void copy_from_host(", "void copy_to_host(", "void resize(", "size_t get_bytes()",
+                         "class GPUMemoryArena", "class Allocation", "allocate_workspace(hipStream_t stream, size_t n_bytes)",
+                         "allocate_workspace_and_distribute(", "void free_gpu_memory_arena(hipStream_t stream)"],
+        "multi_stream.h": ["struct SyncedMultiStream", "SyncedMultiStream(hipStream_t stream, size_t n_streams)",
+                           "hipStream_t get(size_t idx)", "reserve_multi_stream(", "free_multi_streams("],
         "random.h": ["struct pcg32", "using default_rng_t = pcg32", "generate_random_uniform("],
         "common_device.h": ["linear_kernel(", "n_blocks_linear(", "N_THREADS_LINEAR"],
         "common.h": ["network_precision_t = __half", "BATCH_SIZE_GRANULARITY = 256", "enum class MatrixLayout",
