@@ -12,6 +12,7 @@
 namespace tcnn_amd {
 
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+typedef float f2v __attribute__((ext_vector_type(2)));
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -82,6 +83,21 @@ struct GridDesc {
 __device__ __forceinline__ _Float16 f16_rn(float x) {
 	asm("" : "+v"(x));
 	return (_Float16)x;
+}
+
+// N fp32 values (N even) -> fp16, each rounded once from its fp32 value, as pairs: a two-element
+// conversion selects v_cvt_pk_f16_f32, which hipcc does not fold with the producing multiplies into
+// a v_fma_mix (a lone scalar conversion of a product it does fold, even under `fp contract(off)`).
+// No asm barrier, so the producers stay free to schedule. tests/test_isa_rounding.py pins the result.
+template <uint32_t N>
+__device__ __forceinline__ void f16_rn_pairs(const float (&x)[N], _Float16 (&h)[N]) {
+	static_assert(N % 2 == 0, "pairs");
+#pragma unroll
+	for (uint32_t c = 0; c < N; c += 2) {
+		const h2 p = __builtin_convertvector((f2v){x[c], x[c + 1]}, h2);
+		h[c] = p[0];
+		h[c + 1] = p[1];
+	}
 }
 
 // Engine log (reference common_host.h:46-66: LogSeverity, log_callback, log_info/debug/warning).

@@ -56,6 +56,7 @@ __global__ __launch_bounds__(256) void k_grid_fwd(uint32_t B, const float* __res
 		constexpr uint32_t NC = 1u << D;
 		HVec<F> v[NC];
 		_Float16 w16[NC];
+		float wf[NC];
 #pragma unroll
 		for (uint32_t c = 0; c < NC; ++c) {
 			float w = 1.0f;
@@ -65,9 +66,10 @@ __global__ __launch_bounds__(256) void k_grid_fwd(uint32_t B, const float* __res
 				if ((c & (1u << d)) == 0) { w *= 1.0f - p[d]; local[d] = pg[d]; }
 				else { w *= p[d]; local[d] = pg[d] + 1; }
 			}
-			w16[c] = (_Float16)w;  // v_cvt_f16_f32, see encode_level_f2 (tests/test_isa_rounding.py)
+			wf[c] = w;  // converted in pairs, see encode_level_f2 (tests/test_isa_rounding.py)
 			v[c] = tv[li.offset + grid_index<D, H>(hash_grid != 0, li.size, li.res, local)];
 		}
+		f16_rn_pairs(wf, w16);
 		// packed fp16 FMA (v_pk_fma_f16: one rounding, = CUDA __hfma2 of grid.h:162); the scalar
 		// _Float16 fma is lowered through fp32 and would double-round.
 #pragma unroll

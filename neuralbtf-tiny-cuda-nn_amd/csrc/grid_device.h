@@ -13,15 +13,12 @@
 
 namespace tcnn_amd {
 
-// Packed fp16 FMA with ONE rounding (CUDA __hfma2 semantics, reference grid.h:162 / vec.h:370-376).
-// Pinned as v_pk_fma_f16: left to itself hipcc may select v_fma_mix{lo,hi}_f16, whose fp32-internal
-// result is rounded twice and differs from __hfma2 in ~1e-5 of cases.
-__device__ __forceinline__ h2 pk_fma_f16(h2 a, h2 b, h2 c) {
-	uint32_t r;
-	asm("v_pk_fma_f16 %0, %1, %2, %3" : "=v"(r) : "v"(__builtin_bit_cast(uint32_t, a)), "v"(__builtin_bit_cast(uint32_t, b)),
-	    "v"(__builtin_bit_cast(uint32_t, c)));
-	return __builtin_bit_cast(h2, r);
-}
+// Packed fp16 FMA with ONE rounding (CUDA __hfma2 semantics, reference grid.h:162 / vec.h:370-376):
+// llvm.fma on <2 x half> is single-rounded by definition, so hipcc must select v_pk_fma_f16 (the
+// double-rounding v_fma_mix forms only arise from fp32 arithmetic truncated to fp16, which this
+// is not; tests/test_isa_rounding.py rejects any mix form in the library). No inline asm: the
+// compiler sees the instruction and pads its MFMA hazards itself (tests/test_isa_hazards.py).
+__device__ __forceinline__ h2 pk_fma_f16(h2 a, h2 b, h2 c) { return __builtin_elementwise_fma(a, b, c); }
 
 struct LevelInfo {
 	float scale;
@@ -156,6 +153,7 @@ __device__ __forceinline__ h2 encode_level_f2(const uint32_t* __restrict__ table
 	constexpr uint32_t NC = 1u << D;
 	uint32_t v[NC];
 	_Float16 w16[NC];
+	float wf[NC];
 #pragma unroll
 	for (uint32_t c = 0; c < NC; ++c) {
 		float w = 1.0f;
@@ -165,12 +163,13 @@ __device__ __forceinline__ h2 encode_level_f2(const uint32_t* __restrict__ table
 			if ((c & (1u << d)) == 0) { w *= 1.0f - pos[d]; local[d] = pg[d]; }
 			else { w *= pos[d]; local[d] = pg[d] + 1; }
 		}
-		// plain conversion: the compiler emits v_cvt_f16_f32 here (no fused mix rounding; pinned for
-		// every kernel by tests/test_isa_rounding.py), and the f16_rn barrier costs the fused kernel
-		// ~10% by serialising the weight / gather schedule
-		w16[c] = (_Float16)w;
+		// converted in pairs below (f16_rn_pairs: v_cvt_pk_f16_f32, no fused mix rounding; pinned for
+		// every kernel by tests/test_isa_rounding.py); an f16_rn barrier per weight costs the fused
+		// kernel ~10% by serialising the weight / gather schedule
+		wf[c] = w;
 		v[c] = table_u32[li.offset + grid_index<D, H>(hash_grid, li.size, li.res, local)];
 	}
+	f16_rn_pairs(wf, w16);
 	h2 r = {(_Float16)0.0f, (_Float16)0.0f};
 #pragma unroll
 	for (uint32_t c = 0; c < NC; ++c) {
@@ -259,6 +258,7 @@ __device__ __forceinline__ h2 encode_level_f2_inrange(const uint32_t* __restrict
 	const uint32_t m = lc.m, hmask = lc.hmask, obytes = lc.obytes;
 	uint32_t v[NC];
 	_Float16 w16[NC];
+	float wf[NC];
 #pragma unroll
 	for (uint32_t c = 0; c < NC; ++c) {
 		float w = 1.0f;
@@ -275,9 +275,10 @@ __device__ __forceinline__ h2 encode_level_f2_inrange(const uint32_t* __restrict
 #ifdef TCNN_DIAG_GATHER_MASK  // diagnostic builds only (wrong results): gathers confined to a few cache lines
 		idx &= TCNN_DIAG_GATHER_MASK;
 #endif
-		w16[c] = (_Float16)w;  // as encode_level_f2
+		wf[c] = w;  // as encode_level_f2
 		v[c] = *(const uint32_t*)((const char*)table_u32 + (obytes + (idx << 2)));
 	}
+	f16_rn_pairs(wf, w16);
 	h2 r = {(_Float16)0.0f, (_Float16)0.0f};
 #pragma unroll
 	for (uint32_t c = 0; c < NC; ++c) {

@@ -38,17 +38,16 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ h4 zero4() { return h4{(_Float16)0.0f, (_Float16)0.0f, (_Float16)0.0f, (_Float16)0.0f}; }
 
 // ReLU on the fp16-rounded accumulator, the reference's own order (relu<half> = __hmax(val, 0) on
-// the fp16 fragment, common_device.h:90-97): v_pk_max_f16 with 0 as the first operand, one packed
-// instruction per two values (max(0, -0) = +0 and max(0, NaN) = 0 on gfx950: tools/relu_probe.hip).
-// Rounding first then clamping equals clamping then rounding (the rounding is monotone and
-// fixes 0). As fp32 C code (v > 0 ? v : 0) the compiler emitted two v_max_f32 per value (a
-// canonicalising one first); as asm on the fp32 value it would read the MFMA result registers,
-// whose read-after-MFMA hazard the compiler does not pad for inline asm -- the cvt in between is an
-// ordinary instruction, so the asm here only reads VALU results.
+// the fp16 fragment, common_device.h:90-97): v_pk_max_f16, one packed instruction per two values.
+// Rounding first then clamping equals clamping then rounding (the rounding is monotone and fixes 0).
+// maxnum leaves the sign of a zero result open (max(-0, +0) may be either), and act_bwd below tests
+// "bits != 0", so the sign bit is cleared afterwards: the result is x for x > 0 and +0 otherwise
+// (NaN -> +0, as __hmax(NaN, 0) = 0). Written with builtins, not inline asm: as asm, hipcc neither
+// saw nor padded the instruction's MFMA hazards (an asm v_pk_max_f16 fed an MFMA B operand one wait
+// state after writing it, where gfx950 requires two; tools/hazard_scan.py, tests/test_isa_hazards.py).
 __device__ __forceinline__ uint32_t relu_pk_f16(uint32_t x) {
-	uint32_t r;
-	asm("v_pk_max_f16 %0, 0, %1" : "=v"(r) : "v"(x));
-	return r;
+	const h2 m = __builtin_elementwise_max(__builtin_bit_cast(h2, x), (h2){(_Float16)0.0f, (_Float16)0.0f});
+	return __builtin_bit_cast(uint32_t, m) & 0x7fff7fffu;
 }
 template <Act A>
 __device__ __forceinline__ h4 act_fwd(f4 v) {
@@ -65,15 +64,16 @@ __device__ __forceinline__ h4 act_fwd(f4 v) {
 // activation transfer given the post-activation value (reference common_device.h:240-297).
 // ReLU: fwd > 0 ? g : 0. act_fwd only produces +0 or positive values (never -0 or NaN), so the test
 // is "fwd bits != 0", done on packed u16 lanes: r * min(bits, 1) keeps both halves of a register
-// packed. Written as inline asm (two packed VALU per register): from the equivalent C the compiler
-// proves the operand is an fp16 value, turns "bits != 0" into an fp16 class test and lowers that
-// per half through ~10 SDWA compares + SALU mask ops (r03 ISA: 320 16-bit compares, ~40 % of the
-// fused kernel's MLP instructions).
+// packed (v_pk_min_u16 + v_pk_mul_lo_u16). The constant 1 goes through an empty asm statement (no
+// instruction, no hazard): when the compiler can see it, it proves the operand is an fp16 value,
+// turns "bits != 0" into an fp16 class test and lowers that per half through ~10 SDWA compares +
+// SALU mask ops (r03 ISA: 320 16-bit compares, ~40 % of the fused kernel's MLP instructions).
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t relu_mask_pk(uint32_t r, uint32_t fwd) {
-	uint32_t t;
-	asm("v_pk_min_u16 %0, %1, %2" : "=v"(t) : "v"(fwd), "s"(0x00010001u));
-	asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(r) : "v"(r), "v"(t));
-	return r;
+	uint32_t one = 0x00010001u;
+	asm("" : "+s"(one));
+	const u16x2 t = __builtin_elementwise_min(__builtin_bit_cast(u16x2, fwd), __builtin_bit_cast(u16x2, one));
+	return __builtin_bit_cast(uint32_t, (u16x2)(__builtin_bit_cast(u16x2, r) * t));
 }
 template <Act A>
 __device__ __forceinline__ h4 act_bwd(h4 fwd, f4 g) {

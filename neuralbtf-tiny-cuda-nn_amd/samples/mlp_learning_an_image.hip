@@ -19,7 +19,10 @@
 //
 // Test hooks (not in the reference): TCNN_SAMPLE_SEED replaces the batch RNG's seed 1337 and
 // TCNN_SAMPLE_TRAINER_SEED the Trainer's parameter seed 1337 (tests/test_gpu_render_pin.py measures
-// the seed-to-seed spread of the render PSNR with them).
+// the seed-to-seed spread of the render PSNR with them); TCNN_SAMPLE_TEX_ROUND = rint (default) |
+// trunc | exact selects how the bilinear fraction is held (the texture unit's 8 fractional bits,
+// rounded or truncated, or fp32) and TCNN_SAMPLE_LOG2_BATCH replaces the batch size 2^18
+// (tools/render_sweep.py varies them to look for the reference run's pipeline).
 #include <tiny-cuda-nn/common_device.h>
 
 #include <tiny-cuda-nn/config.h>
@@ -85,7 +88,14 @@ void save_image(const T* image, int width, int height, int n_channels, int chann
 struct ImageTexture {
 	const float4* data;
 	int width, height;
+	int round_mode;  // 0: rint to 1/256 (default), 1: truncate to 1/256, 2: fp32 fraction (test hook)
 };
+
+__device__ inline float tex_fraction(float f, int mode) {
+	if (mode == 1) return floorf(f * 256.0f) * (1.0f / 256.0f);
+	if (mode == 2) return f;
+	return rintf(f * 256.0f) * (1.0f / 256.0f);
+}
 
 // tex2D<float4>(texture, u, v) with cudaFilterModeLinear, normalizedCoords, cudaAddressModeClamp:
 // x_B = u * width - 0.5, i = floor(x_B), alpha = frac(x_B), tex = (1-a)(1-b) T[i,j] + a(1-b) T[i+1,j]
@@ -95,7 +105,7 @@ struct ImageTexture {
 __device__ inline float4 sample_bilinear(const ImageTexture& t, float u, float v) {
 	const float x = u * t.width - 0.5f, y = v * t.height - 0.5f;
 	const float fx = floorf(x), fy = floorf(y);
-	const float ax = rintf((x - fx) * 256.0f) * (1.0f / 256.0f), ay = rintf((y - fy) * 256.0f) * (1.0f / 256.0f);
+	const float ax = tex_fraction(x - fx, t.round_mode), ay = tex_fraction(y - fy, t.round_mode);
 	const int x0 = min(max((int)fx, 0), t.width - 1), x1 = min(max((int)fx + 1, 0), t.width - 1);
 	const int y0 = min(max((int)fy, 0), t.height - 1), y1 = min(max((int)fy + 1, 0), t.height - 1);
 	const float4 a = t.data[y0 * t.width + x0], b = t.data[y0 * t.width + x1];
@@ -151,7 +161,10 @@ int main(int argc, char* argv[]) {
 		GPUMemory<float> image = load_image(argv[1], width, height);
 
 		// Second step: the image as a bilinear "texture", used to generate training data on the fly
-		ImageTexture texture{(const float4*)image.data(), width, height};
+		const char* round_env = std::getenv("TCNN_SAMPLE_TEX_ROUND");  // test hook, see the header
+		const std::string round_mode = round_env ? round_env : "rint";
+		if (round_mode != "rint" && round_mode != "trunc" && round_mode != "exact") throw std::runtime_error{"TCNN_SAMPLE_TEX_ROUND: rint | trunc | exact"};
+		ImageTexture texture{(const float4*)image.data(), width, height, round_mode == "rint" ? 0 : round_mode == "trunc" ? 1 : 2};
 
 		// Third step: sample a reference image to dump to disk
 		int sampling_width = width;
@@ -179,7 +192,8 @@ int main(int argc, char* argv[]) {
 		save_image(sampled_image.data(), sampling_width, sampling_height, 3, 3, "reference.ppm");
 
 		// Fourth step: train the model by sampling the above image and optimizing an error metric
-		const uint32_t batch_size = 1 << 18;
+		const char* batch_env = std::getenv("TCNN_SAMPLE_LOG2_BATCH");  // test hook, see the header
+		const uint32_t batch_size = 1u << (batch_env ? std::atoi(batch_env) : 18);
 		const uint32_t n_training_steps = argc >= 4 ? atoi(argv[3]) : 10000000;
 		const uint32_t n_input_dims = 2;   // 2-D image coordinate
 		const uint32_t n_output_dims = 3;  // RGB color
