@@ -8,6 +8,13 @@
 // virtual memory management it falls back to one hipMalloc'd buffer that is re-allocated (and
 // copied) 1.5x larger, as the reference's fallback does. Allocations are 128-byte aligned
 // intervals, first fit, freed intervals merged.
+//
+// Lifetime as the reference's shared_ptr<GPUMemoryArena> (gpu_memory.h:690-760): free_gpu_memory_arena
+// and free_all_gpu_memory_arenas detach arenas from their streams; a detached arena lives on until its
+// last allocation is freed. An arena is built on the device its stream belongs to. Growth never
+// synchronises on the VMM path (mapping is complete when hipMemSetAccess returns, and queued work
+// cannot touch the new range), so allocating while a stream is being captured is legal there; the
+// fallback's copy-to-a-larger-buffer needs the device idle and refuses under capture.
 #include <algorithm>
 #include <map>
 #include <memory>
@@ -35,8 +42,7 @@ struct Arena {
 	std::vector<void*> old_bufs;                    // fallback: earlier buffers, kept for live pointers
 	std::unordered_map<const void*, size_t> offset_of;  // live pointer -> interval start
 
-	Arena() {
-		TCNN_HIP_CHECK(hipGetDevice(&device));
+	explicit Arena(int dev) : device(dev) {
 		int vm = 0;
 		hipDeviceGetAttribute(&vm, hipDeviceAttributeVirtualMemoryManagementSupported, device);
 		size_t free_b = 0, total_b = 0;
@@ -64,6 +70,12 @@ struct Arena {
 		free_iv[0] = max_size;
 	}
 	~Arena() {
+		// queued work may still use the memory (the reference frees with the same caveat); an arena is
+		// destroyed only when detached and empty, never under capture
+		int cur = 0;
+		hipGetDevice(&cur);
+		hipSetDevice(device);
+		hipDeviceSynchronize();
 		if (vmm) {
 			for (auto& m : mapped) hipMemUnmap(base + m.first, m.second);
 			for (auto h : handles) hipMemRelease(h);
@@ -72,13 +84,18 @@ struct Arena {
 			if (base) hipFree(base);
 			for (void* b : old_bufs) hipFree(b);
 		}
+		hipSetDevice(cur);
 	}
 	bool in_use() const { return !used.empty(); }
 
-	void enlarge(size_t n_bytes) {  // gpu_memory.h:510-561
+	void enlarge(size_t n_bytes, hipStream_t st) {  // gpu_memory.h:510-601
 		if (n_bytes <= size) return;
-		TCNN_HIP_CHECK(hipDeviceSynchronize());  // queued work may still read the old fallback buffer
 		if (!vmm) {
+			hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+			if (st) TCNN_HIP_CHECK(hipStreamIsCapturing(st, &cs));
+			TCNN_CHECK(cs == hipStreamCaptureStatusNone,
+			           "GPUMemoryArena: growing the fallback arena (no virtual memory support) under stream capture");
+			TCNN_HIP_CHECK(hipDeviceSynchronize());  // queued work may still read the old buffer
 			const size_t ns = (size_t)(n_bytes * 1.5 + gran - 1) / gran * gran;
 			void* p = nullptr;
 			TCNN_HIP_CHECK(hipMalloc(&p, ns));
@@ -92,19 +109,21 @@ struct Arena {
 		}
 		const size_t add = (n_bytes - size + gran - 1) / gran * gran;
 		// mapped as chunks of at most MAX_CHUNK (a chunk whose map or access fails is retried as
-		// granularity-sized pieces)
+		// granularity-sized pieces); `size` advances with every mapped piece, so a failure part-way
+		// leaves the arena consistent (the mapped prefix is kept and reused by the next growth)
 		constexpr size_t MAX_CHUNK = (size_t)256 << 20;
-		size_t done = 0;
-		while (done < add) {
-			const size_t want = std::min(MAX_CHUNK, add - done);
-			if (!map_chunk(size + done, want)) {
-				for (size_t o = 0; o < want; o += gran)
-					if (!map_chunk(size + done + o, gran)) throw std::runtime_error("GPUMemoryArena: mapping device memory failed");
+		const size_t target = size + add;
+		while (size < target) {
+			const size_t want = std::min(MAX_CHUNK, target - size);
+			if (map_chunk(size, want)) {
+				size += want;
+				continue;
 			}
-			done += want;
+			for (size_t o = 0; o < want; o += gran) {
+				if (!map_chunk(size, gran)) throw std::runtime_error("GPUMemoryArena: mapping device memory failed");
+				size += gran;
+			}
 		}
-		size += add;
-		TCNN_HIP_CHECK(hipDeviceSynchronize());
 	}
 
 	bool map_chunk(size_t off, size_t bytes) {
@@ -133,15 +152,15 @@ struct Arena {
 		return true;
 	}
 
-	size_t allocate(size_t n) {  // gpu_memory.h:563-592: first fit
+	size_t allocate(size_t n, hipStream_t st) {  // gpu_memory.h:563-592: first fit
 		n = std::max<size_t>((n + ARENA_ALIGN - 1) / ARENA_ALIGN * ARENA_ALIGN, ARENA_ALIGN);
 		for (auto it = free_iv.begin(); it != free_iv.end(); ++it) {
 			if (it->second - it->first < n) continue;
 			const size_t start = it->first, end = it->second;
+			enlarge(start + n, st);  // may throw: the interval lists are untouched until it succeeded
 			free_iv.erase(it);
 			if (start + n < end) free_iv[start + n] = end;
 			used[start] = n;
-			enlarge(start + n);
 			return start;
 		}
 		throw std::runtime_error("GPUMemoryArena: out of memory");
@@ -170,19 +189,24 @@ struct Arena {
 
 struct Arenas {
 	std::mutex mu;
-	std::unordered_map<hipStream_t, std::unique_ptr<Arena>> by_stream;
-	std::unordered_map<int, std::unique_ptr<Arena>> by_device;  // the null stream
-	Arena& get(hipStream_t st) {
+	std::unordered_map<hipStream_t, std::shared_ptr<Arena>> by_stream;
+	std::unordered_map<int, std::shared_ptr<Arena>> by_device;  // the null stream
+	std::unordered_map<const void*, std::shared_ptr<Arena>> owner;  // live allocation -> its arena
+	std::shared_ptr<Arena>& get(hipStream_t st) {
 		if (st) {
 			auto& a = by_stream[st];
-			if (!a) a = std::make_unique<Arena>();
-			return *a;
+			if (!a) {
+				int dev = 0;
+				TCNN_HIP_CHECK(hipStreamGetDevice(st, &dev));  // the stream's device, not the current one
+				a = std::make_shared<Arena>(dev);
+			}
+			return a;
 		}
 		int d = 0;
 		TCNN_HIP_CHECK(hipGetDevice(&d));
 		auto& a = by_device[d];
-		if (!a) a = std::make_unique<Arena>();
-		return *a;
+		if (!a) a = std::make_shared<Arena>(d);
+		return a;
 	}
 };
 
@@ -197,47 +221,82 @@ void* workspace_allocate(hipStream_t st, size_t n_bytes) {
 	if (n_bytes == 0) return nullptr;
 	Arenas& A = arenas();
 	std::lock_guard<std::mutex> lk(A.mu);
-	Arena& a = A.get(st);
-	const size_t off = a.allocate(n_bytes);
-	a.offset_of[a.base + off] = off;
-	return a.base + off;
+	std::shared_ptr<Arena> a = A.get(st);
+	int cur = 0;
+	TCNN_HIP_CHECK(hipGetDevice(&cur));
+	if (cur != a->device) TCNN_HIP_CHECK(hipSetDevice(a->device));
+	size_t off = 0;
+	try {
+		off = a->allocate(n_bytes, st);
+	} catch (...) {
+		if (cur != a->device) hipSetDevice(cur);
+		throw;
+	}
+	if (cur != a->device) TCNN_HIP_CHECK(hipSetDevice(cur));
+	void* p = a->base + off;
+	a->offset_of[p] = off;
+	A.owner[p] = a;
+	return p;
 }
 
 void workspace_free(hipStream_t st, void* p) {
+	(void)st;  // the allocation knows its arena (which may have been detached from the stream since)
 	if (!p) return;
 	Arenas& A = arenas();
-	std::lock_guard<std::mutex> lk(A.mu);
-	Arena& a = A.get(st);
-	auto it = a.offset_of.find(p);
-	TCNN_CHECK(it != a.offset_of.end(), "GPUMemoryArena: freeing an address that this stream's arena did not allocate");
-	a.release(it->second);
-	a.offset_of.erase(it);
+	std::shared_ptr<Arena> a;
+	{
+		std::lock_guard<std::mutex> lk(A.mu);
+		auto o = A.owner.find(p);
+		TCNN_CHECK(o != A.owner.end(), "GPUMemoryArena: freeing an address that no arena allocated");
+		a = std::move(o->second);
+		A.owner.erase(o);
+		auto it = a->offset_of.find(p);
+		a->release(it->second);
+		a->offset_of.erase(it);
+	}
+	// `a` going out of scope here destroys a detached arena whose last allocation this was
 }
 
-void workspace_arena_free(hipStream_t st) {  // free_gpu_memory_arena (gpu_memory.h:743-754)
+// free_gpu_memory_arena (gpu_memory.h:743-749): detach the stream's arena; it is destroyed now if it
+// has no live allocations, else when its last one is freed
+void workspace_arena_free(hipStream_t st) {
 	Arenas& A = arenas();
-	std::lock_guard<std::mutex> lk(A.mu);
-	if (st) {
-		auto it = A.by_stream.find(st);
-		if (it == A.by_stream.end()) return;
-		TCNN_CHECK(!it->second->in_use(), "free_gpu_memory_arena: the arena still has live allocations");
-		TCNN_HIP_CHECK(hipStreamSynchronize(st));
-		A.by_stream.erase(it);
-	} else {
-		int d = 0;
-		TCNN_HIP_CHECK(hipGetDevice(&d));
-		auto it = A.by_device.find(d);
-		if (it == A.by_device.end()) return;
-		TCNN_CHECK(!it->second->in_use(), "free_gpu_memory_arena: the arena still has live allocations");
-		TCNN_HIP_CHECK(hipDeviceSynchronize());
-		A.by_device.erase(it);
+	std::shared_ptr<Arena> drop;
+	{
+		std::lock_guard<std::mutex> lk(A.mu);
+		if (st) {
+			auto it = A.by_stream.find(st);
+			if (it == A.by_stream.end()) return;
+			drop = std::move(it->second);
+			A.by_stream.erase(it);
+		} else {
+			int d = 0;
+			TCNN_HIP_CHECK(hipGetDevice(&d));
+			auto it = A.by_device.find(d);
+			if (it == A.by_device.end()) return;
+			drop = std::move(it->second);
+			A.by_device.erase(it);
+		}
+	}
+}
+
+// free_all_gpu_memory_arenas (gpu_memory.h:751-754)
+void workspace_arena_free_all() {
+	Arenas& A = arenas();
+	std::vector<std::shared_ptr<Arena>> drop;
+	{
+		std::lock_guard<std::mutex> lk(A.mu);
+		for (auto& kv : A.by_stream) drop.push_back(std::move(kv.second));
+		for (auto& kv : A.by_device) drop.push_back(std::move(kv.second));
+		A.by_stream.clear();
+		A.by_device.clear();
 	}
 }
 
 void workspace_arena_info(hipStream_t st, uint64_t* mapped_bytes, int* vmm) {
 	Arenas& A = arenas();
 	std::lock_guard<std::mutex> lk(A.mu);
-	Arena& a = A.get(st);
+	Arena& a = *A.get(st);
 	if (mapped_bytes) *mapped_bytes = a.size;
 	if (vmm) *vmm = a.vmm ? 1 : 0;
 }

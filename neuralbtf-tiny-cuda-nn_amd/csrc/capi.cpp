@@ -273,7 +273,12 @@ int tcnn_cuda_device(void) {
 int tcnn_set_cuda_device(int device) {
 	return guard([&] { TCNN_HIP_CHECK(hipSetDevice(device)); });
 }
-void tcnn_free_temporary_memory(void) {}
+void tcnn_free_temporary_memory(void) {  // free_all_gpu_memory_arenas (gpu_memory.h:751-754)
+	try {
+		tcnn_amd::workspace_arena_free_all();
+	} catch (...) {
+	}
+}
 int tcnn_has_networks(void) { return 1; }
 
 int tcnn_generate_random_uniform(void* stream, uint64_t* rng_state, uint64_t* rng_inc, uint64_t n, float* out, float lower, float upper) {
@@ -514,7 +519,9 @@ int tcnn_trainer_optimizer_state(tcnn_trainer* t, float** m1, float** m2, uint32
 	return 0;
 }
 int tcnn_trainer_set_gradient_scale(tcnn_trainer* t, float s) {
-	t->t->grad_scale = s;
+	TrainerHost& h = *t->t;
+	h.grad_scale_user = s;
+	h.grad_scale = s * (h.dp ? 1.0f / (float)h.dp->nranks : 1.0f);
 	return 0;
 }
 int tcnn_trainer_set_graph(tcnn_trainer* t, int on) {

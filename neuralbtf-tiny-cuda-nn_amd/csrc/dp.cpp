@@ -114,11 +114,18 @@ static void grow_preserve(DevBuf& b, size_t bytes, size_t valid) {
 }
 
 void TrainerHost::set_dp(DpComm* c, bool sharded) {
+	// Leaving a sharded schedule (detach, re-attach, or switch to replicated) first completes every
+	// rank's fp32 masters, Adam moments and step counts over the OLD communicator -- otherwise the next
+	// step's Adam would run on state that is stale outside this rank's shard and overwrite the gathered
+	// fp16 weights of the other shards. This makes set_dp collective whenever state is partial: every
+	// rank of the old communicator calls it (as every rank calls the sharded step).
+	if (dp && dp_sharded && dp_state_partial) dp_gather_state(nullptr);
 	TCNN_HIP_CHECK(hipDeviceSynchronize());
 	dp = c;
 	dp_sharded = c && sharded;
 	dp_state_partial = false;
-	grad_scale = c ? 1.0f / (float)c->nranks : 1.0f;
+	// Adam reads the SUM over ranks: the caller's own scale (tcnn_trainer_set_gradient_scale) times 1/N
+	grad_scale = grad_scale_user * (c ? 1.0f / (float)c->nranks : 1.0f);
 	if (graph) set_graph(use_graph);  // drop captured graphs (their keys do not hold the exchange)
 	if (!dp_sharded) return;
 	// shard s owns parameters [s per, (s + 1) per); every per-parameter buffer is padded to N per so

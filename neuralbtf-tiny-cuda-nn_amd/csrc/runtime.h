@@ -303,6 +303,7 @@ struct TrainerFwdCtx {
 void* workspace_allocate(hipStream_t st, size_t n_bytes);
 void workspace_free(hipStream_t st, void* p);
 void workspace_arena_free(hipStream_t st);
+void workspace_arena_free_all();
 void workspace_arena_info(hipStream_t st, uint64_t* mapped_bytes, int* vmm);
 
 struct TrainerHost {
@@ -326,7 +327,8 @@ struct TrainerHost {
 	AdamArgs adam_args_table(hipStream_t st, uint32_t upto, uint32_t reserve = 0);
 	StepWorkspace ws;
 	uint32_t adam_step = 0;
-	float grad_scale = 1.0f;
+	float grad_scale = 1.0f;       // what Adam multiplies the fp32 gradient sum by
+	float grad_scale_user = 1.0f;  // the caller's factor (tcnn_trainer_set_gradient_scale); x 1/N under set_dp
 	float loss_scale = 128.0f;  // default_loss_scale<__half> (common.h:232)
 	uint32_t last_B = 0;
 	// two-launch single-GPU step: reductions + Adam fused into the grid backward's epilogue

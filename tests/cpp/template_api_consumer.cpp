@@ -125,6 +125,37 @@ int main(int argc, char** argv) {
 			}
 			free_gpu_memory_arena(s);
 			std::printf("arena vmm=%d\n", vmm);
+			// growth while the stream is being captured (the reference defers its synchronisation to the
+			// capture, gpu_memory.h:596-601; the VMM arena needs none): the graph writes the new memory
+			if (vmm) {
+				hipGraph_t g;
+				hipGraphExec_t ge;
+				HIP_CHECK_THROW(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+				auto grown = allocate_workspace(s, (size_t)1 << 30);
+				HIP_CHECK_THROW(hipMemsetAsync(grown.data(), 0x7b, 4096, s));
+				HIP_CHECK_THROW(hipStreamEndCapture(s, &g));
+				HIP_CHECK_THROW(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+				HIP_CHECK_THROW(hipGraphLaunch(ge, s));
+				std::vector<uint8_t> h(4096);
+				HIP_CHECK_THROW(hipMemcpyAsync(h.data(), grown.data(), 4096, hipMemcpyDeviceToHost, s));
+				HIP_CHECK_THROW(hipStreamSynchronize(s));
+				bool ok = true;
+				for (uint8_t v : h) ok = ok && v == 0x7b;
+				EXPECT(ok);
+				HIP_CHECK_THROW(hipGraphExecDestroy(ge));
+				HIP_CHECK_THROW(hipGraphDestroy(g));
+			}
+			// detaching an arena that still has a live allocation (free_gpu_memory_arena of the reference
+			// drops its shared_ptr; the allocation keeps the arena alive and frees into it later)
+			{
+				auto live = allocate_workspace(s, 1 << 20);
+				free_gpu_memory_arena(s);
+				HIP_CHECK_THROW(hipMemsetAsync(live.data(), 0, 1 << 20, s));
+				HIP_CHECK_THROW(hipStreamSynchronize(s));
+				auto fresh = allocate_workspace(s, 1 << 20);  // a new arena for the same stream
+				EXPECT(fresh.data() != nullptr && fresh.data() != live.data());
+			}
+			free_all_gpu_memory_arenas();
 			// fork / join: four streams each fill a quarter, the parent reads the whole after the join
 			GPUMemory<float> buf(4096);
 			{

@@ -65,3 +65,26 @@ def test_engine_dp_one_rank_equals_plain_step(group, sharded, graph):
         caps, reps = t.graph_stats()
         assert caps >= 1 and reps >= 1, (caps, reps)
     t.set_dp(None)
+
+
+def test_detach_after_sharded_steps_keeps_state_and_scale(group):
+    """Detaching a sharded trainer (set_dp(None)) with partial state completes the state first
+    (csrc/dp.cpp set_dp), so local steps afterwards continue the same trajectory; the
+    caller's gradient scale survives attach / detach (x 1/N only while attached)."""
+    torch = group
+    from tinycudann import Trainer
+    from tinycudann.parallel import EngineComm
+    comm = EngineComm()
+    ref = Trainer(2, 3, CONFIG_HASH, seed=1337)
+    t = Trainer(2, 3, CONFIG_HASH, seed=1337)
+    t.set_dp(comm, sharded=True)
+    B = 4096
+    for s in range(6):
+        pos, tgt = make_batch(B, step=s)
+        p, g = torch.from_numpy(pos).cuda(), torch.from_numpy(tgt).cuda()
+        ref.training_step(p, g)
+        if s == 3:
+            t.set_dp(None)  # no explicit gather: set_dp must complete the sharded state itself
+        t.training_step(p, g)
+        assert t.loss() == ref.loss(), s
+    assert t.serialize(optimizer=True) == ref.serialize(optimizer=True)
