@@ -145,8 +145,10 @@ int tcnn_trainer_optimizer_step(tcnn_trainer* t, void* stream);
 typedef struct tcnn_trainer_context tcnn_trainer_context;  /* Trainer::ForwardContext (trainer.h:89-95) */
 tcnn_trainer_context* tcnn_trainer_forward(tcnn_trainer* t, void* stream, uint32_t n, const float* input, const float* target,
                                            const float* data_pdf, const void* external_dL_dy, int prepare_input_gradients);
+/* gradient_mode: GradientMode (common.h) -- 0 Overwrite, 1 Accumulate, 2 Ignore (dL/dinput only; the
+ * parameter gradients are left as they are) */
 int tcnn_trainer_backward(tcnn_trainer* t, void* stream, const tcnn_trainer_context* ctx, uint32_t n, const float* input,
-                          float* dL_dinput, int accumulate);
+                          float* dL_dinput, int gradient_mode);
 /* Trainer::loss(stream, ctx) (trainer.h:205-211): synchronises stream; 0 for an external-dL/dy context */
 float tcnn_trainer_context_loss(tcnn_trainer* t, void* stream, const tcnn_trainer_context* ctx);
 const void* tcnn_trainer_context_output(const tcnn_trainer_context* ctx);
@@ -212,6 +214,10 @@ int tcnn_trainer_serialize(tcnn_trainer* t, int with_optimizer, void* buf, uint6
 /* Trainer::deserialize: msgpack bytes (or the JSON text of the same object, binaries as {"bytes": [...]},
  * gpu_memory_json.h:52-71); params_type "__half" or "float", optional optimizer state. */
 int tcnn_trainer_deserialize(tcnn_trainer* t, const void* buf, uint64_t size);
+/* Trainer::serialize(with_optimizer) as json (trainer.h:275-290): the JSON text of the same object,
+ * binaries in nlohmann's {"bytes": [...], "subtype": null} form, NUL-terminated; *size includes the NUL.
+ * Call with buf = NULL for the size. tcnn_trainer_deserialize accepts the text back. */
+int tcnn_trainer_serialize_json(tcnn_trainer* t, int with_optimizer, char* buf, uint64_t capacity, uint64_t* size);
 uint32_t tcnn_trainer_optimizer_step_count(const tcnn_trainer* t);
 /* Trainer::update_hyperparams(json) (trainer.h:213-216): {"optimizer": {...}} fields update Adam
  * (adam.h:235-283: learning_rate, betas, epsilon, l2_reg, ...). */

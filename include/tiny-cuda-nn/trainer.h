@@ -4,8 +4,8 @@
 // The engine runs forward, loss, backward and (optionally) the optimizer of one training step as
 // three launches on the caller's stream (neuralbtf-tiny-cuda-nn_amd/csrc/runtime.cpp,
 // TrainerHost::training_step_overlapped), so training_step() is one C-ABI call. The ForwardContext it
-// returns identifies the step; loss(ctx) reads that step's loss sum (trainer.h:205-211 reduces the
-// context's loss values). With any of the reference's options (data_pdf, external dL/dy, dL/dinput,
+// returns holds a copy of that step's loss sum on the device; loss(ctx) reads it for any live context
+// (trainer.h:205-211 reduces the context's loss values). With any of the reference's options (data_pdf, external dL/dy, dL/dinput,
 // Accumulate gradients) training_step runs as the reference's does: forward() (network output +
 // loss, or the caller's dL/dy) then backward() (tcnn_trainer_forward / _backward), then the optimizer;
 // loss(ctx) then reads the context's own loss.
@@ -50,15 +50,37 @@ public:
 
 	// trainer.h:89-95. A context made by forward() (or an optioned training_step) owns the engine's
 	// context: output and dL_doutput are views of its fp16 [padded_output_width x batch] buffers.
+	// Device slots holding the loss of each live fused-step context: the fused step keeps one loss sum,
+	// so training_step copies it (stream-ordered, 4 bytes) into the context's own slot and loss(ctx)
+	// reads that -- any live context, as the reference's loss(ctx) reduces the context's own values.
+	struct LossSlots {
+		std::vector<GPUMemory<float>> blocks;
+		std::vector<float*> free_list;
+		static constexpr size_t BLOCK = 1024;
+		float* take() {
+			if (free_list.empty()) {
+				blocks.emplace_back(BLOCK);
+				for (size_t k = 0; k < BLOCK; ++k) free_list.push_back(blocks.back().data() + (BLOCK - 1 - k));
+			}
+			float* p = free_list.back();
+			free_list.pop_back();
+			return p;
+		}
+	};
 	struct ForwardContext : public Context {
 		const Trainer* owner = nullptr;
 		uint64_t step = 0;
 		tcnn_trainer_context* h = nullptr;
 		GPUMatrix<COMPUTE_T> output, dL_doutput;
+		std::shared_ptr<LossSlots> slots;  // a fused step's loss slot (returned on destruction)
+		float* loss_slot = nullptr;
 		ForwardContext() = default;
 		ForwardContext(const ForwardContext&) = delete;
 		ForwardContext& operator=(const ForwardContext&) = delete;
-		~ForwardContext() { tcnn_trainer_context_destroy(h); }
+		~ForwardContext() {
+			tcnn_trainer_context_destroy(h);
+			if (slots && loss_slot) slots->free_list.push_back(loss_slot);
+		}
 	};
 
 	uint32_t padded_output_width() const { return tcnn_trainer_padded_output_width(m_h); }
@@ -105,10 +127,9 @@ public:
 	              bool use_inference_params = false, GradientMode param_gradients_mode = GradientMode::Overwrite) {
 		(void)use_inference_params;
 		if (!ctx.h || ctx.owner != this) throw std::runtime_error{"Trainer::backward: the context was not made by this trainer's forward()"};
-		if (param_gradients_mode == GradientMode::Ignore) throw std::runtime_error{"Trainer::backward: GradientMode::Ignore is not supported"};
 		if (dL_dinput) CHECK_THROW(dL_dinput->m() == m_model->input_width() && dL_dinput->n() == input.n() && dL_dinput->layout() == CM);
 		detail::check_rc(tcnn_trainer_backward(m_h, stream, ctx.h, input.n(), input.data(), dL_dinput ? dL_dinput->data() : nullptr,
-		                                       param_gradients_mode == GradientMode::Accumulate ? 1 : 0));
+		                                       param_gradients_mode == GradientMode::Overwrite ? 0 : param_gradients_mode == GradientMode::Accumulate ? 1 : 2));
 	}
 	void backward(const ForwardContext& ctx, const GPUMatrixDynamic<T>& input, GPUMatrixDynamic<T>* dL_dinput = nullptr,
 	              bool use_inference_params = false, GradientMode param_gradients_mode = GradientMode::Overwrite) {
@@ -146,6 +167,9 @@ public:
 		auto ctx = std::make_unique<ForwardContext>();
 		ctx->owner = this;
 		ctx->step = ++m_n_steps;
+		ctx->slots = m_loss_slots;
+		ctx->loss_slot = m_loss_slots->take();
+		HIP_CHECK_THROW(hipMemcpyAsync(ctx->loss_slot, tcnn_trainer_loss_device(m_h), sizeof(float), hipMemcpyDeviceToDevice, stream));
 		return ctx;
 	}
 	std::unique_ptr<ForwardContext> training_step(const GPUMatrixDynamic<T>& input, const GPUMatrixDynamic<float>& target,
@@ -164,10 +188,10 @@ public:
 			if (v < 0.0f) throw std::runtime_error{tcnn_last_error()};
 			return v;
 		}
-		if (ctx.owner != this || ctx.step != m_n_steps)
-			throw std::runtime_error{"Trainer::loss: only the loss of this trainer's most recent training step is retained"};
-		const float v = tcnn_trainer_loss(m_h, stream);
-		if (v < 0.0f) throw std::runtime_error{tcnn_last_error()};
+		if (ctx.owner != this || !ctx.loss_slot) throw std::runtime_error{"Trainer::loss: the context was not made by this trainer"};
+		float v = 0.0f;
+		HIP_CHECK_THROW(hipMemcpyAsync(&v, ctx.loss_slot, sizeof(float), hipMemcpyDeviceToHost, stream));
+		HIP_CHECK_THROW(hipStreamSynchronize(stream));
 		return v;
 	}
 	float loss(const ForwardContext& ctx) const { return loss(nullptr, ctx); }
@@ -234,6 +258,22 @@ public:
 	void deserialize_msgpack(const std::vector<uint8_t>& data) {
 		detail::check_rc(tcnn_trainer_deserialize(m_h, data.data(), data.size()));
 	}
+	// trainer.h:275-315 with the reference's signatures: json::to_msgpack(trainer->serialize(true)) and
+	// trainer->deserialize(json::from_msgpack(...)) read the same. This json library (nlohmann 3.1.1)
+	// has no binary type, so the binaries travel as nlohmann's binary-as-JSON object
+	// {"bytes": [u8...], "subtype": null}; deserialize accepts that form and the msgpack image alike.
+	json serialize(bool serialize_optimizer = false) {
+		uint64_t n = 0;
+		detail::check_rc(tcnn_trainer_serialize_json(m_h, serialize_optimizer ? 1 : 0, nullptr, 0, &n));
+		std::string text(n, '\0');
+		detail::check_rc(tcnn_trainer_serialize_json(m_h, serialize_optimizer ? 1 : 0, &text[0], n, &n));
+		text.resize(n ? n - 1 : 0);
+		return json::parse(text);
+	}
+	void deserialize(const json& data) {
+		const std::string text = data.dump();
+		detail::check_rc(tcnn_trainer_deserialize(m_h, text.data(), text.size()));
+	}
 
 	std::shared_ptr<Model> model() const { return m_model; }
 	std::shared_ptr<Optimizer<PARAMS_T>> optimizer() const { return m_optimizer; }
@@ -249,6 +289,7 @@ private:
 	uint32_t m_seed;
 	tcnn_trainer* m_h = nullptr;
 	uint64_t m_n_steps = 0;
+	std::shared_ptr<LossSlots> m_loss_slots = std::make_shared<LossSlots>();
 };
 
 }  // namespace tcnn

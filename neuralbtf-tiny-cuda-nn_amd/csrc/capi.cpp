@@ -457,10 +457,11 @@ tcnn_trainer_context* tcnn_trainer_forward(tcnn_trainer* t, void* stream, uint32
 	return rc == 0 ? r : nullptr;
 }
 int tcnn_trainer_backward(tcnn_trainer* t, void* stream, const tcnn_trainer_context* ctx, uint32_t n, const float* in, float* dL_din,
-                          int accumulate) {
+                          int gradient_mode) {
 	return guard([&] {
 		TCNN_CHECK(ctx != nullptr, "backward: null context");
-		t->t->backward((hipStream_t)stream, *ctx->c, n, in, dL_din, accumulate != 0);
+		TCNN_CHECK(gradient_mode >= 0 && gradient_mode <= 2, "backward: gradient_mode must be 0 (Overwrite), 1 (Accumulate) or 2 (Ignore)");
+		t->t->backward((hipStream_t)stream, *ctx->c, n, in, dL_din, gradient_mode);
 	});
 }
 float tcnn_trainer_context_loss(tcnn_trainer* t, void* stream, const tcnn_trainer_context* ctx) {
@@ -539,6 +540,16 @@ int tcnn_trainer_serialize(tcnn_trainer* t, int with_optimizer, void* buf, uint6
 		if (buf) {
 			TCNN_CHECK(capacity >= b.size(), "tcnn_trainer_serialize: buffer too small");
 			std::memcpy(buf, b.data(), b.size());
+		}
+	});
+}
+int tcnn_trainer_serialize_json(tcnn_trainer* t, int with_optimizer, char* buf, uint64_t capacity, uint64_t* size) {
+	return guard([&] {
+		const std::string j = t->t->serialize_json(with_optimizer != 0);
+		if (size) *size = j.size() + 1;
+		if (buf) {
+			TCNN_CHECK(capacity >= j.size() + 1, "tcnn_trainer_serialize_json: buffer too small");
+			std::memcpy(buf, j.c_str(), j.size() + 1);
 		}
 	});
 }

@@ -1238,16 +1238,19 @@ std::unique_ptr<TrainerFwdCtx> TrainerHost::forward(hipStream_t st, uint32_t B, 
 	return c;
 }
 
-void TrainerHost::backward(hipStream_t st, const TrainerFwdCtx& c, uint32_t B, const float* input, float* dL_dinput, bool accumulate) {
+void TrainerHost::backward(hipStream_t st, const TrainerFwdCtx& c, uint32_t B, const float* input, float* dL_dinput, int gradient_mode) {
 	TCNN_CHECK(B == c.B, "backward: batch size differs from the forward's");
+	// Accumulate: this backward's gradients into a scratch sum, added afterwards (trainer.h:146-153).
+	// Ignore: the same scratch, never added -- the parameter gradients stay as they were and only
+	// dL/dinput is delivered (the engine's fused backward computes both in one pass).
 	float* dst = g32.as<float>();
-	if (accumulate) {
+	if (gradient_mode != 0) {
 		g32_acc.reserve(n_params * 4);
 		dst = g32_acc.as<float>();
 	}
 	model->fwd_bwd(st, ws, B, input, nullptr, n_output_dims, 1.0f, w16.p, c.dLdy(), nullptr, dst, nullptr, dL_dinput,
 	               c.keep.p ? c.keep.p : nullptr, c.layout);
-	if (accumulate) launch_add_f32(st, dst, g32.as<float>(), n_params);
+	if (gradient_mode == 1) launch_add_f32(st, dst, g32.as<float>(), n_params);
 	ws.wimage_valid = false;
 	last_B = B;
 }

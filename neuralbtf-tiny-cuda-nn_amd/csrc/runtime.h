@@ -348,7 +348,8 @@ struct TrainerHost {
 	// optimizer_step() reads.
 	std::unique_ptr<TrainerFwdCtx> forward(hipStream_t st, uint32_t B, const float* input, const float* target, const float* pdf,
 	                                       const void* ext_dLdy16, bool prep_dinput);
-	void backward(hipStream_t st, const TrainerFwdCtx& c, uint32_t B, const float* input, float* dL_dinput, bool accumulate);
+	// gradient_mode: 0 Overwrite, 1 Accumulate, 2 Ignore (GradientMode, common.h)
+	void backward(hipStream_t st, const TrainerFwdCtx& c, uint32_t B, const float* input, float* dL_dinput, int gradient_mode);
 	float ctx_loss(hipStream_t st, const TrainerFwdCtx& c);
 	DevBuf g32_acc;  // Accumulate mode: this backward's gradients before they are added
 	// data-parallel exchange inside the step (dp.cpp): with a communicator attached every
@@ -368,6 +369,8 @@ struct TrainerHost {
 	void set_params_full_precision(const float* host, uint64_t n);
 	// snapshot in the reference's msgpack format (Trainer::serialize / deserialize, trainer.h:275-315)
 	std::vector<uint8_t> serialize(bool with_optimizer);
+	// the same object as JSON text, binaries as {"bytes": [...], "subtype": null} (json serialize(bool))
+	std::string serialize_json(bool with_optimizer);
 	void deserialize(const void* data, size_t size);
 	void mark(hipStream_t st, int phase);  // records phase boundary when timing is enabled
 	void profile_end(double* ms, uint32_t n_phases, uint32_t* n_steps);

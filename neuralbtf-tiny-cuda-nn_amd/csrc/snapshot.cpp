@@ -220,7 +220,46 @@ MsgValue from_json_text(const json& j) {
 	return v;
 }
 
+// MsgValue -> nlohmann json, binaries in nlohmann's binary-as-JSON form {"bytes": [...], "subtype": null}
+// (json::dump of a binary value in nlohmann >= 3.8; the reference's Trainer::serialize returns json
+// holding binaries, trainer.h:275-290) -- the form deserialize() accepts back
+json to_json(const MsgValue& v) {
+	switch (v.kind) {
+		case MsgValue::Nil: return json();
+		case MsgValue::Bool: return json(v.u != 0);
+		case MsgValue::UInt: return json(v.u);
+		case MsgValue::Int: return json(v.i);
+		case MsgValue::Float: return json(v.f);
+		case MsgValue::Str: return json(v.s);
+		case MsgValue::Bin: {
+			json bytes = json::array();
+			for (unsigned char c : v.s) bytes.push_back((unsigned)c);
+			json b = json::object();
+			b["bytes"] = std::move(bytes);
+			b["subtype"] = json();
+			return b;
+		}
+		case MsgValue::Map: {
+			json o = json::object();
+			for (const auto& kv : v.m) o[kv.first] = to_json(kv.second);
+			return o;
+		}
+		case MsgValue::Arr: {
+			json a = json::array();
+			for (const auto& e : v.a) a.push_back(to_json(e));
+			return a;
+		}
+	}
+	return json();
+}
+
 }  // namespace
+
+std::string TrainerHost::serialize_json(bool with_optimizer) {
+	const std::vector<uint8_t> b = serialize(with_optimizer);
+	MsgReader r{b.data(), b.data() + b.size()};
+	return to_json(r.value()).dump();
+}
 
 std::vector<uint8_t> TrainerHost::serialize(bool with_optimizer) {
 	TCNN_CHECK(!(with_optimizer && dp_sharded && dp_state_partial),

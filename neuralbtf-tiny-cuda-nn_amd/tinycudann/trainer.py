@@ -67,13 +67,17 @@ class Trainer:
                                          ptr(external_dL_dy), int(prepare_input_gradients))
         return ForwardContext(self, L.check_ptr(h), input.shape[0], (input, target, data_pdf, external_dL_dy))
 
-    def backward(self, ctx, input, dL_dinput=None, accumulate=False, stream=None):
+    def backward(self, ctx, input, dL_dinput=None, accumulate=False, stream=None, gradient_mode=None):
         """Trainer::backward (trainer.h:146-153): parameter gradients into gradients_fp32()
-        (Overwrite, or Accumulate with accumulate=True) and optionally dL/dinput (float32 [B, n_in])."""
+        (Overwrite, or Accumulate with accumulate=True) and optionally dL/dinput (float32 [B, n_in]).
+        gradient_mode ("overwrite" | "accumulate" | "ignore", GradientMode, common.h) overrides
+        `accumulate`; "ignore" leaves the parameter gradients untouched and only writes dL/dinput."""
         assert ctx.trainer is self
+        modes = {"overwrite": 0, "accumulate": 1, "ignore": 2}
+        mode = modes[gradient_mode.lower()] if gradient_mode is not None else int(bool(accumulate))
         L.check(L.lib().tcnn_trainer_backward(self.h, _stream(stream), ctx.h, input.shape[0], ctypes.c_void_p(input.data_ptr()),
                                               ctypes.c_void_p(dL_dinput.data_ptr() if dL_dinput is not None else 0),
-                                              int(accumulate)))
+                                              mode))
 
     def optimizer_step_range(self, begin, end, stream=None):
         """Adam on parameters [begin, end) only (one optimizer step; data-parallel sharded optimizer)."""

@@ -192,18 +192,14 @@ int main(int argc, char** argv) {
 			if (i == 0) first = model.trainer->loss(stream, *ctx);
 			if (i == 199) last = model.trainer->loss(stream, *ctx);
 			if (i == 198) {
-				// a context of an earlier step is rejected by loss(), as documented
+				// the loss of any live context, not only the most recent step's (trainer.h:205-211)
 				auto old = std::move(ctx);
-				bool threw = false;
+				const float l198 = model.trainer->loss(stream, *old);
 				auto ctx2 = model.trainer->training_step(stream, batch, target);
-				try {
-					model.trainer->loss(stream, *old);
-				} catch (const std::runtime_error&) {
-					threw = true;
-				}
-				EXPECT(threw);
+				EXPECT(model.trainer->loss(stream, *old) == l198);
 				++i;
 				last = model.trainer->loss(stream, *ctx2);
+				EXPECT(last != l198);
 			}
 		}
 		std::printf("loss first=%g last=%g\n", first, last);
@@ -240,6 +236,15 @@ int main(int argc, char** argv) {
 			float mx = 0.0f;
 			for (float v : dxh) mx = std::fmax(mx, std::fabs(v));
 			EXPECT(mx > 0.0f && std::isfinite(mx));
+			// GradientMode::Ignore: dL/dinput again, the parameter gradients stay those of the last backward
+			std::vector<float> g4(n), g5(n);
+			HIP_CHECK_THROW(hipStreamSynchronize(stream));
+			HIP_CHECK_THROW(hipMemcpy(g4.data(), tcnn_trainer_gradients_fp32(model.trainer->handle()), n * 4, hipMemcpyDeviceToHost));
+			GPUMatrix<float> dx2(2, B);
+			model.trainer->backward(stream, *fwd_dx, batch, &dx2, false, GradientMode::Ignore);
+			HIP_CHECK_THROW(hipStreamSynchronize(stream));
+			HIP_CHECK_THROW(hipMemcpy(g5.data(), tcnn_trainer_gradients_fp32(model.trainer->handle()), n * 4, hipMemcpyDeviceToHost));
+			EXPECT(g4 == g5 && dx2.to_cpu_vector() == dxh);
 		}
 
 		model.network->inference(stream, probe, probe_out);
@@ -268,6 +273,11 @@ int main(int argc, char** argv) {
 		std::vector<float> p(model.trainer->n_params());
 		HIP_CHECK_THROW(hipMemcpy(p.data(), model.trainer->params_full_precision(), p.size() * 4, hipMemcpyDeviceToHost));
 		auto snap = model.trainer->serialize_msgpack(true);
+		// json serialize / deserialize with the reference's signatures (trainer.h:275-315)
+		const json jsnap = model.trainer->serialize(true);
+		EXPECT(jsnap["n_params"].get<uint64_t>() == model.trainer->n_params() && jsnap["params_type"] == "__half");
+		EXPECT(jsnap["params_binary"]["bytes"].size() == model.trainer->n_params() * 2);
+		EXPECT(jsnap["optimizer"]["first_moments_binary"]["bytes"].size() == model.trainer->n_params() * 4);
 		TrainableModel other = create_from_config(2, 3, config);
 		other.trainer->set_params_full_precision(p.data(), p.size());
 		std::vector<float> q(p.size());
@@ -279,6 +289,15 @@ int main(int argc, char** argv) {
 		third.network->inference(stream, probe, out3);
 		HIP_CHECK_THROW(hipStreamSynchronize(stream));
 		EXPECT(out3.to_cpu_vector() == out);
+		{
+			TrainableModel fourth = create_from_config(2, 3, config);
+			fourth.trainer->deserialize(jsnap);
+			GPUMatrix<float> out4(3, 4096);
+			fourth.network->inference(stream, probe, out4);
+			HIP_CHECK_THROW(hipStreamSynchronize(stream));
+			EXPECT(out4.to_cpu_vector() == out);
+			EXPECT(fourth.trainer->serialize_msgpack(true) == snap);  // the optimizer state came back too
+		}
 
 		// the reference's error behaviour: CHECK_THROW on a batch that is not a multiple of 256
 		{

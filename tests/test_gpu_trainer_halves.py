@@ -114,6 +114,15 @@ def test_external_dL_dy_and_accumulate(torch_mod, which):
     np.testing.assert_array_equal(trainer_arrays(t)["g32"], g_loss)
     t.backward(ce, x, accumulate=True)
     np.testing.assert_array_equal(trainer_arrays(t)["g32"], 2 * g_loss)
+    # GradientMode::Ignore (common.h, trainer.h:146-153): parameter gradients untouched, dL/dinput written
+    ci = t.forward(x, y, prepare_input_gradients=True)
+    dx = torch.zeros(B, 2, device="cuda")
+    t.backward(ci, x, dL_dinput=dx, gradient_mode="ignore")
+    np.testing.assert_array_equal(trainer_arrays(t)["g32"], 2 * g_loss)
+    dx2 = torch.zeros(B, 2, device="cuda")
+    t.backward(ci, x, dL_dinput=dx2)
+    np.testing.assert_array_equal(dx.cpu().numpy(), dx2.cpu().numpy())
+    assert float(dx.abs().max()) > 0
 
 
 @pytest.mark.parametrize("which", ["fused", "tile"])
