@@ -98,6 +98,7 @@ _SIGS = {
     "tcnn_trainer_profile_begin": (c_int, [c_void_p]),
     "tcnn_trainer_profile_begin_sampled": (c_int, [c_void_p, c_uint32]),
     "tcnn_trainer_serialize": (c_int, [c_void_p, c_int, c_void_p, c_uint64, c_void_p]),
+    "tcnn_trainer_serialize_json": (c_int, [c_void_p, c_int, c_void_p, c_uint64, c_void_p]),
     "tcnn_trainer_deserialize": (c_int, [c_void_p, c_void_p, c_uint64]),
     "tcnn_trainer_profile_end": (c_int, [c_void_p, c_void_p, c_uint32, c_void_p]),
     "tcnn_debug_probe": (c_int, [c_void_p, c_void_p, c_void_p]),
