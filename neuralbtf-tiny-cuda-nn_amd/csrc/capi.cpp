@@ -127,7 +127,7 @@ struct ModuleNWIE : ModuleBase {
 		check_batch(n);
 		auto c = std::make_unique<NwieCtx>();
 		c->pool = pool;
-		if (std::getenv("TCNN_NO_FORWARD_KEEP")) {  // A/B switch (read per call): the backward recomputes the forward
+		if (model.sw.no_forward_keep) {  // A/B switch (read when the module is built): the backward recomputes the forward
 			model.inference(st, ws, n, in, params, out);
 			c->layout = NetworkHost::KEEP_NONE;
 			return c;

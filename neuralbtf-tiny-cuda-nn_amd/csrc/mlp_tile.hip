@@ -72,8 +72,11 @@ uint32_t tile_train_blocks(uint32_t B, uint32_t W, uint32_t IN, uint32_t NH) {
 	TileShapeInfo i{};
 	if (!tile_shape(W, IN, NH, &i)) return 1;
 	uint32_t per_cu = i.wg_per_cu;
-	if (const char* e = std::getenv("TCNN_TILE_WG_PER_CU"))
-		per_cu = std::min(std::max(1u, (uint32_t)std::atoi(e)), std::max(1u, (160u * 1024u) / i.lds_bytes));
+	static const int env = [] {  // read once per process
+		const char* e = std::getenv("TCNN_TILE_WG_PER_CU");
+		return e ? std::atoi(e) : 0;
+	}();
+	if (env > 0) per_cu = std::min(std::max(1u, (uint32_t)env), std::max(1u, (160u * 1024u) / i.lds_bytes));
 	return std::max(1u, std::min(cu_count() * per_cu, B / 32));
 }
 

@@ -92,6 +92,21 @@ void DevBuf::reserve(size_t n) {
 	if (poison) TCNN_HIP_CHECK(hipMemset(p, 0xff, n));
 }
 
+EngineSwitches EngineSwitches::from_env() {
+	EngineSwitches s;
+	auto on = [](const char* n) { return std::getenv(n) != nullptr; };
+	s.no_fused_grid = on("TCNN_NO_FUSED_GRID");
+	s.no_tile_engine = on("TCNN_NO_TILE_ENGINE");
+	s.no_inrange_index = on("TCNN_NO_INRANGE_INDEX");
+	s.split_encode = on("TCNN_SPLIT_ENCODE");
+	s.no_forward_keep = on("TCNN_NO_FORWARD_KEEP");
+	const char* bin = std::getenv("TCNN_GRID_BIN");
+	s.grid_bin_all = bin && std::string(bin) == "all";
+	if (const char* e = std::getenv("TCNN_GRID_BWD_CHUNKS"))
+		if (std::atoi(e) > 0) s.grid_bwd_chunks = (uint32_t)std::atoi(e);
+	return s;
+}
+
 bool ieq(const std::string& a, const std::string& b) {
 	if (a.size() != b.size()) return false;
 	for (size_t i = 0; i < a.size(); ++i)
@@ -187,8 +202,7 @@ GridEncodingHost::GridEncodingHost(uint32_t n_dims, const json& enc) {
 	// levels are a suffix of the parameter vector -- go through the binned backward (grid_bin.hip).
 	// TCNN_GRID_BIN=all bins every level that does not fit whole (tuning switch).
 	const uint32_t S = grid_bwd_slot_budget();
-	const char* bin_env = std::getenv("TCNN_GRID_BIN");
-	const bool bin_all = bin_env && std::string(bin_env) == "all";
+	const bool bin_all = sw.grid_bin_all;
 	first_binned = L;
 	for (uint32_t l = 0; l < L; ++l) {
 		const uint64_t need = bin_all ? (uint64_t)levels[l].size * F : (uint64_t)levels[l].size;
@@ -515,7 +529,7 @@ NetworkHost::NetworkHost(uint32_t n_in, uint32_t n_out, const json& e, const jso
 bool NetworkHost::fused_ok() const {
 	// CutlassMLP / "MLP" run on the layer-wise engine (the reference's separate GEMM-per-layer network)
 	const bool ff = ieq(mlp.otype, "FullyFusedMLP") || ieq(mlp.otype, "MegakernelMLP");
-	if (std::getenv("TCNN_NO_FUSED_GRID")) return false;  // A/B switch: the tile engine instead
+	if (sw.no_fused_grid) return false;  // A/B switch: the tile engine instead
 	return ff && grid && grid->n_to_pad == 0 && !grid->opts().active && mlp.output_activation == 0 &&
 	       (mlp.activation == ACT_NONE || mlp.activation == ACT_RELU) &&
 	       fused_train_supported(mlp.width, mlp.n_input, mlp.n_hidden_layers, grid->desc.n_pos_dims,
@@ -525,7 +539,7 @@ bool NetworkHost::fused_ok() const {
 bool NetworkHost::tile_shape_ok() const {
 	const bool ff = ieq(mlp.otype, "FullyFusedMLP") || ieq(mlp.otype, "MegakernelMLP");
 	if (!ff || mlp.output_activation == ACT_SINE) return false;  // Sine has no post-activation backward (common_device.h:271-275)
-	if (std::getenv("TCNN_NO_TILE_ENGINE")) return false;  // A/B switch: the layer-wise engine instead
+	if (sw.no_tile_engine) return false;  // A/B switch: the layer-wise engine instead
 	return tile_train_supported(mlp.width, mlp.n_input, mlp.n_hidden_layers, mlp.padded_output, mlp.activation);
 }
 
@@ -571,7 +585,8 @@ void NetworkHost::forward_layers(hipStream_t st, StepWorkspace& ws, uint32_t B, 
 	launch_layer_fwd(st, B, OUTP, W, p, x, out16, mlp.output_activation);
 }
 
-void NetworkHost::inference(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const void* params16, void* out16) {
+void NetworkHost::inference(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const void* params16, void* out16,
+                            bool trust_image) {
 	TCNN_CHECK(B % 32 == 0, "inference: batch must be a multiple of 32");
 	const uint32_t IN = mlp.n_input;
 	const uint8_t* eparams = (const uint8_t*)params16 + (size_t)mlp.n_params() * 2;
@@ -579,8 +594,11 @@ void NetworkHost::inference(hipStream_t st, StepWorkspace& ws, uint32_t B, const
 		ws.enc16.reserve((size_t)IN * B * 2);
 		launch_grid_fwd(st, grid->desc.n_pos_dims, grid->desc.n_features_per_level, grid->desc.hash_type, B, grid->desc.n_levels,
 		                pos, grid->desc.n_pos_dims, eparams, ws.enc16.p, true, 0, grid->dev_levels(), grid->hash_grid(), grid->desc.interp);
-		ws.wimage.reserve(fused_weight_image_bytes(mlp.width, IN, mlp.n_hidden_layers));
-		launch_pack_weights(st, mlp.width, IN, mlp.n_hidden_layers, params16, ws.wimage.p);
+		if (!(trust_image && ws.wimage_valid)) {
+			ws.wimage.reserve(fused_weight_image_bytes(mlp.width, IN, mlp.n_hidden_layers));
+			launch_pack_weights(st, mlp.width, IN, mlp.n_hidden_layers, params16, ws.wimage.p);
+			if (trust_image) ws.wimage_valid = true;  // the image now matches the trainer's parameters
+		}
 		launch_mlp_infer(st, mlp.width, IN, mlp.n_hidden_layers, mlp.activation, true, B, ws.wimage.p, ws.enc16.p, out16);
 		return;
 	}
@@ -661,7 +679,7 @@ void NetworkHost::fused_kernel(hipStream_t st, StepWorkspace& ws, uint32_t B, co
 	                   mlp.activation, B, dims, loss_scale, params16, table, pos, target, out16, ws.dLdenc.p,
 	                   ws.wgrad_partial.as<float>(), ws.loss_partial.as<float>(), grid->dev_levels(), grid->hash_grid(),
 	                   grid->desc.interp, nb, dout16, ws.wimage.p, loss_l2,
-	                   grid->inrange_index_ok && grid->desc.interp == Interp::Linear && !std::getenv("TCNN_NO_INRANGE_INDEX"), enc_soa);
+	                   grid->inrange_index_ok && grid->desc.interp == Interp::Linear && !sw.no_inrange_index, enc_soa);
 }
 
 void NetworkHost::grid_backward(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, GridBwdEpilogue* ep) {
@@ -909,7 +927,7 @@ void TrainerHost::training_step_overlapped(hipStream_t st, uint32_t B, const flo
 	NetworkHost& m = *model;
 	mark(st, 0);
 	const void* enc_soa = nullptr;
-	if (std::getenv("TCNN_SPLIT_ENCODE")) {  // A/B experiment: the encoding as its own pass, read by the fused kernel
+	if (m.sw.split_encode) {  // A/B experiment: the encoding as its own pass, read by the fused kernel
 		const GridEncodingHost& g = *m.grid;
 		ws.enc16.reserve((size_t)m.mlp.n_input * B * 2);
 		launch_grid_fwd(st, g.desc.n_pos_dims, g.desc.n_features_per_level, g.desc.hash_type, B, g.desc.n_levels, input, g.desc.n_pos_dims,
@@ -1281,7 +1299,7 @@ float TrainerHost::loss(hipStream_t st) {
 void TrainerHost::inference(hipStream_t st, uint32_t B, const float* input, float* out) {
 	const uint32_t OUTP = model->mlp.padded_output;
 	ws.out16.reserve((size_t)B * OUTP * 2);
-	model->inference(st, ws, B, input, w16.p, ws.out16.p);
+	model->inference(st, ws, B, input, w16.p, ws.out16.p, /*trust_image=*/true);
 	launch_trim_cast(st, B, OUTP, n_output_dims, ws.out16.p, out);
 }
 

@@ -53,7 +53,23 @@ struct GridBwdBufs {
 };
 
 // ---- multiresolution grid (reference encodings/grid.h:652-1208) ----
+// The engine's A/B and tuning switches (TCNN_* environment variables). Read once when an engine
+// object is built -- never per step -- so an experiment sets them before creating its trainer or
+// module. Process-wide debug switches (TCNN_DEBUG_POISON, TCNN_DEBUG_GRID_TIMES, TCNN_TILE_REG_A,
+// TCNN_TILE_WG_PER_CU) are read once per process where they are used.
+struct EngineSwitches {
+	bool no_fused_grid = false;     // TCNN_NO_FUSED_GRID: grid models train on the tile engine
+	bool no_tile_engine = false;    // TCNN_NO_TILE_ENGINE: FullyFusedMLP shapes train on the layer-wise engine
+	bool no_inrange_index = false;  // TCNN_NO_INRANGE_INDEX: the generic grid index in every kernel
+	bool split_encode = false;      // TCNN_SPLIT_ENCODE: the encoding as its own pass (experiment)
+	bool no_forward_keep = false;   // TCNN_NO_FORWARD_KEEP: Module backward recomputes the forward
+	bool grid_bin_all = false;      // TCNN_GRID_BIN=all: bin every grid level that does not fit whole
+	uint32_t grid_bwd_chunks = 0;   // TCNN_GRID_BWD_CHUNKS: grid backward point chunks (0: automatic)
+	static EngineSwitches from_env();
+};
+
 struct GridEncodingHost {
+	EngineSwitches sw = EngineSwitches::from_env();
 	GridDesc desc{};
 	uint32_t n_features = 0;     // L * F
 	uint32_t n_to_pad = 0;       // alignment padding (reference set_padded_output_width)
@@ -88,7 +104,7 @@ struct GridEncodingHost {
 		o.n_features = n_features;
 		const float t = (max_level * (float)n_features) / (float)desc.n_features_per_level + 1e-3f;
 		o.active = (stochastic || max_level_gpu || (float)(desc.n_levels - 1) >= t) ? 1u : 0u;
-		o.inrange_index = (inrange_index_ok && desc.interp == Interp::Linear && !std::getenv("TCNN_NO_INRANGE_INDEX")) ? 1u : 0u;
+		o.inrange_index = (inrange_index_ok && desc.interp == Interp::Linear && !sw.no_inrange_index) ? 1u : 0u;
 		return o;
 	}
 	const GridSlabMap* slab_map() const { return d_slab_map.as<GridSlabMap>(); }
@@ -101,8 +117,7 @@ struct GridEncodingHost {
 		const uint32_t n_cu = 256;
 		const uint32_t fit = (n_cu > reserved ? n_cu - reserved : 1u) / (uint32_t)slices.size();
 		uint32_t c = std::max(1u, fit > 2 ? fit - 1 : fit);
-		if (const char* e = std::getenv("TCNN_GRID_BWD_CHUNKS"))  // tuning override
-			if (std::atoi(e) > 0) c = (uint32_t)std::atoi(e);
+		if (sw.grid_bwd_chunks) c = sw.grid_bwd_chunks;  // tuning override
 		return std::max(1u, std::min(std::min(c, 32u), B / 4096));
 	}
 	// bin-pass geometry for B points (reserves the record / directory buffers in w)
@@ -191,6 +206,7 @@ struct StepWorkspace {
 //   "layered" everything else (CutlassMLP, other widths, output activations):
 //             per-layer MFMA kernels (mlp_layers.hip) with fp16 activations in HBM.
 struct NetworkHost {
+	EngineSwitches sw = EngineSwitches::from_env();
 	std::unique_ptr<EncodingHost> enc;
 	GridEncodingHost* grid = nullptr;  // enc->grid when the encoding is a grid
 	MlpHost mlp;
@@ -208,7 +224,10 @@ struct NetworkHost {
 	void initialize_params(Pcg32& rng, float* host_out, float scale = 1.0f) const;  // network first (nwie.h:124-130)
 
 	// params16: [mlp | encoding] fp16. out16: fp16 [B][padded_output].
-	void inference(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const void* params16, void* out16);
+	// trust_image: ws.wimage_valid tracks params16 (the Trainer's own parameters, whose every writer
+	// clears it), so a valid fused weight image is reused instead of re-packed
+	void inference(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const void* params16, void* out16,
+	               bool trust_image = false);
 	// Forward that keeps what the backward needs (the reference's forward context, cpp_api.cu:84-109,
 	// network_with_input_encoding.h:70-81): the encoding, in the layout of the engine the backward will
 	// run (with_dinput: the caller wants dL/dinput) -- SoA [IN][B] for the register-resident grid kernel,

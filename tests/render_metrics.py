@@ -105,3 +105,21 @@ def to_ldr(v):
     """the sample's to_ldr (mlp_learning_an_image.cu:61-71): (uint8)(clamp(v)^(1/2.2) * 255 + 0.5)"""
     v = np.clip(v.astype(np.float32), 0.0, 1.0)
     return (np.power(v, np.float32(1.0 / 2.2)) * np.float32(255.0) + np.float32(0.5)).astype(np.uint8)
+
+
+def load_reference_crops():
+    """the reference's renders data/readme/{100,1000}.jpg, luma of a central crop
+    (tests/golden/reference_render_crops.npz, tools/make_reference_render_crops.py)"""
+    z = np.load(os.path.join(GOLD, "reference_render_crops.npz"))
+    return {"100": z["render_100"], "1000": z["render_1000"],
+            "rows": slice(int(z["crop_rows"][0]), int(z["crop_rows"][1])),
+            "cols": slice(int(z["crop_cols"][0]), int(z["crop_cols"][1]))}
+
+
+def render_vs_reference(render, img, crops, step):
+    """render-to-render agreement with the reference's render of `step` on the fixture's crop: PSNR
+    between the two renders and the correlation of their residuals against the training image"""
+    ours = luma(render)[crops["rows"], crops["cols"]].astype(np.float64)
+    ref = crops[step].astype(np.float64)
+    a = img[crops["rows"], crops["cols"]].astype(np.float64)
+    return {"psnr": psnr(ours, ref), "residual_corr": float(np.corrcoef((ours - a).ravel(), (ref - a).ravel())[0, 1])}

@@ -12,10 +12,15 @@ samples/mlp_learning_an_image.cu:213-288).
     reference-mimic mode (fp16 WMMA / CUTLASS accumulators and fp16 atomics). The
     first steps are re-run here and must reproduce the frozen losses exactly.
 
-Finding: the reference's render is 0.62 dB below the oracle's at 100 steps, and the
-mimic mode moves the oracle by only +0.07 dB, so the gap is not the reference's fp16 arithmetic.
-The bands: the oracle is no worse than the reference's render (-3 sigma of the seed spread,
-tests/golden/render_spread.json) and at most 1 dB better; the mimic stays within 0.2 dB of the ideal.
+Finding (r04): the reference's renders were made with batches of 2^16 points, not
+the sample's 2^18 (the only pipeline change that reproduces the reference's error pattern pixel by
+pixel). At 2^18 the oracle sits +0.62 dB above the reference's render (the mimic mode moves it by only
++0.07 dB: not the reference's fp16 arithmetic); at 2^16 (key ideal_b16, 101 steps, ~4 min) the
+oracle's render is within 0.03 dB of the reference's image PSNR and 42.5 dB from the reference's
+render itself (residual correlation 0.972; other seed pairs of the same pipeline reach <= 33.6 dB /
+0.78). The bands: the 2^16 oracle within 3 sigma of the reference's render (both sides, sigma of the
+2^16 seed spread, tests/golden/render_spread_b16.json), its render within 40 dB / 0.93 of the
+reference's; at 2^18 the mimic stays within 0.2 dB of the ideal.
 """
 import json
 import os
@@ -69,7 +74,7 @@ def _replay(mode, n_steps):
     try:
         om = O.OracleModel(cfg, 2, 3, seed=1337)
         rng = O.pcg32(1337)
-        B = 1 << 18
+        B = 1 << (16 if mode.endswith("_b16") else 18)
         out = []
         for _ in range(n_steps):
             pos = O.generate_uniform(rng, 2 * B).reshape(B, 2)
@@ -79,7 +84,7 @@ def _replay(mode, n_steps):
         O.set_mimic(False)
 
 
-@pytest.mark.parametrize("mode,n_steps", [("ideal", 2), ("mimic", 1)])
+@pytest.mark.parametrize("mode,n_steps", [("ideal", 2), ("mimic", 1), ("ideal_b16", 3)])
 def test_oracle_render_trajectory_reproduces(mode, n_steps):
     frozen = _json("oracle_render.json")[mode]["losses"]
     assert len(frozen) == 101
@@ -90,10 +95,21 @@ def test_oracle_render_psnr_against_reference():
     ref = _json("reference_renders.json")["psnr_gray"]["100"]
     o = _json("oracle_render.json")
     ideal, mimic = o["ideal"]["psnr_gray_100"], o["mimic"]["psnr_gray_100"]
-    s = sigma(100)
-    assert ref - 3 * s <= ideal <= ref + 1.0, (ideal, ref, s)
     assert abs(mimic - ideal) <= 0.2, (mimic, ideal)
-    # the losses fall like a trained model's (both modes)
-    for m in ("ideal", "mimic"):
+    # the reference's run (B = 2^16): image PSNR within 3 sigma both sides, and the render itself
+    s16 = _json("render_spread_b16.json")["stats"]["100"]["std"]
+    b16 = o["ideal_b16"]
+    assert abs(b16["psnr_gray_100"] - ref) <= 3 * s16, (b16["psnr_gray_100"], ref, s16)
+    rr = b16["vs_reference_render_100"]
+    assert rr["psnr"] >= 40.0 and rr["residual_corr"] >= 0.93, rr
+    # the losses fall like a trained model's (every mode)
+    for m in ("ideal", "mimic", "ideal_b16"):
         l = o[m]["losses"]
         assert l[-1] < 0.01 * l[0], (m, l[0], l[-1])
+
+
+def test_oracle_b16_crop_matches_reference_crop():
+    """the frozen oracle crop against the frozen reference crop (same window, same luma)"""
+    crops = RM.load_reference_crops()
+    z = np.load(os.path.join(RM.GOLD, "oracle_render_b16_crop.npz"))
+    assert RM.psnr(z["render_100"], crops["100"]) >= 40.0

@@ -12,7 +12,12 @@ render PSNR):
 tests/test_render_pin.py re-runs the first steps on the live oracle (the losses must reproduce
 exactly) and holds the PSNRs to the reference's own render (tests/golden/reference_renders.json).
 
-usage: python tools/make_oracle_render.py [ideal|mimic] [n_threads]
+The reference's renders were made with batches of 2^16 points (tools/render_crops.py +
+tools/render_compare.py: that batch reproduces their error pattern, 42.5 dB render-to-render), so
+`b16` runs the ideal-mode oracle at B = 2^16 under the key ideal_b16 (also saving a central crop of
+its render, the one tools/render_crops.py takes, for the render-to-render check).
+
+usage: python tools/make_oracle_render.py [ideal|mimic] [n_threads] [b16]
 """
 import json
 import os
@@ -24,10 +29,10 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tests"))
+sys.path.insert(0, os.path.join(REPO, "tools"))
 import render_metrics as RM  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 
-B = 1 << 18
 N_STEPS = 101
 OUT = os.path.join(RM.GOLD, "oracle_render.json")
 
@@ -36,6 +41,9 @@ def main():
     mode = sys.argv[1] if len(sys.argv) > 1 else "ideal"
     assert mode in ("ideal", "mimic"), mode
     nt = int(sys.argv[2]) if len(sys.argv) > 2 else os.cpu_count()
+    b16 = len(sys.argv) > 3 and sys.argv[3] == "b16"
+    B = 1 << (16 if b16 else 18)
+    key = mode + ("_b16" if b16 else "")
     O.set_mimic(mode == "mimic")
     cfg = json.load(open(os.path.join(RM.GOLD, "config_hash.json")))
     img = RM.load_albert_full()
@@ -66,7 +74,7 @@ def main():
     render = render.reshape(H, W, 3)
     res = {
         "what": f"CPU oracle (oracle/tcnn_oracle.c, {mode} mode) running the reference README experiment: "
-                "config_hash.json, full-resolution albert, B = 2^18, pcg32{1337} batches, 8-bit-weight bilinear "
+                f"config_hash.json, full-resolution albert, B = 2^{16 if b16 else 18}, pcg32{{1337}} batches, 8-bit-weight bilinear "
                 "targets; render after steps 0..100",
         "batch": B,
         "losses": losses,
@@ -77,7 +85,10 @@ def main():
     doc = json.load(open(OUT)) if os.path.exists(OUT) else {}
     if "losses" in doc:  # a single-run file from before the modes
         doc = {"ideal": doc}
-    doc[mode] = res
+    doc[key] = res
+    if b16:
+        from render_crops import CROP  # noqa: E402
+        np.save(os.path.join(REPO, "gpurun_out", "oracle_b16_100_crop.npy"), RM.luma(render)[CROP])
     with open(OUT, "w") as f:
         json.dump(doc, f, indent=1)
     print(json.dumps({k: v for k, v in res.items() if k != "losses"}, indent=1))
