@@ -78,6 +78,15 @@ tcnn_context* tcnn_module_forward(tcnn_module* m, void* stream, uint32_t n, cons
 int tcnn_module_backward(tcnn_module* m, void* stream, const tcnn_context* ctx, uint32_t n, float* dL_dinput,
                          const void* dL_doutput, void* dL_dparams, const float* input, const void* output,
                          const void* params);
+/* The torch binding's backward with its loss-scale arithmetic folded in (reference
+ * bindings/torch/tinycudann/modules.py:128-138): dL_doutput (fp16) is multiplied by loss_scale and
+ * rounded to fp16, the module's backward runs on it, dL_dinput (fp32) is divided by loss_scale and
+ * dL_dparams = fp16(fp16 gradient / loss_scale) -- stored as fp16, or widened to fp32 when
+ * dparams_fp32 (the gradient of fp32 master parameters cast to fp16 for the module) -- the same
+ * values the binding computes with three torch operations. */
+int tcnn_module_backward_scaled(tcnn_module* m, void* stream, const tcnn_context* ctx, uint32_t n, float* dL_dinput,
+                                const void* dL_doutput, void* dL_dparams, const float* input, const void* output,
+                                const void* params, float loss_scale, int dparams_fp32);
 /* Module::backward_backward_input(stream, ctx, n, dL_ddLdinput, input, dL_doutput?, dL_dparams?,
  * dL_ddLdoutput?, dL_dinput?, params) (cpp_api.h:94): second-order gradients from dL/d(dL/dinput)
  * fp32 [n][n_input_dims]. Implemented by grid encodings (grid.h:902-1026); every other module

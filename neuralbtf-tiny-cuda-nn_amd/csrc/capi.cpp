@@ -248,6 +248,7 @@ struct ModuleGrid : ModuleBase {
 
 struct tcnn_module {
 	std::unique_ptr<ModuleBase> m;
+	DevBuf dout_scaled, dparams16;  // tcnn_module_backward_scaled's temporaries
 };
 struct tcnn_context {
 	uint32_t n = 0;
@@ -357,6 +358,33 @@ int tcnn_module_backward(tcnn_module* m, void* stream, const tcnn_context* ctx, 
 		}
 		TCNN_CHECK(ctx->n == n, "backward: batch size differs from the forward's");
 		m->m->backward((hipStream_t)stream, ctx->impl.get(), n, dL_din, dL_dout, dL_dparams, in, out, params);
+	});
+}
+
+int tcnn_module_backward_scaled(tcnn_module* m, void* stream, const tcnn_context* ctx, uint32_t n, float* dL_din, const void* dL_dout,
+                                void* dL_dparams, const float* in, const void* out, const void* params, float loss_scale,
+                                int dparams_fp32) {
+	return guard([&] {
+		TCNN_CHECK(ctx != nullptr, "backward: null context");
+		TCNN_CHECK(loss_scale != 0.0f, "backward: loss scale must be nonzero");
+		const hipStream_t st = (hipStream_t)stream;
+		const uint64_t np = m->m->n_params();
+		if (n == 0) {
+			if (dL_dparams) TCNN_HIP_CHECK(hipMemsetAsync(dL_dparams, 0, np * (dparams_fp32 ? 4 : 2), st));
+			return;
+		}
+		TCNN_CHECK(ctx->n == n, "backward: batch size differs from the forward's");
+		const size_t n_out = (size_t)n * m->m->n_output_dims();
+		m->dout_scaled.reserve(n_out * 2);
+		launch_scale_f16(st, dL_dout, m->dout_scaled.p, loss_scale, n_out);  // modules.py:135 doutput * loss_scale
+		void* g16 = dL_dparams;
+		if (dL_dparams && dparams_fp32) {
+			m->dparams16.reserve(np * 2);
+			g16 = m->dparams16.p;
+		}
+		m->m->backward(st, ctx->impl.get(), n, dL_din, m->dout_scaled.p, g16, in, out, params);
+		if (dL_din) launch_div_f32(st, dL_din, loss_scale, (size_t)n * m->m->n_input_dims());  // modules.py:137
+		if (dL_dparams) launch_div_f16(st, g16, dL_dparams, loss_scale, np, dparams_fp32 != 0);  // modules.py:138
 	});
 }
 

@@ -236,6 +236,11 @@ void launch_adam(hipStream_t st, const AdamArgs& a, float* w32, void* w16, const
 
 void launch_cast_f32_f16(hipStream_t st, const float* in, void* out, size_t n);
 void launch_cast_f16_f32(hipStream_t st, const void* in, float* out, size_t n);
+// loss-scale arithmetic of the torch binding (modules.py:128-137): out = fp16(in * s); x /= s (fp32);
+// out = fp16(in / s), stored as fp16 or widened to fp32
+void launch_scale_f16(hipStream_t st, const void* in, void* out, float s, size_t n);
+void launch_div_f32(hipStream_t st, float* x, float s, size_t n);
+void launch_div_f16(hipStream_t st, const void* in, void* out, float s, size_t n, bool out_f32);
 
 // RelativeL2 (standalone, reference relative_l2.h:40-76): pred fp16 [B][stride] -> values, grads
 void launch_relative_l2(hipStream_t st, uint32_t B, uint32_t stride, uint32_t dims, float loss_scale,

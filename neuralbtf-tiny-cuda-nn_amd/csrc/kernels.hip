@@ -179,6 +179,40 @@ __global__ void k_cast_f16_f32(const _Float16* __restrict__ in, float* __restric
 	const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
 	if (i < n) out[i] = (float)in[i];
 }
+// The torch binding's loss-scale arithmetic (reference bindings/torch/tinycudann/modules.py:128-137) done
+// by the engine, in torch's rounding: fp16 x scalar and fp16 / scalar compute in fp32 and round once
+// to fp16 (f16_rn: no fused mix rounding), fp32 / scalar in fp32.
+__global__ void k_scale_f16(const _Float16* __restrict__ in, _Float16* __restrict__ out, float s, size_t n) {
+	const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (i < n) out[i] = f16_rn((float)in[i] * s);
+}
+__global__ void k_div_f32(float* __restrict__ x, float s, size_t n) {
+	const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (i < n) x[i] = x[i] / s;
+}
+__global__ void k_div_f16(const _Float16* __restrict__ in, void* __restrict__ out, float s, size_t n, int out_f32) {
+	const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	const _Float16 h = f16_rn((float)in[i] / s);
+	if (out_f32) ((float*)out)[i] = (float)h;
+	else ((_Float16*)out)[i] = h;
+}
+void launch_scale_f16(hipStream_t st, const void* in, void* out, float s, size_t n) {
+	if (!n) return;
+	hipLaunchKernelGGL(k_scale_f16, dim3(div_round_up(n, 256)), dim3(256), 0, st, (const _Float16*)in, (_Float16*)out, s, n);
+	TCNN_HIP_CHECK(hipGetLastError());
+}
+void launch_div_f32(hipStream_t st, float* x, float s, size_t n) {
+	if (!n) return;
+	hipLaunchKernelGGL(k_div_f32, dim3(div_round_up(n, 256)), dim3(256), 0, st, x, s, n);
+	TCNN_HIP_CHECK(hipGetLastError());
+}
+void launch_div_f16(hipStream_t st, const void* in, void* out, float s, size_t n, bool out_f32) {
+	if (!n) return;
+	hipLaunchKernelGGL(k_div_f16, dim3(div_round_up(n, 256)), dim3(256), 0, st, (const _Float16*)in, out, s, n, out_f32 ? 1 : 0);
+	TCNN_HIP_CHECK(hipGetLastError());
+}
+
 void launch_cast_f32_f16(hipStream_t st, const float* in, void* out, size_t n) {
 	if (!n) return;
 	hipLaunchKernelGGL(k_cast_f32_f16, dim3(div_round_up(n, 256)), dim3(256), 0, st, in, (_Float16*)out, n);

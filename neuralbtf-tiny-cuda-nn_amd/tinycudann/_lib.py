@@ -37,6 +37,7 @@ _SIGS = {
     "tcnn_module_inference": (c_int, [c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_void_p]),
     "tcnn_module_forward": (c_void_p, [c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_int]),
     "tcnn_module_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "tcnn_module_backward_scaled": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int]),
     "tcnn_module_backward_backward_input": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32] + [c_void_p] * 7),
     "tcnn_context_destroy": (None, [c_void_p]),
     "tcnn_module_set_max_level": (c_int, [c_void_p, c_float]),

@@ -65,26 +65,44 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
+_GRANULARITY = None
+
+
+def _granularity():
+    global _GRANULARITY
+    if _GRANULARITY is None:
+        _GRANULARITY = int(L.lib().tcnn_batch_size_granularity())
+    return _GRANULARITY
+
+
 def free_temporary_memory():
     gc.collect()
     L.lib().tcnn_free_temporary_memory()
 
 
 class _NativeModule:
-    """Python twin of bindings.cpp's Module class (bindings.cpp:75-171)."""
+    """Python twin of bindings.cpp's Module class (bindings.cpp:75-171). A module's sizes and
+    precisions are fixed at creation; they are read once here, so a training step makes no ctypes
+    round trips for them (the torch step is host-bound: tools/torch_step_profile.py)."""
 
     def __init__(self, handle):
         self.h = L.check_ptr(handle)
+        lib = L.lib()
+        self._n_in = lib.tcnn_module_n_input_dims(self.h)
+        self._n_out = lib.tcnn_module_n_output_dims(self.h)
+        self._n_params = lib.tcnn_module_n_params(self.h)
+        self._param_dtype = _torch_precision(lib.tcnn_module_param_precision(self.h))
+        self._out_dtype = _torch_precision(lib.tcnn_module_output_precision(self.h))
 
     # bindings.cpp:306-313: sizes are methods on the native module, as in the reference
     def n_input_dims(self):
-        return L.lib().tcnn_module_n_input_dims(self.h)
+        return self._n_in
 
     def n_output_dims(self):
-        return L.lib().tcnn_module_n_output_dims(self.h)
+        return self._n_out
 
     def n_params(self):
-        return L.lib().tcnn_module_n_params(self.h)
+        return self._n_params
 
     def __del__(self):
         try:
@@ -118,16 +136,32 @@ class _NativeModule:
         return p
 
     def fwd(self, input, params):
-        assert input.dtype == torch.float32 and input.is_contiguous() and input.shape[1] == self.n_input_dims()
-        assert params.dtype == _torch_precision(self.param_precision()) and params.numel() == self.n_params()
+        assert input.dtype == torch.float32 and input.is_contiguous() and input.shape[1] == self._n_in
+        assert params.dtype == self._param_dtype and params.numel() == self._n_params
         B = input.shape[0]
-        out = torch.empty(B, self.n_output_dims(), dtype=_torch_precision(self.output_precision()), device=input.device)
+        out = torch.empty(B, self._n_out, dtype=self._out_dtype, device=input.device)
         if not (input.requires_grad or params.requires_grad):
             L.check(L.lib().tcnn_module_inference(self.h, _stream(), B, _ptr(input), _ptr(out), _ptr(params)))
             return None, out
         ctx = L.check_ptr(L.lib().tcnn_module_forward(self.h, _stream(), B, _ptr(input), _ptr(out), _ptr(params),
                                                        int(input.requires_grad)))
         return _NativeContext(ctx), out
+
+    def bwd_scaled(self, ctx, input, params, output, doutput, loss_scale, need_input, need_params):
+        """the binding's first-order backward (modules.py:128-138 of the reference: doutput * loss_scale,
+        Module::backward, dL/dinput and dL/dparams divided by loss_scale) as ONE engine call
+        (tcnn_module_backward_scaled), with the same roundings as the three torch operations"""
+        B = input.shape[0]
+        dL_dinput = torch.empty_like(input) if need_input else None
+        dL_dparams = torch.empty(self._n_params, dtype=self._param_dtype, device=input.device) if need_params else None
+        if doutput.dtype != self._out_dtype:
+            doutput = doutput.to(self._out_dtype)
+        if not doutput.is_contiguous():
+            doutput = doutput.contiguous()
+        L.check(L.lib().tcnn_module_backward_scaled(self.h, _stream(), ctx.h, B, _ptr(dL_dinput), _ptr(doutput),
+                                                    _ptr(dL_dparams), _ptr(input), _ptr(output), _ptr(params),
+                                                    float(loss_scale), 0))
+        return dL_dinput, dL_dparams
 
     def bwd(self, ctx, input, params, output, dL_doutput):
         B = input.shape[0]
@@ -197,6 +231,14 @@ class _module_function(torch.autograd.Function):
             warnings.warn("doutput must be a CUDA tensor, but isn't. This indicates suboptimal performance.")
             doutput = doutput.cuda()
         input, params, output = ctx.saved_tensors
+        if not torch.is_grad_enabled():
+            # a first-order backward (no create_graph): nothing will differentiate the gradients, so the
+            # differentiable wrapper below and its torch scaling ops are skipped -- one engine call, same values
+            if doutput.dtype != output.dtype:
+                doutput = doutput.to(output.dtype)  # the binding's doutput * loss_scale has the output's dtype
+            input_grad, params_grad = ctx.native_tcnn_module.bwd_scaled(
+                ctx.native_ctx, input, params, output, doutput, ctx.loss_scale, ctx.needs_input_grad[1], ctx.needs_input_grad[2])
+            return None, input_grad, params_grad, None
         input_grad, params_grad = _module_function_backward.apply(ctx, doutput, input, params, output)
         return None, null_tensor_to_none(input_grad), null_tensor_to_none(params_grad), None
 
@@ -247,15 +289,22 @@ class Module(torch.nn.Module):
             warnings.warn("input must be a CUDA tensor, but isn't. This indicates suboptimal performance.")
             x = x.cuda()
         batch_size = x.shape[0]
-        g = int(L.lib().tcnn_batch_size_granularity())
+        g = _granularity()
         padded = (batch_size + g - 1) // g * g
         x_padded = x if batch_size == padded else torch.nn.functional.pad(x, [0, 0, 0, padded - batch_size])
-        output = _module_function.apply(
-            self.native_tcnn_module,
-            x_padded.to(torch.float).contiguous(),
-            self.params.to(_torch_precision(self.native_tcnn_module.param_precision())).contiguous(),
-            self.loss_scale,
-        )
+        if x_padded.dtype != torch.float:
+            x_padded = x_padded.to(torch.float)
+        if not x_padded.is_contiguous():
+            x_padded = x_padded.contiguous()
+        params = self.params
+        pdtype = self.native_tcnn_module._param_dtype
+        if params.dtype != pdtype:
+            params = params.to(pdtype)
+        if not params.is_contiguous():
+            params = params.contiguous()
+        output = _module_function.apply(self.native_tcnn_module, x_padded, params, self.loss_scale)
+        if batch_size == padded and output.shape[1] == self.n_output_dims:
+            return output
         return output[:batch_size, :self.n_output_dims]
 
     def __getstate__(self):

@@ -1,0 +1,40 @@
+"""The torch binding's first-order backward fast path (tinycudann/modules.py `_module_function.backward`
+without create_graph: one tcnn_module_backward_scaled call) gives the same gradients, bit for bit, as
+the reference's differentiable path (modules.py:128-138: doutput * loss_scale, Module::backward,
+division by loss_scale -- taken here when create_graph=True), for the parameter and input gradients of
+a grid + fused MLP network and of a grid encoding."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from helpers import CONFIG_HASH
+
+pytestmark = pytest.mark.gpu
+
+
+def _grads(torch, model, x, create_graph):
+    model.zero_grad(set_to_none=True)
+    xi = x.clone().requires_grad_(True)
+    out = model(xi)
+    loss = ((out.float() - 0.25) ** 2).sum()
+    loss.backward(create_graph=create_graph)
+    return model.params.grad.detach().clone(), xi.grad.detach().clone()
+
+
+@pytest.mark.parametrize("kind", ["network", "grid"])
+def test_first_order_fast_path_matches_differentiable_path(kind):
+    import torch
+    import tinycudann as tcnn
+    torch.manual_seed(3)
+    if kind == "network":
+        model = tcnn.NetworkWithInputEncoding(2, 3, CONFIG_HASH["encoding"], CONFIG_HASH["network"]).cuda()
+    else:
+        model = tcnn.Encoding(2, CONFIG_HASH["encoding"]).cuda()
+    x = torch.rand(4096, 2, device="cuda")
+    gp_fast, gx_fast = _grads(torch, model, x, False)
+    gp_ref, gx_ref = _grads(torch, model, x, True)
+    assert float(gp_fast.abs().max()) > 0 and float(gx_fast.abs().max()) > 0
+    np.testing.assert_array_equal(gp_fast.cpu().numpy(), gp_ref.cpu().numpy())
+    np.testing.assert_array_equal(gx_fast.cpu().numpy(), gx_ref.cpu().numpy())

@@ -9,7 +9,7 @@ the fp32 parameters. Trainer step = one tcnn_trainer_training_step (fused kernel
 network Adam, grid Adam). Synthetic uniform positions and analytic targets resident in HBM;
 torch.cuda events around K steps after W warm-up steps. Also reports the torch step with the forward
 context disabled (backward recomputes the forward: TCNN_NO_FORWARD_KEEP=1) for the A/B, in the same
-process (the switch is read per forward call).
+process (the switch is read when a module is built, so the A/B builds a second model under it).
 
   python tools/torch_step_bench.py [--out profiles/r03_torch_step.json]
 """
@@ -49,19 +49,22 @@ def run(iters, graph):
         model = tcnn.NetworkWithInputEncoding(2, 3, cfg["encoding"], cfg["network"]).cuda()
         opt = torch.optim.Adam(model.parameters(), lr=0.01)
 
-        def torch_step():
-            out = model(pos)
-            loss = ((out - tgt.to(out.dtype)) ** 2 / (out.detach() ** 2 + 0.01)).mean()
-            opt.zero_grad()
-            loss.backward()
-            opt.step()
+        def make_step(model, opt):
+            def torch_step():
+                out = model(pos)
+                loss = ((out - tgt.to(out.dtype)) ** 2 / (out.detach() ** 2 + 0.01)).mean()
+                opt.zero_grad()
+                loss.backward()
+                opt.step()
+            return torch_step
 
+        os.environ["TCNN_NO_FORWARD_KEEP"] = "1"  # read when the module is built: the backward recomputes the forward
+        model_rc = tcnn.NetworkWithInputEncoding(2, 3, cfg["encoding"], cfg["network"]).cuda()
         os.environ.pop("TCNN_NO_FORWARD_KEEP", None)
-        s_torch = timed(torch_step, iters)
-        os.environ["TCNN_NO_FORWARD_KEEP"] = "1"  # read per forward call: the backward recomputes the forward
-        s_recompute = timed(torch_step, iters)
-        os.environ.pop("TCNN_NO_FORWARD_KEEP", None)
-        s_keep2 = timed(torch_step, iters)  # again, to see the drift between the two measurements
+        opt_rc = torch.optim.Adam(model_rc.parameters(), lr=0.01)
+        s_torch = timed(make_step(model, opt), iters)
+        s_recompute = timed(make_step(model_rc, opt_rc), iters)
+        s_keep2 = timed(make_step(model, opt), iters)  # again, to see the drift between the two measurements
         t = Trainer(2, 3, cfg, seed=1337)
         if graph:
             t.set_graph(True)
@@ -72,7 +75,7 @@ def run(iters, graph):
                      "module_engine": model.native_tcnn_module.engine(),
                      "module_inference_engine": model.native_tcnn_module.inference_engine()})
         print(json.dumps(rows[-1]), flush=True)
-        del model, opt, t
+        del model, opt, t, model_rc, opt_rc
     return rows
 
 
