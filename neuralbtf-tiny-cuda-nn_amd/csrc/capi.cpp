@@ -90,6 +90,12 @@ struct ModuleBase {
 	virtual std::unique_ptr<ModuleCtx> forward(hipStream_t st, uint32_t n, const float* in, void* out, const void* params, bool prep) = 0;
 	virtual void backward(hipStream_t st, const ModuleCtx* ctx, uint32_t n, float* dL_din, const void* dL_dout, void* dL_dparams,
 	                      const float* in, const void* out, const void* params) = 0;
+	// tcnn_module_backward_scaled specialised by the module (false: the generic scale / backward /
+	// divide sequence runs instead)
+	virtual bool backward_scaled(hipStream_t, const ModuleCtx*, uint32_t, float*, const void*, void*, const float*, const void*,
+	                             const void*, float, bool) {
+		return false;
+	}
 	// object.h:278-288: only encodings that define it (the grid) support second-order gradients
 	virtual void backward_backward_input(hipStream_t, uint32_t, const float*, const float*, const void*, void*, void*, float*,
 	                                     const void*) {
@@ -150,6 +156,39 @@ struct ModuleNWIE : ModuleBase {
 		              use ? c->keep->p : nullptr, use ? c->layout : NetworkHost::KEEP_NONE);
 		if (dL_dparams) launch_cast_f32_f16(st, grad32.as<float>(), dL_dparams, n_params());
 	}
+	// the torch binding's backward in as few launches as the engine allows: the loss scale folded
+	// into the fused kernel's dL/dy load (or one scaling pass for the other engines), the gradient
+	// finalised as fp16(fp16(g) / s) in one pass (launch_grad_finalize) instead of a cast and a division
+	bool backward_scaled(hipStream_t st, const ModuleCtx* ctx, uint32_t n, float* dL_din, const void* dL_dout, void* dL_dparams,
+	                     const float* in, const void*, const void* params, float s, bool dparams_f32) override {
+		check_batch(n);
+		if (!dL_dparams && !dL_din) return true;
+		grad32.reserve(n_params() * 4);
+		const NwieCtx* c = dynamic_cast<const NwieCtx*>(ctx);
+		const bool use = c && c->keep && c->layout != NetworkHost::KEEP_NONE && c->in == in && c->params == params;
+		const void* dout = dL_dout;
+		const bool fused = model.fused_ok() && !dL_din;
+		if (fused) {
+			model.ext_dout_scale = s;
+		} else {
+			const size_t n_out = (size_t)n * model.mlp.padded_output;
+			dout_scaled.reserve(n_out * 2);
+			launch_scale_f16(st, dL_dout, dout_scaled.p, s, n_out);
+			dout = dout_scaled.p;
+		}
+		try {
+			model.fwd_bwd(st, ws, n, in, nullptr, model.n_output_dims, 1.0f, params, dout, nullptr, grad32.as<float>(), nullptr, dL_din,
+			              use ? c->keep->p : nullptr, use ? c->layout : NetworkHost::KEEP_NONE);
+		} catch (...) {
+			model.ext_dout_scale = 1.0f;
+			throw;
+		}
+		model.ext_dout_scale = 1.0f;
+		if (dL_din) launch_div_f32(st, dL_din, s, (size_t)n * model.n_input_dims);
+		if (dL_dparams) launch_grad_finalize(st, grad32.as<float>(), dL_dparams, s, n_params(), dparams_f32);
+		return true;
+	}
+	DevBuf dout_scaled;
 	GridEncodingHost* grid_encoding() override { return model.grid; }
 	const char* engine() const override { return model.engine(); }
 	const char* inference_engine() const override { return model.inference_engine(); }
@@ -374,6 +413,8 @@ int tcnn_module_backward_scaled(tcnn_module* m, void* stream, const tcnn_context
 			return;
 		}
 		TCNN_CHECK(ctx->n == n, "backward: batch size differs from the forward's");
+		if (m->m->backward_scaled(st, ctx->impl.get(), n, dL_din, dL_dout, dL_dparams, in, out, params, loss_scale, dparams_fp32 != 0))
+			return;
 		const size_t n_out = (size_t)n * m->m->n_output_dims();
 		m->dout_scaled.reserve(n_out * 2);
 		launch_scale_f16(st, dL_dout, m->dout_scaled.p, loss_scale, n_out);  // modules.py:135 doutput * loss_scale

@@ -126,7 +126,7 @@ void launch_fused_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, ui
                         const float* pos, const float* target, void* out16, void* dLdenc_pairs,
                         float* wgrad_partial, float* loss_partial, const LevelInfo* levels, bool hash_grid,
                         Interp interp, uint32_t n_blocks, const void* dout16, const void* wimage, uint32_t loss_l2,
-                        bool inrange_index, const void* enc16) {
+                        bool inrange_index, const void* enc16, float dout_scale) {
 	TCNN_CHECK(B % 32 == 0, "fused train: batch must be a multiple of 32");
 	FusedTrainArgs a;
 	a.enc = (const _Float16*)enc16;
@@ -134,6 +134,7 @@ void launch_fused_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, ui
 	a.inrange_index = inrange_index ? 1u : 0u;
 	a.wimage = (const _Float16*)wimage;
 	a.dout = (const _Float16*)dout16;
+	a.dout_scale = dout_scale;
 	a.B = B;
 	a.dims = dims;
 	a.loss_scale = loss_scale;
@@ -216,7 +217,7 @@ void launch_fused_train_profile(hipStream_t st, uint32_t B, uint32_t dims, const
 	a.B = B; a.dims = dims; a.loss_scale = 128.0f; a.n_total = (float)(B * dims);
 	a.params = (const _Float16*)params16; a.table = (const uint32_t*)table16; a.pos = pos; a.target = target;
 	a.out = nullptr; a.dLdenc = (uint32_t*)dLdenc; a.wgrad_partial = wgrad_partial; a.loss_partial = loss_partial;
-	a.levels = levels; a.hash_grid = 1; a.interp = (uint32_t)Interp::Linear; a.dout = nullptr; a.enc = nullptr; a.prof = prof;
+	a.levels = levels; a.hash_grid = 1; a.interp = (uint32_t)Interp::Linear; a.dout = nullptr; a.dout_scale = 1.0f; a.enc = nullptr; a.prof = prof;
 	a.inrange_index = 1;
 	using K = RegKernelLayout<64, 32, 2>;
 	static uint64_t done = 0;

@@ -154,6 +154,55 @@ __global__ __launch_bounds__(256) void k_grid_fwd_aos_f2(uint32_t B, const float
 	}
 }
 
+// SoA forward for F = 2 (the Module forward's kept encoding and the fused inference's input, [L*2][B]
+// feature planes): one thread per point for 4 consecutive levels (blockIdx.y), the position loaded
+// once and the 4 levels' 16 gathers in flight together; a level is block-uniform. Points of a wave all
+// in [0, 1] take the branch-free index (grid_index_inrange, as k_grid_fwd_aos_f2), any other wave the
+// generic index. Same values as k_grid_fwd (encode_level_f2: the reference's fp16 FMA chain).
+template <uint32_t D, HashType H>
+__global__ __launch_bounds__(256) void k_grid_fwd_soa_f2(uint32_t B, const float* __restrict__ pos, uint32_t pstride,
+                                                         const uint32_t* __restrict__ table, _Float16* __restrict__ out,
+                                                         const LevelInfo* __restrict__ levels, uint32_t hash_grid, uint32_t interp_u,
+                                                         const GridOpts o, uint32_t L) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	const bool valid = i < B;
+	const Interp interp = (Interp)interp_u;
+	float x[D];
+	bool inr = true;
+#pragma unroll
+	for (uint32_t d = 0; d < D; ++d) {
+		x[d] = valid ? pos[(size_t)i * pstride + d] : 0.0f;
+		inr = inr && x[d] >= 0.0f && x[d] <= 1.0f;
+	}
+	const bool fast = o.inrange_index && !o.active && __builtin_amdgcn_ballot_w64(!inr) == 0;
+	const uint32_t l0 = blockIdx.y * 4;
+	h2 r[4];
+	if (fast) {
+#pragma unroll
+		for (uint32_t k = 0; k < 4; ++k) {
+			const uint32_t level = l0 + k;
+			r[k] = encode_level_f2_inrange<D, H>(table, levels[level < L ? level : 0], hash_grid != 0, x);
+		}
+	} else {
+#pragma unroll
+		for (uint32_t k = 0; k < 4; ++k) {
+			const uint32_t level = l0 + k;
+			r[k] = h2{(_Float16)0.0f, (_Float16)0.0f};
+			if (level < L && valid && !(o.active && (float)level >= grid_max_level(o, i, 2) + 1e-3f))  // masked: 0 (grid.h:75-91)
+				r[k] = encode_level_f2<D, H>(table, levels[level], hash_grid != 0, interp, x);
+		}
+	}
+	if (!valid) return;
+#pragma unroll
+	for (uint32_t k = 0; k < 4; ++k) {
+		const uint32_t level = l0 + k;
+		if (level < L) {
+			out[(size_t)(2 * level) * B + i] = r[k][0];
+			out[(size_t)(2 * level + 1) * B + i] = r[k][1];
+		}
+	}
+}
+
 template <uint32_t D, uint32_t F>
 static void grid_fwd_h(hipStream_t st, HashType h, dim3 g, uint32_t B, const float* pos, uint32_t ps, const _Float16* t,
                        _Float16* o, uint32_t soa, uint32_t os, const LevelInfo* lv, uint32_t hg, uint32_t in, const GridOpts& go) {
@@ -198,6 +247,25 @@ void launch_grid_fwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_
 		else if (D == 4) { AOS2(4) }
 		else throw std::runtime_error("GridEncoding: number of input dims must be 2, 3 or 4");
 #undef AOS2
+		TCNN_HIP_CHECK(hipGetLastError());
+		return;
+	}
+	if (soa && F == 2 && interp != Interp::Nearest) {
+		const dim3 g4(div_round_up(B, 256), div_round_up(L, 4));
+		const uint32_t* t32 = (const uint32_t*)table16;
+		_Float16* o16 = (_Float16*)out16;
+		const uint32_t hg = hash_grid ? 1u : 0u, in = (uint32_t)interp;
+#define SOA2(DD)                                                                                                                   \
+	switch (h) {                                                                                                                   \
+		case HashType::Prime: hipLaunchKernelGGL((k_grid_fwd_soa_f2<DD, HashType::Prime>), g4, dim3(256), 0, st, B, pos, pos_stride, t32, o16, levels, hg, in, go, L); break; \
+		case HashType::ReversedPrime: hipLaunchKernelGGL((k_grid_fwd_soa_f2<DD, HashType::ReversedPrime>), g4, dim3(256), 0, st, B, pos, pos_stride, t32, o16, levels, hg, in, go, L); break; \
+		default: hipLaunchKernelGGL((k_grid_fwd_soa_f2<DD, HashType::CoherentPrime>), g4, dim3(256), 0, st, B, pos, pos_stride, t32, o16, levels, hg, in, go, L); break; \
+	}
+		if (D == 2) { SOA2(2) }
+		else if (D == 3) { SOA2(3) }
+		else if (D == 4) { SOA2(4) }
+		else throw std::runtime_error("GridEncoding: number of input dims must be 2, 3 or 4");
+#undef SOA2
 		TCNN_HIP_CHECK(hipGetLastError());
 		return;
 	}

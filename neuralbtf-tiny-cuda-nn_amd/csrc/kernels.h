@@ -136,7 +136,8 @@ void launch_fused_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, ui
                         const float* pos, const float* target, void* out16, void* dLdenc_pairs,
                         float* wgrad_partial, float* loss_partial, const LevelInfo* levels, bool hash_grid,
                         Interp interp, uint32_t n_blocks, const void* dout16, const void* wimage, uint32_t loss_l2 = 0, bool inrange_index = false,
-                        const void* enc16 = nullptr);  // enc16: the encoding read from memory, SoA [IN][B] (no gathers)
+                        const void* enc16 = nullptr,  // enc16: the encoding read from memory, SoA [IN][B] (no gathers)
+                        float dout_scale = 1.0f);     // dout16 is used as fp16(dout16 * dout_scale)
 // LDS weight image of the fused kernels, built once per parameter update.
 size_t fused_weight_image_bytes(uint32_t W, uint32_t IN, uint32_t NH);
 void launch_pack_weights(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, const void* params16, void* image);
@@ -241,6 +242,7 @@ void launch_cast_f16_f32(hipStream_t st, const void* in, float* out, size_t n);
 void launch_scale_f16(hipStream_t st, const void* in, void* out, float s, size_t n);
 void launch_div_f32(hipStream_t st, float* x, float s, size_t n);
 void launch_div_f16(hipStream_t st, const void* in, void* out, float s, size_t n, bool out_f32);
+void launch_grad_finalize(hipStream_t st, const float* g, void* out, float s, size_t n, bool out_f32);
 
 // RelativeL2 (standalone, reference relative_l2.h:40-76): pred fp16 [B][stride] -> values, grads
 void launch_relative_l2(hipStream_t st, uint32_t B, uint32_t stride, uint32_t dims, float loss_scale,

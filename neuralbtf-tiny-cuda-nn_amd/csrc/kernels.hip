@@ -197,6 +197,21 @@ __global__ void k_div_f16(const _Float16* __restrict__ in, void* __restrict__ ou
 	if (out_f32) ((float*)out)[i] = (float)h;
 	else ((_Float16*)out)[i] = h;
 }
+// fp32 gradient sum -> the binding's parameter gradient fp16(fp16(g) / s): the module's fp16 gradient
+// buffer (cast) divided by the loss scale in torch (fp16 / scalar), in one pass
+__global__ void k_grad_finalize(const float* __restrict__ g, void* __restrict__ out, float s, size_t n, int out_f32) {
+	const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	const _Float16 h = f16_rn((float)(_Float16)g[i] / s);
+	if (out_f32) ((float*)out)[i] = (float)h;
+	else ((_Float16*)out)[i] = h;
+}
+void launch_grad_finalize(hipStream_t st, const float* g, void* out, float s, size_t n, bool out_f32) {
+	if (!n) return;
+	hipLaunchKernelGGL(k_grad_finalize, dim3(div_round_up(n, 256)), dim3(256), 0, st, g, out, s, n, out_f32 ? 1 : 0);
+	TCNN_HIP_CHECK(hipGetLastError());
+}
+
 void launch_scale_f16(hipStream_t st, const void* in, void* out, float s, size_t n) {
 	if (!n) return;
 	hipLaunchKernelGGL(k_scale_f16, dim3(div_round_up(n, 256)), dim3(256), 0, st, (const _Float16*)in, (_Float16*)out, s, n);

@@ -298,6 +298,7 @@ struct FusedTrainArgs {
 	uint32_t hash_grid;
 	uint32_t interp;
 	const _Float16* dout;   // EXT_DOUT: external dL/d(output) fp16 [B][16] (loss-scaled by the caller)
+	float dout_scale;       // EXT_DOUT: dL/dy = fp16(dout * dout_scale) (the torch binding's loss scale; 1: as given)
 	const _Float16* enc;    // ENC_MEM: the encoding kept by the forward, SoA [IN][B] (no gathers)
 	unsigned long long* prof;  // diagnostic build only: per-wave phase cycle sums [waves][8]
 };
@@ -400,7 +401,8 @@ __device__ __forceinline__ void slice_fwd_loss(const FusedTrainArgs& a, uint32_t
 				// forward (registers); register r of lane group q = output 4r + q (out_row)
 				(void)Gext;
 				const _Float16* dp = a.dout + (size_t)i * 16 + q;
-				G[tau] = h4{dp[0], dp[4], dp[8], dp[12]};
+				const float ds = a.dout_scale;  // x 1 is exact: fp16(h * 1) = h
+				G[tau] = h4{f16_rn((float)dp[0] * ds), f16_rn((float)dp[4] * ds), f16_rn((float)dp[8] * ds), f16_rn((float)dp[12] * ds)};
 				continue;
 			}
 			const h4 y = __builtin_convertvector(yacc[tau], h4);

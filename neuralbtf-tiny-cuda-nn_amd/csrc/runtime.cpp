@@ -593,7 +593,8 @@ void NetworkHost::inference(hipStream_t st, StepWorkspace& ws, uint32_t B, const
 	if (fused_ok() && mlp_infer_supported(mlp.width, IN, mlp.n_hidden_layers, mlp.padded_output, mlp.activation)) {
 		ws.enc16.reserve((size_t)IN * B * 2);
 		launch_grid_fwd(st, grid->desc.n_pos_dims, grid->desc.n_features_per_level, grid->desc.hash_type, B, grid->desc.n_levels,
-		                pos, grid->desc.n_pos_dims, eparams, ws.enc16.p, true, 0, grid->dev_levels(), grid->hash_grid(), grid->desc.interp);
+		                pos, grid->desc.n_pos_dims, eparams, ws.enc16.p, true, 0, grid->dev_levels(), grid->hash_grid(), grid->desc.interp,
+		                grid->opts());
 		if (!(trust_image && ws.wimage_valid)) {
 			ws.wimage.reserve(fused_weight_image_bytes(mlp.width, IN, mlp.n_hidden_layers));
 			launch_pack_weights(st, mlp.width, IN, mlp.n_hidden_layers, params16, ws.wimage.p);
@@ -627,7 +628,8 @@ int NetworkHost::forward_keep(hipStream_t st, StepWorkspace& ws, uint32_t B, con
 	if (layout == KEEP_FUSED_SOA && mlp_infer_supported(mlp.width, IN, mlp.n_hidden_layers, mlp.padded_output, mlp.activation)) {
 		keep.reserve((size_t)IN * B * 2);
 		launch_grid_fwd(st, grid->desc.n_pos_dims, grid->desc.n_features_per_level, grid->desc.hash_type, B, grid->desc.n_levels, pos,
-		                grid->desc.n_pos_dims, eparams, keep.p, true, 0, grid->dev_levels(), grid->hash_grid(), grid->desc.interp);
+		                grid->desc.n_pos_dims, eparams, keep.p, true, 0, grid->dev_levels(), grid->hash_grid(), grid->desc.interp,
+		                grid->opts());
 		ws.wimage.reserve(fused_weight_image_bytes(mlp.width, IN, mlp.n_hidden_layers));
 		launch_pack_weights(st, mlp.width, IN, mlp.n_hidden_layers, params16, ws.wimage.p);
 		launch_mlp_infer(st, mlp.width, IN, mlp.n_hidden_layers, mlp.activation, true, B, ws.wimage.p, keep.p, out16);
@@ -679,7 +681,8 @@ void NetworkHost::fused_kernel(hipStream_t st, StepWorkspace& ws, uint32_t B, co
 	                   mlp.activation, B, dims, loss_scale, params16, table, pos, target, out16, ws.dLdenc.p,
 	                   ws.wgrad_partial.as<float>(), ws.loss_partial.as<float>(), grid->dev_levels(), grid->hash_grid(),
 	                   grid->desc.interp, nb, dout16, ws.wimage.p, loss_l2,
-	                   grid->inrange_index_ok && grid->desc.interp == Interp::Linear && !sw.no_inrange_index, enc_soa);
+	                   grid->inrange_index_ok && grid->desc.interp == Interp::Linear && !sw.no_inrange_index, enc_soa,
+	                   dout16 ? ext_dout_scale : 1.0f);
 }
 
 void NetworkHost::grid_backward(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, GridBwdEpilogue* ep) {
@@ -704,10 +707,20 @@ void NetworkHost::fwd_bwd_fused(hipStream_t st, StepWorkspace& ws, uint32_t B, c
 	const uint32_t n_mlp = mlp.n_params();
 	fused_kernel(st, ws, B, pos, target, dims, loss_scale, params16, true, dout16, out16, enc_soa);
 	if (mark) mark(1);
-	grid_backward(st, ws, B, pos);
+	// the network-gradient column sums run in the grid backward's spare workgroups (the epilogue
+	// without Adam: block_column_sums, the order of launch_column_sums), not as a launch of their own
+	GridBwdEpilogue ep{};
+	ep.enabled = 1;
+	ep.apply_adam = 0;
+	ep.buf.g32 = grad32;
+	ep.n_mlp_groups = MLP_TAIL_GROUPS;
+	ep.n_mlp = n_mlp;
+	ws.loss_sum.reserve(16);
+	ep.d_loss = ws.loss_sum.as<float>();
+	TCNN_CHECK(n_mlp % 4 == 0, "network parameter count must be a multiple of 4");
+	grid_backward(st, ws, B, pos, &ep);
 	grid->backward_acc(st, ws.gbw, B, ws.dLdenc.p, 0, 0, grad32 + n_mlp);
 	if (mark) mark(2);
-	launch_column_sums(st, ws.wgrad_partial.as<float>(), ws.n_fused_blocks, n_mlp, grad32);
 	grid->reduce_items(st, ws.gbw, grad32 + n_mlp);
 	if (mark) mark(3);
 }
@@ -931,7 +944,7 @@ void TrainerHost::training_step_overlapped(hipStream_t st, uint32_t B, const flo
 		const GridEncodingHost& g = *m.grid;
 		ws.enc16.reserve((size_t)m.mlp.n_input * B * 2);
 		launch_grid_fwd(st, g.desc.n_pos_dims, g.desc.n_features_per_level, g.desc.hash_type, B, g.desc.n_levels, input, g.desc.n_pos_dims,
-		                (const uint8_t*)w16.p + n_mlp * 2, ws.enc16.p, true, 0, g.dev_levels(), g.hash_grid(), g.desc.interp);
+		                (const uint8_t*)w16.p + n_mlp * 2, ws.enc16.p, true, 0, g.dev_levels(), g.hash_grid(), g.desc.interp, g.opts());
 		enc_soa = ws.enc16.p;
 	}
 	m.fused_kernel(st, ws, B, input, target, n_output_dims, loss_scale, w16.p, false, nullptr, nullptr, enc_soa);

@@ -194,6 +194,7 @@ struct StepWorkspace {
 	GridBwdBufs gbw;
 	DevBuf acts, delta0, delta1, dout16, red_tmp;  // layer-wise engine
 	DevBuf tile_wT;  // tile engine: transposed copy of the streamed hidden matrices
+	DevBuf loss_sum;  // the grid backward epilogue's loss sum where nobody reads it (fwd_bwd_fused)
 	uint32_t n_fused_blocks = 0, n_loss_partials = 0;
 	bool wimage_valid = false;  // fused weight image matches the current fp16 params (trainer fast path)
 };
@@ -207,6 +208,9 @@ struct StepWorkspace {
 //             per-layer MFMA kernels (mlp_layers.hip) with fp16 activations in HBM.
 struct NetworkHost {
 	EngineSwitches sw = EngineSwitches::from_env();
+	// the fused kernel reads an external dL/dy as fp16(dL/dy * ext_dout_scale): the torch binding's loss
+	// scale folded into the load (set only around a Module backward, tcnn_module_backward_scaled)
+	float ext_dout_scale = 1.0f;
 	std::unique_ptr<EncodingHost> enc;
 	GridEncodingHost* grid = nullptr;  // enc->grid when the encoding is a grid
 	MlpHost mlp;

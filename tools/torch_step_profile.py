@@ -19,7 +19,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "neuralbtf-tiny-cuda-nn_amd")]
 
 
-def run(iters, batches):
+def run(iters, batches, fused_adam=False):
     import torch
     from bench import rgb_field_torch
     import tinycudann as tcnn
@@ -32,7 +32,7 @@ def run(iters, batches):
         pos = torch.rand(B, 2, device="cuda")
         tgt = rgb_field_torch(pos)
         model = tcnn.NetworkWithInputEncoding(2, 3, cfg["encoding"], cfg["network"]).cuda()
-        opt = torch.optim.Adam(model.parameters(), lr=0.01)
+        opt = torch.optim.Adam(model.parameters(), lr=0.01, fused=True) if fused_adam else torch.optim.Adam(model.parameters(), lr=0.01)
         phases = ["forward", "loss", "zero_grad", "backward", "optimizer"]
         host = dict.fromkeys(phases, 0.0)
 
@@ -100,7 +100,8 @@ def run(iters, batches):
         ev[1].record()
         torch.cuda.synchronize()
         tr = ev[0].elapsed_time(ev[1]) * 1e-3 / iters
-        row = {"batch": B, "torch_step_s": wall, "torch_host_issue_s": (h1 - h0) / iters, "torch_gpu_busy_s": busy,
+        row = {"batch": B, "optimizer": "torch.optim.Adam(fused=True)" if fused_adam else "torch.optim.Adam (default)",
+               "torch_step_s": wall, "torch_host_issue_s": (h1 - h0) / iters, "torch_gpu_busy_s": busy,
                "host_s_by_phase": {k: v / iters for k, v in host.items()}, "gpu_kernels_per_step": n_kernels,
                "trainer_step_s": tr, "torch_over_trainer": wall / tr}
         rows.append(row)
@@ -117,7 +118,8 @@ def main():
     args = ap.parse_args()
     res = {"what": "torch NetworkWithInputEncoding training step (reference mlp_learning_an_image_pytorch.py:159-170): "
                    "host issue time per phase, GPU time per step, vs Trainer::training_step; config_hash.json",
-           "rows": run(args.iters, tuple(int(b) for b in args.batches.split(",")))}
+           "rows": run(args.iters, tuple(int(b) for b in args.batches.split(","))) +
+                   run(args.iters, tuple(int(b) for b in args.batches.split(",")), fused_adam=True)}
     if args.out:
         with open(args.out, "w") as f:
             json.dump(res, f, indent=1)
