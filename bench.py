@@ -188,13 +188,15 @@ def main():
                     help="strong: shard the global batch over ranks (configs[4]); weak: a full batch per rank")
     ap.add_argument("--allreduce-dtype", choices=["fp32", "fp16"], default="fp32")
     ap.add_argument("--no-overlap", action="store_true", help="all-reduce after the whole backward")
-    ap.add_argument("--optimizer", choices=["sharded", "replicated"], default="replicated",
-                    help="N > 1: replicated = all-reduce of the gradient sums, Adam everywhere (default: the schedule "
-                         "with the plainest collective; no multi-GPU RCCL run of either is recorded yet); sharded = "
-                         "reduce-scatter, Adam on 1/N of the parameters, all-gather of the fp16 parameters")
-    ap.add_argument("--exchange", choices=["torch", "engine"], default="torch",
-                    help="N > 1: torch = torch.distributed collectives driven from Python; engine = RCCL issued by "
-                         "the training step itself (tcnn_trainer_set_dp: one call per step, hipGraph-capturable)")
+    ap.add_argument("--optimizer", choices=["sharded", "replicated"], default="sharded",
+                    help="N > 1: sharded (default) = each rank's Adam on 1/N of the parameters after summing that shard's "
+                         "gradients, then the fp16 parameters gathered; replicated = all-reduce of the gradient sums, Adam "
+                         "everywhere (exchange torch/engine only)")
+    ap.add_argument("--exchange", choices=["peer", "engine", "torch"], default="peer",
+                    help="N > 1: peer (default) = the engine sums the shards straight from the other ranks' memory over "
+                         "xGMI (csrc/dp_peer.hip; falls back to engine if a rank cannot map its peers); engine = RCCL "
+                         "issued by the training step itself (tcnn_trainer_set_dp); torch = torch.distributed collectives "
+                         "driven from Python")
     ap.add_argument("--graph", action="store_true", help="replay the single-GPU training step as a hipGraph")
     ap.add_argument("--all-ranks-on-device0", action="store_true",
                     help="rehearse N>1 on a 1-GPU box (gloo); never used for measurements")
@@ -252,8 +254,11 @@ def main():
     from tinycudann.parallel import DataParallelTrainer
     sharded = world > 1 and args.optimizer == "sharded" and args.allreduce_dtype == "fp32"
     exchange = args.exchange if args.allreduce_dtype == "fp32" else "torch"
+    if exchange == "peer":
+        sharded = world > 1  # the peer exchange is the sharded schedule
     dp = DataParallelTrainer(trainer, overlap=not args.no_overlap, allreduce_dtype=args.allreduce_dtype,
-                             shard_optimizer=sharded, exchange=exchange)
+                             shard_optimizer=sharded, exchange=exchange, peer_fallback=True)
+    exchange = dp.exchange  # what actually runs (peer falls back to engine collectively)
     if args.graph:
         trainer.set_graph(True)
 
@@ -320,7 +325,8 @@ def main():
                             else f"dp{world} ({B} points per rank)") +
                            ((", fp32 reduce-scatter + Adam on 1/N of the parameters + fp16 all-gather (sharded optimizer)" if sharded else
                              f", {args.allreduce_dtype} all-reduce" + ("" if args.no_overlap else " overlapped with the grid backward")) +
-                            (", RCCL issued by the engine's step" if exchange == "engine" else ", torch.distributed from Python")
+                            (", peer-memory exchange over xGMI issued by the engine's step (no collective library)" if exchange == "peer" else
+                             ", RCCL issued by the engine's step" if exchange == "engine" else ", torch.distributed from Python")
                             if world > 1 else ""),
         },
         "step_graph": bool(args.graph),

@@ -168,6 +168,23 @@ uint32_t tcnn_trainer_padded_output_width(const tcnn_trainer* t);
  * optimizer: each rank updates its shard of the reduce-scattered gradient sums; the caller then
  * all-gathers the fp16 parameters). Not in the reference, which has no multi-GPU path. */
 int tcnn_trainer_optimizer_step_range(tcnn_trainer* t, void* stream, uint64_t begin, uint64_t end);
+/* Data-parallel exchange over peer-mapped device memory (xGMI / same-device IPC), no collective
+ * library: every rank of a node exports a blob of tcnn_dp_peer_blob_bytes() bytes (IPC handles of its
+ * gradient, parameter and optimizer-state buffers and of its step counters), the caller gathers the
+ * N blobs in rank order (any host transport) and every rank attaches them; from then on each
+ * training_step(run_optimizer = 1) sums the ranks' gradient sums for this rank's 1/N shard directly
+ * from the peers' memory, runs Adam on that shard (gradient scale 1/N) and copies the other shards'
+ * updated fp16 parameters -- one C-ABI call per step, no host synchronisation. The optimizer state
+ * is sharded like the RCCL sharded schedule (tcnn_trainer_dp_gather_state completes it). Detach is
+ * collective (every rank calls it). A rank that does not arrive within 10 s raises an error at the
+ * next call instead of hanging the GPU. */
+uint64_t tcnn_dp_peer_blob_bytes(void);
+int tcnn_trainer_dp_peer_export(tcnn_trainer* t, int nranks, int rank, void* blob);
+int tcnn_trainer_dp_peer_attach(tcnn_trainer* t, const void* blobs);
+int tcnn_trainer_dp_peer_detach(tcnn_trainer* t);
+/* Drop this rank's export / attachment without the collective barrier -- only before any exchange
+ * step ran, e.g. when another rank failed to attach (the caller then falls back to another exchange). */
+int tcnn_trainer_dp_peer_abandon(tcnn_trainer* t);
 /* ---- data-parallel exchange inside the engine (not in the reference, which has no multi-GPU path;
  * SURVEY.md §5, §8(e)) ----
  * One process per GPU. Rank 0 creates a unique id, the caller broadcasts its TCNN_DP_ID_BYTES bytes

@@ -562,6 +562,19 @@ void tcnn_dp_comm_destroy(tcnn_dp_comm* c) { delete c; }
 int tcnn_trainer_set_dp(tcnn_trainer* t, tcnn_dp_comm* c, int sharded) {
 	return guard([&] { t->t->set_dp(c ? c->c.get() : nullptr, sharded != 0); });
 }
+uint64_t tcnn_dp_peer_blob_bytes(void) { return tcnn_amd::dp_peer_blob_bytes(); }
+int tcnn_trainer_dp_peer_export(tcnn_trainer* t, int nranks, int rank, void* blob) {
+	return guard([&] { t->t->dp_peer_export(nranks, rank, blob); });
+}
+int tcnn_trainer_dp_peer_attach(tcnn_trainer* t, const void* blobs) {
+	return guard([&] { t->t->dp_peer_attach(blobs); });
+}
+int tcnn_trainer_dp_peer_detach(tcnn_trainer* t) {
+	return guard([&] { t->t->dp_peer_detach(); });
+}
+int tcnn_trainer_dp_peer_abandon(tcnn_trainer* t) {
+	return guard([&] { t->t->dp_peer_abandon(); });
+}
 int tcnn_trainer_dp_gather_state(tcnn_trainer* t, void* stream) {
 	return guard([&] { t->t->dp_gather_state((hipStream_t)stream); });
 }

@@ -120,6 +120,7 @@ void TrainerHost::set_dp(DpComm* c, bool sharded) {
 	// fp16 weights of the other shards. This makes set_dp collective whenever state is partial: every
 	// rank of the old communicator calls it (as every rank calls the sharded step).
 	if (dp && dp_sharded && dp_state_partial) dp_gather_state(nullptr);
+	TCNN_CHECK(!(c && peer_attached), "set_dp: the trainer is attached to a peer exchange (detach it first)");
 	TCNN_HIP_CHECK(hipDeviceSynchronize());
 	dp = c;
 	dp_sharded = c && sharded;
@@ -197,6 +198,10 @@ void TrainerHost::training_step_dp(hipStream_t st, uint32_t B, const float* inpu
 // All-gather the sharded optimizer state so every rank holds the full vectors (fp32 masters, Adam
 // moments, per-parameter step counts), e.g. before serialize(with_optimizer).
 void TrainerHost::dp_gather_state(hipStream_t st) {
+	if (peer_attached) {
+		if (dp_state_partial) dp_peer_gather_state(st);
+		return;
+	}
 	if (!dp || !dp_sharded || !dp_state_partial) return;
 	for (DevBuf* b : {&w32, &m1, &m2, &steps}) dp->all_gather(b->p, (size_t)dp_per, 4, st);
 	TCNN_HIP_CHECK(hipStreamSynchronize(st));

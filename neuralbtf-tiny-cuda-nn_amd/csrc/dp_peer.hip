@@ -1,0 +1,380 @@
+// dp_peer.hip -- the data-parallel exchange over peer-mapped device memory (xGMI), without a
+// collective library.
+//
+// Why: at 8 ranks a rank's step is 2^15 points (~48 us on one MI355X) while every RCCL collective
+// costs ~28 us of latency (profiles/r03_dp_floor.json), so the RCCL schedules cannot scale. Here the
+// ranks of a node exchange through each other's memory directly: every rank exports IPC handles of
+// its gradient / parameter / optimizer-state buffers and a small flag array; after attaching, one
+// training step is
+//   local step (fused kernel, grid backward; the gradient sums complete in g32)
+//   -> signal "gradients ready" (a monotonic per-rank counter in the rank's own flag array)
+//   -> wait until every rank's counter reached this step (one workgroup polls; timeout guarded)
+//   -> Adam on this rank's 1/N shard, reading the gradient of parameter i as
+//      sum_p g32_p[i] over the ranks p = 0 .. N-1 in that fixed order (peer loads over xGMI)
+//   -> signal "weights ready" -> wait -> copy the other ranks' updated fp16 shards into w16.
+// Per rank and step that moves (N-1)/N of 4 + 2 bytes per parameter over the links -- the
+// reduce-scatter + all-gather volume -- with no collective launch, no proxy thread and no host
+// involvement; every kernel reads its step counter from device memory, so the step is also
+// graph-capturable. The shards are summed in rank order on the rank that owns them, so replicas
+// stay bit-identical (and, for two ranks, bit-identical to any all-reduce: a + b is one sum).
+//
+// Coherence without fences: everything another rank reads -- this rank's gradient sums, its updated
+// fp16 shard, its optimizer-state shard when gathered, and the step counters -- lives in UNCACHED
+// device memory (hipDeviceMallocUncached: every access goes to memory, as RCCL allocates its
+// protocol buffers), written once and read once per step, so no L2 holds a stale copy and no
+// acquire / release cache maintenance is needed (a first version used fine-grained-free buffers with
+// a system-scope acquire per workgroup: 147 us per step on one rank, the repeated L2 invalidations).
+// The parameters the kernels re-read (the grid table) stay in ordinary memory: the gather copies the
+// peers' shards from their uncached mirrors into it. Kernel boundaries order the stores of one rank's
+// stream; the counters are stored and polled with system-scope atomics.
+//
+// Waits are one-workgroup kernels of their own (the data kernels launch after them), so a waiting
+// rank never occupies the CUs another rank on the same GPU needs to make progress (the 2-process
+// test shares one GPU). Every wait gives up after a timeout, raising an error flag in host-mapped
+// memory that the next step (or gather) turns into an exception -- a dead peer cannot hang the GPU.
+#include <cstring>
+#include <vector>
+
+#include "adam_device.h"
+#include "runtime.h"
+
+namespace tcnn_amd {
+
+namespace {
+
+constexpr uint32_t PEER_MAGIC = 0x50454552u;  // "PEER"
+constexpr int PEER_NBUF = 4;                  // exported: gradient sums, fp16 shard mirror, state staging, counters
+enum PeerBuf { PB_G32 = 0, PB_W16, PB_STATE, PB_FLAGS };
+enum PeerSlot { SLOT_GRAD = 0, SLOT_WEIGHTS = 1, SLOT_GATHER = 2, SLOT_DETACH = 3 };
+enum PeerCtr { CTR_STEP = 0, CTR_SYNC = 1 };
+
+struct PeerBlob {
+	uint32_t magic, nranks, rank, device;
+	uint64_t n_params, per;
+	hipIpcMemHandle_t h[PEER_NBUF];
+};
+
+__device__ __forceinline__ uint32_t load_sys(const uint32_t* p) {
+	return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// counter ctr[c] (+1 when bump), then flags[slot] = that value (system-scope store; every earlier
+// write of this stream went to uncached memory and finished with its kernel)
+__global__ void k_peer_signal(uint32_t* __restrict__ ctr, int c, int bump, uint32_t* __restrict__ flags, int slot) {
+	if (threadIdx.x != 0) return;
+	uint32_t v = ctr[c];
+	if (bump) {
+		v += 1u;
+		ctr[c] = v;
+	}
+	__hip_atomic_store(flags + slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// one workgroup: wait until every rank's flags[slot] reached ctr[c]; on timeout raise *err (host-mapped)
+__global__ void k_peer_wait(uint32_t* const* __restrict__ flag_ptrs, int nranks, int slot, const uint32_t* __restrict__ ctr, int c,
+                            long long timeout_ticks, int* __restrict__ err) {
+	if (threadIdx.x != 0) return;
+	const uint32_t target = ctr[c];
+	const long long t0 = wall_clock64();
+	for (int p = 0; p < nranks; ++p) {
+		while ((int32_t)(load_sys(flag_ptrs[p] + slot) - target) < 0) {
+			if (wall_clock64() - t0 > timeout_ticks) {
+				__hip_atomic_store(err, 1 + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+				return;
+			}
+			__builtin_amdgcn_s_sleep(2);
+		}
+	}
+}
+
+// Adam on this rank's shard [a.begin, a.n) with the gradient summed over the ranks' gradient sums in
+// rank order (g_0 + g_1 + ...); the updated fp16 parameter also goes to the uncached mirror the other
+// ranks gather from
+__global__ __launch_bounds__(256) void k_peer_adam(const AdamArgs a, const AdamBuffers s, const float* const* __restrict__ gptrs,
+                                                   int nranks, _Float16* __restrict__ w16_mirror) {
+	const uint32_t i = a.begin + blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= a.n) return;
+	float v[8];
+	float gsum = 0.0f;
+	for (int p0 = 0; p0 < nranks; p0 += 8) {  // loads in flight together, additions in rank order
+#pragma unroll
+		for (int u = 0; u < 8; ++u)
+			if (p0 + u < nranks) v[u] = gptrs[p0 + u][i];
+#pragma unroll
+		for (int u = 0; u < 8; ++u)
+			if (p0 + u < nranks) gsum = (p0 + u == 0) ? v[0] : gsum + v[u];  // no 0 + g_0: a -0 stays -0
+	}
+	s.g32[i] = gsum;
+	w16_mirror[i] = adam_update(a, s, i, gsum);
+}
+
+// copy every other rank's shard of up to 4 buffers (blockIdx.y) from its mirror into the local arrays,
+// 16 bytes per thread; shard bytes are multiples of 16
+struct PeerGatherArgs {
+	uint8_t* local[4];
+	const uint8_t* const* peers[4];  // device arrays [nranks] of the peers' mirrors
+	uint64_t peer_offset[4];         // byte offset of this buffer inside each mirror
+	uint32_t elem_bytes[4];
+	uint32_t nranks, rank;
+	uint64_t per;  // elements per shard
+};
+__global__ __launch_bounds__(256) void k_peer_gather(const PeerGatherArgs g) {
+	const uint32_t b = blockIdx.y;
+	const uint64_t shard_bytes = g.per * g.elem_bytes[b];
+	const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // 16-byte unit over all ranks' shards
+	const uint64_t units = shard_bytes / 16;
+	const uint64_t p = q / units;
+	if (p >= g.nranks || p == g.rank) return;
+	const uint64_t off = p * shard_bytes + (q % units) * 16;
+	*(uint4*)(g.local[b] + off) = *(const uint4*)(g.peers[b][p] + g.peer_offset[b] + off);
+}
+
+// this rank's shard of the optimizer state into its uncached staging mirror (for the peers' gather)
+__global__ __launch_bounds__(256) void k_peer_stage(const float* __restrict__ w32, const float* __restrict__ m1, const float* __restrict__ m2,
+                                                    const uint32_t* __restrict__ steps, uint32_t* __restrict__ stage, uint64_t lo,
+                                                    uint64_t cnt, uint64_t stride) {
+	const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (k >= cnt) return;
+	const uint64_t i = lo + k;
+	stage[i] = __float_as_uint(w32[i]);
+	stage[stride + i] = __float_as_uint(m1[i]);
+	stage[2 * stride + i] = __float_as_uint(m2[i]);
+	stage[3 * stride + i] = steps[i];
+}
+
+}  // namespace
+
+struct TrainerHost::PeerDp {
+	int nranks = 1, rank = 0;
+	uint64_t per = 0;
+	bool attached = false;
+	DevBuf ctr;    // [2] local counters (step, sync)
+	DevBuf ptrs;   // [PEER_NBUF][nranks] device pointers (local ones for this rank)
+	// uncached, exported: gradient sums [N*per] fp32, fp16 shard mirror [N*per], state staging
+	// [4][N*per] (w32, m1, m2, steps), counters [64] uint32
+	void* x[PEER_NBUF] = {nullptr, nullptr, nullptr, nullptr};
+	std::vector<void*> opened;  // IPC mappings of the peers' buffers
+	int* err_host = nullptr;
+	int* err_dev = nullptr;
+	long long timeout_ticks = 0;
+	PeerDp() = default;
+	~PeerDp() {
+		for (void* p : opened) (void)hipIpcCloseMemHandle(p);
+		for (void* p : x)
+			if (p) (void)hipFree(p);
+		if (err_host) (void)hipHostFree(err_host);
+	}
+	template <typename T>
+	T* const* table(int b) const { return (T* const*)(ptrs.as<void*>() + (size_t)b * nranks); }
+	void check() const {
+		if (err_host && *(volatile int*)err_host)
+			throw std::runtime_error("data-parallel peer exchange: rank " + std::to_string(*(volatile int*)err_host - 1) +
+			                         " did not arrive within the timeout (a rank stopped, or the ranks' steps diverged)");
+	}
+};
+
+uint64_t dp_peer_blob_bytes() { return sizeof(PeerBlob); }
+
+static void grow_keep(DevBuf& b, size_t bytes, size_t valid) {
+	if (b.bytes >= bytes) return;
+	DevBuf n;
+	n.reserve(bytes);
+	TCNN_HIP_CHECK(hipMemset(n.p, 0, bytes));
+	if (b.p && valid) TCNN_HIP_CHECK(hipMemcpy(n.p, b.p, valid, hipMemcpyDeviceToDevice));
+	std::swap(b.p, n.p);
+	std::swap(b.bytes, n.bytes);
+}
+
+void TrainerHost::dp_peer_export(int nranks, int rank, void* blob_out) {
+	TCNN_CHECK(!dp, "peer exchange: detach the RCCL communicator first (set_dp(NULL))");
+	TCNN_CHECK(nranks >= 1 && rank >= 0 && rank < nranks, "peer exchange: rank outside [0, nranks)");
+	TCNN_CHECK(overlapped_ok(), "peer exchange: needs the fused grid engine (the step's gradient sums in one buffer)");
+	if (peer) dp_peer_detach();
+	TCNN_HIP_CHECK(hipDeviceSynchronize());
+	auto pd = std::make_shared<PeerDp>();
+	pd->nranks = nranks;
+	pd->rank = rank;
+	// shards of a multiple of 8 parameters: 16-byte units of fp16 and fp32 shards alike
+	const uint64_t per = ((n_params + nranks - 1) / nranks + 7) / 8 * 8;
+	pd->per = per;
+	const size_t pad = (size_t)(per * nranks);
+	grow_keep(w32, pad * 4, n_params * 4);
+	grow_keep(w16, pad * 2, n_params * 2);
+	grow_keep(g16, pad * 2, n_params * 2);
+	grow_keep(g32, pad * 4, n_params * 4);
+	grow_keep(m1, pad * 4, n_params * 4);
+	grow_keep(m2, pad * 4, n_params * 4);
+	grow_keep(steps, pad * 4, n_params * 4);
+	const size_t xbytes[PEER_NBUF] = {pad * 4, pad * 2, 4 * pad * 4, 256};
+	for (int k = 0; k < PEER_NBUF; ++k) {
+		TCNN_HIP_CHECK(hipExtMallocWithFlags(&pd->x[k], xbytes[k], hipDeviceMallocUncached));
+		TCNN_HIP_CHECK(hipMemset(pd->x[k], 0, xbytes[k]));
+	}
+	pd->ctr.reserve(64);
+	TCNN_HIP_CHECK(hipMemset(pd->ctr.p, 0, 64));
+	TCNN_HIP_CHECK(hipHostMalloc((void**)&pd->err_host, 64, hipHostMallocMapped));
+	*pd->err_host = 0;
+	TCNN_HIP_CHECK(hipHostGetDevicePointer((void**)&pd->err_dev, pd->err_host, 0));
+	int dev = 0, khz = 0;
+	TCNN_HIP_CHECK(hipGetDevice(&dev));
+	TCNN_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+	pd->timeout_ticks = (long long)std::max(khz, 1) * 1000LL * 10;  // 10 s
+	PeerBlob b;
+	std::memset(&b, 0, sizeof(b));
+	b.magic = PEER_MAGIC;
+	b.nranks = (uint32_t)nranks;
+	b.rank = (uint32_t)rank;
+	b.device = (uint32_t)dev;
+	b.n_params = n_params;
+	b.per = per;
+	for (int k = 0; k < PEER_NBUF; ++k) TCNN_HIP_CHECK(hipIpcGetMemHandle(&b.h[k], pd->x[k]));
+	std::memcpy(blob_out, &b, sizeof(b));
+	peer = std::move(pd);
+	ws.wimage_valid = false;
+}
+
+void TrainerHost::dp_peer_attach(const void* blobs) {
+	TCNN_CHECK(peer && !peer->attached, "peer exchange: export before attaching");
+	PeerDp& pd = *peer;
+	const int N = pd.nranks;
+	std::vector<void*> host((size_t)PEER_NBUF * N);
+	for (int p = 0; p < N; ++p) {
+		PeerBlob b;
+		std::memcpy(&b, (const uint8_t*)blobs + (size_t)p * sizeof(PeerBlob), sizeof(b));
+		TCNN_CHECK(b.magic == PEER_MAGIC && (int)b.nranks == N && (int)b.rank == p && b.n_params == n_params && b.per == pd.per,
+		           "peer exchange: blob " + std::to_string(p) + " does not describe rank " + std::to_string(p) + " of the same model");
+		for (int k = 0; k < PEER_NBUF; ++k) {
+			if (p == pd.rank) {
+				host[(size_t)k * N + p] = pd.x[k];
+				continue;
+			}
+			void* q = nullptr;
+			TCNN_HIP_CHECK(hipIpcOpenMemHandle(&q, b.h[k], hipIpcMemLazyEnablePeerAccess));
+			pd.opened.push_back(q);
+			host[(size_t)k * N + p] = q;
+		}
+	}
+	pd.ptrs.reserve(host.size() * sizeof(void*));
+	TCNN_HIP_CHECK(hipMemcpy(pd.ptrs.p, host.data(), host.size() * sizeof(void*), hipMemcpyHostToDevice));
+	pd.attached = true;
+	peer_attached = true;
+	dp_sharded = true;
+	dp_state_partial = false;
+	dp_per = pd.per;
+	grad_scale = grad_scale_user / (float)N;
+	if (graph) set_graph(use_graph);
+}
+
+void TrainerHost::peer_signal(hipStream_t st, int c, bool bump, int slot) {
+	hipLaunchKernelGGL(k_peer_signal, dim3(1), dim3(64), 0, st, peer->ctr.as<uint32_t>(), c, bump ? 1 : 0, (uint32_t*)peer->x[PB_FLAGS],
+	                   slot);
+	TCNN_HIP_CHECK(hipGetLastError());
+}
+
+void TrainerHost::peer_wait(hipStream_t st, int c, int slot) {
+	PeerDp& pd = *peer;
+	hipLaunchKernelGGL(k_peer_wait, dim3(1), dim3(64), 0, st, pd.table<uint32_t>(PB_FLAGS), pd.nranks, slot, pd.ctr.as<uint32_t>(), c,
+	                   pd.timeout_ticks, pd.err_dev);
+	TCNN_HIP_CHECK(hipGetLastError());
+}
+
+void TrainerHost::training_step_peer(hipStream_t st, uint32_t B, const float* input, const float* target) {
+	PeerDp& pd = *peer;
+	pd.check();
+	// this rank's gradient sums, straight into its uncached exchange buffer
+	training_step_overlapped(st, B, input, target, false, (float*)pd.x[PB_G32]);
+	peer_signal(st, CTR_STEP, true, SLOT_GRAD);
+	peer_wait(st, CTR_STEP, SLOT_GRAD);
+	const uint64_t lo = std::min<uint64_t>(n_params, (uint64_t)pd.rank * pd.per), hi = std::min<uint64_t>(n_params, lo + pd.per);
+	++adam_step;
+	AdamArgs a = adam_args_table(st, adam_step);
+	a.begin = (uint32_t)lo;
+	a.n = (uint32_t)hi;
+	const AdamBuffers s{w32.as<float>(), w16.as<_Float16>(), g32.as<float>(), g16.as<_Float16>(), m1.as<float>(), m2.as<float>(),
+	                    steps.as<uint32_t>()};
+	if (hi > lo)
+		hipLaunchKernelGGL(k_peer_adam, dim3(div_round_up(hi - lo, 256)), dim3(256), 0, st, a, s, pd.table<const float>(PB_G32), pd.nranks,
+		                   (_Float16*)pd.x[PB_W16]);
+	TCNN_HIP_CHECK(hipGetLastError());
+	peer_signal(st, CTR_STEP, false, SLOT_WEIGHTS);
+	peer_wait(st, CTR_STEP, SLOT_WEIGHTS);
+	peer_gather(st, 1);
+	ws.wimage_valid = false;
+	dp_state_partial = true;
+	last_B = B;
+}
+
+// copy the other ranks' shards from their mirrors: what = 1: the fp16 parameters; 4: fp32 masters,
+// both moments, step counts (from the staging mirror)
+void TrainerHost::peer_gather(hipStream_t st, int what) {
+	PeerDp& pd = *peer;
+	PeerGatherArgs g{};
+	g.nranks = (uint32_t)pd.nranks;
+	g.rank = (uint32_t)pd.rank;
+	g.per = pd.per;
+	const uint64_t pad = pd.per * (uint64_t)pd.nranks;
+	if (what == 1) {
+		g.local[0] = (uint8_t*)w16.p;
+		g.peers[0] = pd.table<const uint8_t>(PB_W16);
+		g.elem_bytes[0] = 2;
+	} else {
+		void* loc[4] = {w32.p, m1.p, m2.p, steps.p};
+		for (int k = 0; k < 4; ++k) {
+			g.local[k] = (uint8_t*)loc[k];
+			g.peers[k] = pd.table<const uint8_t>(PB_STATE);
+			g.peer_offset[k] = (uint64_t)k * pad * 4;
+			g.elem_bytes[k] = 4;
+		}
+	}
+	uint32_t maxb = 0;
+	for (int k = 0; k < what; ++k) maxb = std::max(maxb, g.elem_bytes[k]);
+	const uint64_t units = pd.per * maxb / 16 * (uint64_t)pd.nranks;
+	hipLaunchKernelGGL(k_peer_gather, dim3(div_round_up(units, 256), what), dim3(256), 0, st, g);
+	TCNN_HIP_CHECK(hipGetLastError());
+}
+
+void TrainerHost::dp_peer_gather_state(hipStream_t st) {
+	PeerDp& pd = *peer;
+	pd.check();
+	const uint64_t lo = std::min<uint64_t>(n_params, (uint64_t)pd.rank * pd.per), hi = std::min<uint64_t>(n_params, lo + pd.per);
+	if (hi > lo)
+		hipLaunchKernelGGL(k_peer_stage, dim3(div_round_up(hi - lo, 256)), dim3(256), 0, st, w32.as<float>(), m1.as<float>(), m2.as<float>(),
+		                   steps.as<uint32_t>(), (uint32_t*)pd.x[PB_STATE], lo, hi - lo, pd.per * (uint64_t)pd.nranks);
+	TCNN_HIP_CHECK(hipGetLastError());
+	peer_signal(st, CTR_SYNC, true, SLOT_GATHER);
+	peer_wait(st, CTR_SYNC, SLOT_GATHER);
+	peer_gather(st, 4);
+	TCNN_HIP_CHECK(hipStreamSynchronize(st));
+	pd.check();
+	dp_state_partial = false;
+}
+
+// collective: completes the sharded state, then waits until every rank has stopped reading this
+// rank's mirrors before the mappings are closed and the mirrors freed
+void TrainerHost::dp_peer_detach() {
+	if (!peer) return;
+	if (peer->attached) {
+		if (dp_state_partial) dp_peer_gather_state(nullptr);
+		peer_signal(nullptr, CTR_SYNC, true, SLOT_DETACH);
+		peer_wait(nullptr, CTR_SYNC, SLOT_DETACH);
+		TCNN_HIP_CHECK(hipDeviceSynchronize());
+	}
+	peer.reset();
+	peer_attached = false;
+	dp_sharded = false;
+	dp_state_partial = false;
+	grad_scale = grad_scale_user;
+	if (graph) set_graph(use_graph);
+}
+
+void TrainerHost::dp_peer_abandon() {
+	if (!peer) return;
+	TCNN_HIP_CHECK(hipDeviceSynchronize());
+	peer.reset();
+	peer_attached = false;
+	dp_sharded = false;
+	dp_state_partial = false;
+	grad_scale = grad_scale_user;
+}
+
+}  // namespace tcnn_amd

@@ -913,6 +913,10 @@ void TrainerHost::training_step(hipStream_t st, uint32_t B, const float* input, 
 		training_step_dp(st, B, input, target);
 		return;
 	}
+	if (peer_attached && run_optimizer) {
+		training_step_peer(st, B, input, target);
+		return;
+	}
 	if (overlapped_ok()) {
 		if (use_graph && run_optimizer && !timer.enabled && !adam.adabound && training_step_graph(st, B, input, target)) return;
 		training_step_overlapped(st, B, input, target, run_optimizer);
@@ -936,8 +940,10 @@ void TrainerHost::training_step(hipStream_t st, uint32_t B, const float* input, 
 // backward's chunk slabs on the fly, or (run_optimizer = false: the multi-GPU path, whose
 // all-reduce sits between the gradients and Adam) the slab reduction into the fp32 gradient.
 // Summation orders are the same either way (bit-identical parameters).
-void TrainerHost::training_step_overlapped(hipStream_t st, uint32_t B, const float* input, const float* target, bool run_optimizer) {
+void TrainerHost::training_step_overlapped(hipStream_t st, uint32_t B, const float* input, const float* target, bool run_optimizer,
+                                           float* grad_out) {
 	NetworkHost& m = *model;
+	float* const gsum = (grad_out && !run_optimizer) ? grad_out : g32.as<float>();
 	mark(st, 0);
 	const void* enc_soa = nullptr;
 	if (m.sw.split_encode) {  // A/B experiment: the encoding as its own pass, read by the fused kernel
@@ -955,7 +961,7 @@ void TrainerHost::training_step_overlapped(hipStream_t st, uint32_t B, const flo
 	ep.apply_adam = run_optimizer ? 1 : 0;
 	ep.adam_mlp = run_optimizer ? adam_args_table(st, adam_step) : adam_args();
 	ep.adam_mlp.n = (uint32_t)n_mlp;
-	ep.buf = AdamBuffers{w32.as<float>(), w16.as<_Float16>(), g32.as<float>(), g16.as<_Float16>(), m1.as<float>(), m2.as<float>(),
+	ep.buf = AdamBuffers{w32.as<float>(), w16.as<_Float16>(), gsum, g16.as<_Float16>(), m1.as<float>(), m2.as<float>(),
 	                     steps.as<uint32_t>()};
 	ep.n_mlp_groups = MLP_TAIL_GROUPS;
 	ep.n_mlp = (uint32_t)n_mlp;
@@ -982,9 +988,9 @@ void TrainerHost::training_step_overlapped(hipStream_t st, uint32_t B, const flo
 		if (!g.slices.empty())
 			launch_adam(st, ag, w32.as<float>(), w16.p, g32.as<float>(), g16.p, m1.as<float>(), m2.as<float>(), steps.as<uint32_t>());
 	} else {
-		g.backward_acc(st, ws.gbw, B, ws.dLdenc.p, 0, 0, g32.as<float>() + n_mlp);
+		g.backward_acc(st, ws.gbw, B, ws.dLdenc.p, 0, 0, gsum + n_mlp);
 		mark(st, 2);
-		g.reduce_items(st, ws.gbw, g32.as<float>() + n_mlp);
+		g.reduce_items(st, ws.gbw, gsum + n_mlp);
 	}
 	mark(st, 3);
 	last_B = B;

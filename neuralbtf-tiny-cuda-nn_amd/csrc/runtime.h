@@ -327,6 +327,7 @@ void* workspace_allocate(hipStream_t st, size_t n_bytes);
 void workspace_free(hipStream_t st, void* p);
 void workspace_arena_free(hipStream_t st);
 void workspace_arena_free_all();
+uint64_t dp_peer_blob_bytes();  // bytes of one rank's peer-exchange blob (dp_peer.hip)
 void workspace_arena_info(hipStream_t st, uint64_t* mapped_bytes, int* vmm);
 
 struct TrainerHost {
@@ -356,7 +357,9 @@ struct TrainerHost {
 	uint32_t last_B = 0;
 	// two-launch single-GPU step: reductions + Adam fused into the grid backward's epilogue
 	bool overlapped_ok() const { return model->fused_ok(); }
-	void training_step_overlapped(hipStream_t st, uint32_t B, const float* input, const float* target, bool run_optimizer);
+	// grad_out (run_optimizer = false only): where the fp32 gradient sums go (default g32)
+	void training_step_overlapped(hipStream_t st, uint32_t B, const float* input, const float* target, bool run_optimizer,
+	                              float* grad_out = nullptr);
 	AdamArgs adam_args() const;
 
 	TrainerHost(uint32_t n_in, uint32_t n_out, const json& cfg, uint32_t seed);
@@ -384,6 +387,21 @@ struct TrainerHost {
 	void set_dp(DpComm* c, bool sharded);
 	void training_step_dp(hipStream_t st, uint32_t B, const float* input, const float* target);
 	void dp_gather_state(hipStream_t st);
+	// data-parallel exchange over peer-mapped device memory, no collective library (dp_peer.hip):
+	// export IPC handles of this rank's buffers, attach every rank's, then each training_step exchanges
+	// through the peers' memory (sharded Adam, fp16 parameter gather)
+	struct PeerDp;
+	std::shared_ptr<PeerDp> peer;
+	bool peer_attached = false;
+	void dp_peer_export(int nranks, int rank, void* blob);
+	void dp_peer_attach(const void* blobs);
+	void dp_peer_detach();
+	void dp_peer_abandon();  // local, no barrier: only before any exchange step (a failed attach on some rank)
+	void dp_peer_gather_state(hipStream_t st);
+	void training_step_peer(hipStream_t st, uint32_t B, const float* input, const float* target);
+	void peer_signal(hipStream_t st, int c, bool bump, int slot);
+	void peer_wait(hipStream_t st, int c, int slot);
+	void peer_gather(hipStream_t st, int what);
 	// Adam on parameters [begin, end) only (data-parallel sharded optimizer: each rank updates its
 	// shard of the reduce-scattered gradient, then the fp16 parameters are all-gathered)
 	void optimizer_step_range(hipStream_t st, uint64_t begin, uint64_t end);

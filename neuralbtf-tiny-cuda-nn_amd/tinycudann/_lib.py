@@ -93,6 +93,11 @@ _SIGS = {
     "tcnn_dp_comm_destroy": (None, [c_void_p]),
     "tcnn_trainer_set_dp": (c_int, [c_void_p, c_void_p, c_int]),
     "tcnn_trainer_dp_gather_state": (c_int, [c_void_p, c_void_p]),
+    "tcnn_dp_peer_blob_bytes": (c_uint64, []),
+    "tcnn_trainer_dp_peer_export": (c_int, [c_void_p, c_int, c_int, c_void_p]),
+    "tcnn_trainer_dp_peer_attach": (c_int, [c_void_p, c_void_p]),
+    "tcnn_trainer_dp_peer_detach": (c_int, [c_void_p]),
+    "tcnn_trainer_dp_peer_abandon": (c_int, [c_void_p]),
     "tcnn_trainer_inference_engine": (c_char_p, [c_void_p]),
     "tcnn_module_engine": (c_char_p, [c_void_p]),
     "tcnn_module_inference_engine": (c_char_p, [c_void_p]),

@@ -20,6 +20,9 @@ to fp16 (the reference's gradient buffer is __half, trainer.h:327), the fp16 sum
 collective, and Adam reads it with scale 1. The default fp32 exchange keeps the single-GPU
 numerics (one fp16 rounding of the reduced sum).
 
+exchange="peer": the exchange through the ranks' peer-mapped memory (PeerExchange, csrc/dp_peer.hip):
+sharded, no collective library in the step, one C-ABI call per step.
+
 exchange="engine": the same exchange runs inside the engine instead (EngineComm, tcnn_trainer_set_dp):
 one RCCL communicator created from a unique id broadcast over torch.distributed, the collectives
 issued by the training step itself on its stream (network part overlapped with the grid backward),
@@ -92,14 +95,54 @@ class EngineComm:
             pass
 
 
+class PeerExchange:
+    """The engine's exchange over peer-mapped device memory (tcnn_trainer_dp_peer_*, csrc/dp_peer.hip):
+    every rank exports IPC handles of its buffers, the blobs are all-gathered over torch.distributed
+    (any backend, once), every rank attaches them. From then on the trainer's training_step exchanges
+    through the peers' memory by itself: sharded Adam on the sum of the ranks' gradients read over
+    xGMI, then a gather of the other shards' fp16 parameters -- no collective launch per step."""
+
+    def __init__(self, trainer, group=None):
+        from tinycudann import _lib as L
+        self._L = L
+        self.trainer = trainer
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        n = int(L.lib().tcnn_dp_peer_blob_bytes())
+        blob = (ctypes.c_uint8 * n)()
+        ok = L.lib().tcnn_trainer_dp_peer_export(trainer.h, self.world, self.rank, ctypes.byref(blob)) == 0
+        err = "" if ok else L.lib().tcnn_last_error().decode()
+        blobs = [None] * self.world
+        dist.all_gather_object(blobs, bytes(blob) if ok else None, group=group)
+        if ok and all(b is not None for b in blobs):
+            allb = (ctypes.c_uint8 * (n * self.world)).from_buffer_copy(b"".join(blobs))
+            ok = L.lib().tcnn_trainer_dp_peer_attach(trainer.h, ctypes.byref(allb)) == 0
+            if not ok:
+                err = L.lib().tcnn_last_error().decode()
+        else:
+            ok = False
+        # collective verdict: either every rank attached, or none keeps its attachment
+        oks = [None] * self.world
+        dist.all_gather_object(oks, (ok, err), group=group)
+        if not all(o[0] for o in oks):
+            L.lib().tcnn_trainer_dp_peer_abandon(trainer.h)
+            raise RuntimeError("peer exchange unavailable: " + "; ".join(f"rank {r}: {o[1]}" for r, o in enumerate(oks) if not o[0]))
+        trainer._dp_state_partial = False
+
+    def detach(self):
+        """collective: completes the sharded optimizer state, then closes the peer mappings"""
+        self._L.check(self._L.lib().tcnn_trainer_dp_peer_detach(self.trainer.h))
+
+
 class DataParallelTrainer:
     """Wraps tinycudann.Trainer: training_step = local fwd/bwd, all-reduce (overlapped), Adam."""
 
-    def __init__(self, trainer, group=None, overlap=True, allreduce_dtype="fp32", shard_optimizer=False, exchange="torch"):
+    def __init__(self, trainer, group=None, overlap=True, allreduce_dtype="fp32", shard_optimizer=False, exchange="torch",
+                 peer_fallback=False):
         assert allreduce_dtype in ("fp32", "fp16")
-        assert exchange in ("torch", "engine")
+        assert exchange in ("torch", "engine", "peer")
         assert not (shard_optimizer and allreduce_dtype == "fp16"), "the sharded optimizer exchanges fp32 gradient sums"
-        assert not (exchange == "engine" and allreduce_dtype == "fp16"), "the engine exchange sums fp32 gradients"
+        assert not (exchange in ("engine", "peer") and allreduce_dtype == "fp16"), "the engine exchanges sum fp32 gradients"
         self.trainer = trainer
         self.group = group
         self.overlap = overlap
@@ -108,9 +151,22 @@ class DataParallelTrainer:
         self.exchange = exchange
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.comm = None
+        if self.world > 1 and exchange == "peer":
+            self.shard_optimizer = True  # the peer exchange is the sharded schedule
+            try:
+                self.comm = PeerExchange(trainer, group)
+            except RuntimeError as e:
+                if not peer_fallback:
+                    raise
+                # every rank raised together (collective verdict): take the engine's RCCL exchange instead
+                import warnings
+                warnings.warn(f"{e}; falling back to the engine's RCCL exchange (sharded)")
+                self.exchange = exchange = "engine"
         if self.world > 1 and exchange == "engine":
             self.comm = EngineComm(group)
-            trainer.set_dp(self.comm, sharded=shard_optimizer)
+            trainer.set_dp(self.comm, sharded=self.shard_optimizer)
+        elif self.world > 1 and exchange == "peer":
+            pass  # attached above; the engine scales the gradient by 1/N itself
         elif self.world > 1 and shard_optimizer:
             self.rank = dist.get_rank(group)
             n = trainer.n_params
@@ -173,7 +229,7 @@ class DataParallelTrainer:
         serialize(optimizer=True) (which refuses to run until then)."""
         if self.world == 1 or not self.shard_optimizer:
             return
-        if self.exchange == "engine":
+        if self.exchange in ("engine", "peer"):
             self.trainer.dp_gather_state()
             return
         m1, m2, steps = self.trainer.optimizer_state()
@@ -184,7 +240,7 @@ class DataParallelTrainer:
     gather_master = gather_state  # the round-2 name (it gathered only the masters)
 
     def training_step(self, input, target):
-        if self.world == 1 or self.exchange == "engine":
+        if self.world == 1 or self.exchange in ("engine", "peer"):
             self.trainer.training_step(input, target, run_optimizer=True)
             return
         if self.shard_optimizer:

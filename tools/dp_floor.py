@@ -5,7 +5,8 @@ collectives run, over one rank). Reports per step: GPU time (events around K ste
 time (wall clock of issuing K steps, no synchronisation inside) -- a step is host-bound when the
 second exceeds the first.
 
-Schedules: plain (no exchange); engine (tcnn_trainer_set_dp, RCCL issued by the step; replicated and
+Schedules: plain (no exchange); peer (r04: the exchange through peer-mapped memory, csrc/dp_peer.hip,
+on one rank); engine (tcnn_trainer_set_dp, RCCL issued by the step; replicated and
 sharded, eager and hipGraph); torch (tinycudann.parallel.DataParallelTrainer's Python schedule over
 torch.distributed/RCCL, replicated, overlapped; run with the wrapper's world size forced to 2 on a
 one-rank group so its all-reduce path is taken -- the sums then run over one rank).
@@ -82,6 +83,13 @@ def main():
             row(f"engine {'sharded' if sharded else 'replicated'}{' graph' if graph else ''}", measure(lambda: t.training_step(pos, tgt)))
             t.set_dp(None)
             del t
+    # the peer-memory exchange (csrc/dp_peer.hip) on one rank: signal, wait, shard Adam over the
+    # ranks' gradients, signal, wait, gather -- its whole per-step machinery, minus the link transfers
+    t = Trainer(2, 3, cfg, seed=1337)
+    px = P.PeerExchange(t)
+    row("peer (xGMI exchange, sharded)", measure(lambda: t.training_step(pos, tgt)))
+    px.detach()
+    del t, px
     real_ws = P.dist.get_world_size
     P.dist.get_world_size = lambda group=None: 2  # take the wrapper's all-reduce path on the one-rank group
     try:
