@@ -43,6 +43,7 @@ namespace tcnn_amd {
 namespace {
 
 constexpr uint32_t PEER_MAGIC = 0x50454552u;  // "PEER"
+constexpr int PEER_MAX_RANKS = 64;  // one wave polls the ranks' counters
 constexpr int PEER_NBUF = 4;                  // exported: gradient sums, fp16 shard mirror, state staging, counters
 enum PeerBuf { PB_G32 = 0, PB_W16, PB_STATE, PB_FLAGS };
 enum PeerSlot { SLOT_GRAD = 0, SLOT_WEIGHTS = 1, SLOT_GATHER = 2, SLOT_DETACH = 3 };
@@ -58,32 +59,34 @@ __device__ __forceinline__ uint32_t load_sys(const uint32_t* p) {
 	return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// counter ctr[c] (+1 when bump), then flags[slot] = that value (system-scope store; every earlier
-// write of this stream went to uncached memory and finished with its kernel)
-__global__ void k_peer_signal(uint32_t* __restrict__ ctr, int c, int bump, uint32_t* __restrict__ flags, int slot) {
-	if (threadIdx.x != 0) return;
-	uint32_t v = ctr[c];
-	if (bump) {
-		v += 1u;
-		ctr[c] = v;
+// one workgroup: when my_flags != nullptr first signal -- counter ctr[c] (+1 when bump), then my_flags[slot]
+// = that value (system-scope store; every earlier write of this stream went to uncached memory and
+// finished with its kernel) -- then wait until every rank's flags[slot] reached ctr[c]; on timeout
+// raise *err (host-mapped)
+struct PeerFlags {  // the ranks' counter arrays, by value (no dependent pointer load before the polls)
+	uint32_t* f[PEER_MAX_RANKS];
+};
+__global__ void k_peer_wait(const PeerFlags fl, int nranks, int slot, uint32_t* __restrict__ ctr, int c, long long timeout_ticks,
+                            int* __restrict__ err, uint32_t* __restrict__ my_flags, int bump) {
+	if (threadIdx.x >= 64) return;
+	uint32_t target = ctr[c];
+	if (my_flags && threadIdx.x == 0) {
+		if (bump) ctr[c] = target + 1u;
+		__hip_atomic_store(my_flags + slot, target + (bump ? 1u : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 	}
-	__hip_atomic_store(flags + slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// one workgroup: wait until every rank's flags[slot] reached ctr[c]; on timeout raise *err (host-mapped)
-__global__ void k_peer_wait(uint32_t* const* __restrict__ flag_ptrs, int nranks, int slot, const uint32_t* __restrict__ ctr, int c,
-                            long long timeout_ticks, int* __restrict__ err) {
-	if (threadIdx.x != 0) return;
-	const uint32_t target = ctr[c];
+	if (my_flags && bump) target += 1u;
+	// lane p polls rank p: the ranks' counters are read concurrently (one link round trip per poll, not N)
+	const int p = threadIdx.x;
 	const long long t0 = wall_clock64();
-	for (int p = 0; p < nranks; ++p) {
-		while ((int32_t)(load_sys(flag_ptrs[p] + slot) - target) < 0) {
-			if (wall_clock64() - t0 > timeout_ticks) {
-				__hip_atomic_store(err, 1 + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-				return;
-			}
-			__builtin_amdgcn_s_sleep(2);
+	for (;;) {
+		const bool ok = p >= nranks || (int32_t)(load_sys(fl.f[p] + slot) - target) >= 0;
+		const uint64_t pending = __builtin_amdgcn_ballot_w64(!ok);
+		if (pending == 0) return;
+		if (wall_clock64() - t0 > timeout_ticks) {
+			if (p == (int)__builtin_ctzll(pending)) __hip_atomic_store(err, 1 + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+			return;
 		}
+		__builtin_amdgcn_s_sleep(1);
 	}
 }
 
@@ -157,6 +160,7 @@ struct TrainerHost::PeerDp {
 	int* err_host = nullptr;
 	int* err_dev = nullptr;
 	long long timeout_ticks = 0;
+	PeerFlags flags_arg{};  // the ranks' counter arrays (k_peer_wait's argument)
 	PeerDp() = default;
 	~PeerDp() {
 		for (void* p : opened) (void)hipIpcCloseMemHandle(p);
@@ -188,6 +192,7 @@ static void grow_keep(DevBuf& b, size_t bytes, size_t valid) {
 void TrainerHost::dp_peer_export(int nranks, int rank, void* blob_out) {
 	TCNN_CHECK(!dp, "peer exchange: detach the RCCL communicator first (set_dp(NULL))");
 	TCNN_CHECK(nranks >= 1 && rank >= 0 && rank < nranks, "peer exchange: rank outside [0, nranks)");
+	TCNN_CHECK(nranks <= PEER_MAX_RANKS, "peer exchange: at most 64 ranks (the ranks of one node)");
 	TCNN_CHECK(overlapped_ok(), "peer exchange: needs the fused grid engine (the step's gradient sums in one buffer)");
 	if (peer) dp_peer_detach();
 	TCNN_HIP_CHECK(hipDeviceSynchronize());
@@ -254,6 +259,7 @@ void TrainerHost::dp_peer_attach(const void* blobs) {
 			host[(size_t)k * N + p] = q;
 		}
 	}
+	for (int p = 0; p < N; ++p) pd.flags_arg.f[p] = (uint32_t*)host[(size_t)PB_FLAGS * N + p];
 	pd.ptrs.reserve(host.size() * sizeof(void*));
 	TCNN_HIP_CHECK(hipMemcpy(pd.ptrs.p, host.data(), host.size() * sizeof(void*), hipMemcpyHostToDevice));
 	pd.attached = true;
@@ -265,16 +271,12 @@ void TrainerHost::dp_peer_attach(const void* blobs) {
 	if (graph) set_graph(use_graph);
 }
 
-void TrainerHost::peer_signal(hipStream_t st, int c, bool bump, int slot) {
-	hipLaunchKernelGGL(k_peer_signal, dim3(1), dim3(64), 0, st, peer->ctr.as<uint32_t>(), c, bump ? 1 : 0, (uint32_t*)peer->x[PB_FLAGS],
-	                   slot);
-	TCNN_HIP_CHECK(hipGetLastError());
-}
-
-void TrainerHost::peer_wait(hipStream_t st, int c, int slot) {
+// wait for every rank's flags[slot] to reach counter c; with signal_bump >= 0 this rank signals first
+// (bumping the counter when 1) in the same one-workgroup launch
+void TrainerHost::peer_wait(hipStream_t st, int c, int slot, int signal_bump) {
 	PeerDp& pd = *peer;
-	hipLaunchKernelGGL(k_peer_wait, dim3(1), dim3(64), 0, st, pd.table<uint32_t>(PB_FLAGS), pd.nranks, slot, pd.ctr.as<uint32_t>(), c,
-	                   pd.timeout_ticks, pd.err_dev);
+	hipLaunchKernelGGL(k_peer_wait, dim3(1), dim3(64), 0, st, pd.flags_arg, pd.nranks, slot, pd.ctr.as<uint32_t>(), c, pd.timeout_ticks,
+	                   pd.err_dev, signal_bump >= 0 ? (uint32_t*)pd.x[PB_FLAGS] : nullptr, signal_bump > 0 ? 1 : 0);
 	TCNN_HIP_CHECK(hipGetLastError());
 }
 
@@ -283,8 +285,7 @@ void TrainerHost::training_step_peer(hipStream_t st, uint32_t B, const float* in
 	pd.check();
 	// this rank's gradient sums, straight into its uncached exchange buffer
 	training_step_overlapped(st, B, input, target, false, (float*)pd.x[PB_G32]);
-	peer_signal(st, CTR_STEP, true, SLOT_GRAD);
-	peer_wait(st, CTR_STEP, SLOT_GRAD);
+	peer_wait(st, CTR_STEP, SLOT_GRAD, 1);  // signal "gradients ready" and wait for every rank's
 	const uint64_t lo = std::min<uint64_t>(n_params, (uint64_t)pd.rank * pd.per), hi = std::min<uint64_t>(n_params, lo + pd.per);
 	++adam_step;
 	AdamArgs a = adam_args_table(st, adam_step);
@@ -296,8 +297,7 @@ void TrainerHost::training_step_peer(hipStream_t st, uint32_t B, const float* in
 		hipLaunchKernelGGL(k_peer_adam, dim3(div_round_up(hi - lo, 256)), dim3(256), 0, st, a, s, pd.table<const float>(PB_G32), pd.nranks,
 		                   (_Float16*)pd.x[PB_W16]);
 	TCNN_HIP_CHECK(hipGetLastError());
-	peer_signal(st, CTR_STEP, false, SLOT_WEIGHTS);
-	peer_wait(st, CTR_STEP, SLOT_WEIGHTS);
+	peer_wait(st, CTR_STEP, SLOT_WEIGHTS, 0);  // signal "weights ready" and wait
 	peer_gather(st, 1);
 	ws.wimage_valid = false;
 	dp_state_partial = true;
@@ -341,8 +341,7 @@ void TrainerHost::dp_peer_gather_state(hipStream_t st) {
 		hipLaunchKernelGGL(k_peer_stage, dim3(div_round_up(hi - lo, 256)), dim3(256), 0, st, w32.as<float>(), m1.as<float>(), m2.as<float>(),
 		                   steps.as<uint32_t>(), (uint32_t*)pd.x[PB_STATE], lo, hi - lo, pd.per * (uint64_t)pd.nranks);
 	TCNN_HIP_CHECK(hipGetLastError());
-	peer_signal(st, CTR_SYNC, true, SLOT_GATHER);
-	peer_wait(st, CTR_SYNC, SLOT_GATHER);
+	peer_wait(st, CTR_SYNC, SLOT_GATHER, 1);
 	peer_gather(st, 4);
 	TCNN_HIP_CHECK(hipStreamSynchronize(st));
 	pd.check();
@@ -355,8 +354,7 @@ void TrainerHost::dp_peer_detach() {
 	if (!peer) return;
 	if (peer->attached) {
 		if (dp_state_partial) dp_peer_gather_state(nullptr);
-		peer_signal(nullptr, CTR_SYNC, true, SLOT_DETACH);
-		peer_wait(nullptr, CTR_SYNC, SLOT_DETACH);
+		peer_wait(nullptr, CTR_SYNC, SLOT_DETACH, 1);
 		TCNN_HIP_CHECK(hipDeviceSynchronize());
 	}
 	peer.reset();

@@ -399,8 +399,7 @@ struct TrainerHost {
 	void dp_peer_abandon();  // local, no barrier: only before any exchange step (a failed attach on some rank)
 	void dp_peer_gather_state(hipStream_t st);
 	void training_step_peer(hipStream_t st, uint32_t B, const float* input, const float* target);
-	void peer_signal(hipStream_t st, int c, bool bump, int slot);
-	void peer_wait(hipStream_t st, int c, int slot);
+	void peer_wait(hipStream_t st, int c, int slot, int signal_bump = -1);
 	void peer_gather(hipStream_t st, int what);
 	// Adam on parameters [begin, end) only (data-parallel sharded optimizer: each rank updates its
 	// shard of the reduce-scattered gradient, then the fp16 parameters are all-gathered)

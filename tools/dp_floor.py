@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--batch-log2", type=int, default=15)
+    ap.add_argument("--schedules", default="plain,engine,peer,torch", help="comma-separated subset")
     args = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -69,13 +70,14 @@ def main():
         rows.append(r)
         print(json.dumps(r), flush=True)
 
-    for graph in (False, True):
+    want = set(args.schedules.split(","))
+    for graph in ((False, True) if "plain" in want else ()):
         t = Trainer(2, 3, cfg, seed=1337)
         t.set_graph(graph)
         row(f"plain{' graph' if graph else ''}", measure(lambda: t.training_step(pos, tgt)))
         del t
-    comm = P.EngineComm()
-    for sharded in (False, True):
+    comm = P.EngineComm() if "engine" in want else None
+    for sharded in ((False, True) if "engine" in want else ()):
         for graph in (False, True):
             t = Trainer(2, 3, cfg, seed=1337)
             t.set_dp(comm, sharded=sharded)
@@ -85,18 +87,20 @@ def main():
             del t
     # the peer-memory exchange (csrc/dp_peer.hip) on one rank: signal, wait, shard Adam over the
     # ranks' gradients, signal, wait, gather -- its whole per-step machinery, minus the link transfers
-    t = Trainer(2, 3, cfg, seed=1337)
-    px = P.PeerExchange(t)
-    row("peer (xGMI exchange, sharded)", measure(lambda: t.training_step(pos, tgt)))
-    px.detach()
-    del t, px
+    if "peer" in want:
+        t = Trainer(2, 3, cfg, seed=1337)
+        px = P.PeerExchange(t)
+        row("peer (xGMI exchange, sharded)", measure(lambda: t.training_step(pos, tgt)))
+        px.detach()
+        del t, px
     real_ws = P.dist.get_world_size
     P.dist.get_world_size = lambda group=None: 2  # take the wrapper's all-reduce path on the one-rank group
     try:
-        t = Trainer(2, 3, cfg, seed=1337)
-        dp = P.DataParallelTrainer(t, overlap=True)
-        row("torch replicated overlapped (Python wrapper)", measure(lambda: dp.training_step(pos, tgt)))
-        del dp, t
+        if "torch" in want:
+            t = Trainer(2, 3, cfg, seed=1337)
+            dp = P.DataParallelTrainer(t, overlap=True)
+            row("torch replicated overlapped (Python wrapper)", measure(lambda: dp.training_step(pos, tgt)))
+            del dp, t
     finally:
         P.dist.get_world_size = real_ws
     dist.destroy_process_group()
