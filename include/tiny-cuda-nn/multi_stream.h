@@ -24,9 +24,9 @@ struct StreamAndEvent {  // multi_stream.h:41-94
 	~StreamAndEvent() {
 		if (m_stream) {
 			tcnn_free_workspace_arena(m_stream);
-			hipStreamDestroy(m_stream);
+			(void)hipStreamDestroy(m_stream);
 		}
-		if (m_event) hipEventDestroy(m_event);
+		if (m_event) (void)hipEventDestroy(m_event);
 	}
 	StreamAndEvent(const StreamAndEvent&) = delete;
 	StreamAndEvent& operator=(const StreamAndEvent&) = delete;
@@ -48,7 +48,7 @@ private:
 
 struct MultiStream {  // multi_stream.h:96-148
 	explicit MultiStream(size_t n) : m_streams(n) { HIP_CHECK_THROW(hipEventCreateWithFlags(&m_event, hipEventDisableTiming)); }
-	~MultiStream() { hipEventDestroy(m_event); }
+	~MultiStream() { (void)hipEventDestroy(m_event); }
 	MultiStream(const MultiStream&) = delete;
 	MultiStream& operator=(const MultiStream&) = delete;
 	void wait_for(hipStream_t s) {

@@ -14,6 +14,8 @@
 #include <memory>
 #include <vector>
 
+#include "encoding.h"
+#include "network.h"
 #include "network_with_input_encoding.h"
 #include "optimizer.h"
 
@@ -22,20 +24,25 @@ namespace tcnn {
 template <typename T, typename PARAMS_T, typename COMPUTE_T = T>
 class Trainer {
 public:
-	using Model = NetworkWithInputEncoding<PARAMS_T>;
+	// trainer.h:50: any DifferentiableObject -- NetworkWithInputEncoding, Network (create_network; inputs
+	// of type T, fp16 ones widened for the engine), not an Encoding alone (refused below)
+	using Model = DifferentiableObject<T, PARAMS_T, COMPUTE_T>;
 
 	// trainer.h:50-57: the trainer owns the parameters (seeded pcg32{seed_seq{seed}[0]})
 	Trainer(std::shared_ptr<Model> model, std::shared_ptr<Optimizer<PARAMS_T>> optimizer, std::shared_ptr<Loss<COMPUTE_T>> loss,
 	        uint32_t seed = 1337, float perturbation_sigma = 0)
 	    : m_model{std::move(model)}, m_optimizer{std::move(optimizer)}, m_loss{std::move(loss)}, m_seed{seed} {
-		static_assert(std::is_same<T, float>::value, "Trainer: inputs are fp32 (Trainer<float, __half, __half>)");
+		static_assert(std::is_same<T, float>::value || std::is_same<T, __half>::value, "Trainer: inputs are fp32 or fp16");
 		if (perturbation_sigma != 0) throw std::runtime_error{"Trainer: output perturbation is not supported by the MI355X engine"};
+		if (m_model->engine_network().is_null())
+			throw std::runtime_error{"Trainer: " + m_model->name() + " has no network; this engine trains a network behind an encoding "
+			                         "(NetworkWithInputEncoding, or Network for the network alone)"};
 		// (keyed assignment: brace-initialising with json values would wrap them in arrays)
 		json cfg = json::object();
 		cfg["loss"] = m_loss->config();
 		cfg["optimizer"] = m_optimizer->config();
-		cfg["encoding"] = m_model->encoding_config();
-		cfg["network"] = m_model->network_config();
+		cfg["encoding"] = m_model->engine_encoding();
+		cfg["network"] = m_model->engine_network();
 		m_h = detail::check_handle(tcnn_trainer_create(m_model->input_width(), m_model->output_width(), cfg.dump().c_str(), seed));
 		m_model->attach(m_h);
 		m_optimizer->attach(m_h);
@@ -74,6 +81,7 @@ public:
 		GPUMatrix<COMPUTE_T> output, dL_doutput;
 		std::shared_ptr<LossSlots> slots;  // a fused step's loss slot (returned on destruction)
 		float* loss_slot = nullptr;
+		GPUMemory<float> input_f32;  // Trainer<__half, ...>: the widened input the engine read (for backward)
 		ForwardContext() = default;
 		ForwardContext(const ForwardContext&) = delete;
 		ForwardContext& operator=(const ForwardContext&) = delete;
@@ -106,7 +114,8 @@ public:
 		auto ctx = std::make_unique<ForwardContext>();
 		ctx->owner = this;
 		ctx->step = ++m_n_steps;
-		ctx->h = tcnn_trainer_forward(m_h, stream, n, input.data(), external_dL_dy ? nullptr : target.data(),
+		const float* in = detail::engine_input(stream, input, ctx->input_f32);
+		ctx->h = tcnn_trainer_forward(m_h, stream, n, in, external_dL_dy ? nullptr : target.data(),
 		                              data_pdf ? data_pdf->data() : nullptr, external_dL_dy ? external_dL_dy->data() : nullptr,
 		                              prepare_input_gradients ? 1 : 0);
 		if (!ctx->h) throw std::runtime_error{tcnn_last_error()};
@@ -128,8 +137,20 @@ public:
 		(void)use_inference_params;
 		if (!ctx.h || ctx.owner != this) throw std::runtime_error{"Trainer::backward: the context was not made by this trainer's forward()"};
 		if (dL_dinput) CHECK_THROW(dL_dinput->m() == m_model->input_width() && dL_dinput->n() == input.n() && dL_dinput->layout() == CM);
-		detail::check_rc(tcnn_trainer_backward(m_h, stream, ctx.h, input.n(), input.data(), dL_dinput ? dL_dinput->data() : nullptr,
-		                                       param_gradients_mode == GradientMode::Overwrite ? 0 : param_gradients_mode == GradientMode::Accumulate ? 1 : 2));
+		const int mode = param_gradients_mode == GradientMode::Overwrite ? 0 : param_gradients_mode == GradientMode::Accumulate ? 1 : 2;
+		if constexpr (std::is_same<T, float>::value) {
+			detail::check_rc(tcnn_trainer_backward(m_h, stream, ctx.h, input.n(), input.data(), dL_dinput ? dL_dinput->data() : nullptr, mode));
+		} else {
+			// the engine's fp32 input of this context's forward; fp32 dL/dinput narrowed to T
+			CHECK_THROW(ctx.input_f32.size() >= input.n_elements());
+			GPUMemory<float> din32(dL_dinput ? dL_dinput->n_elements() : 0);
+			detail::check_rc(tcnn_trainer_backward(m_h, stream, ctx.h, input.n(), ctx.input_f32.data(), dL_dinput ? din32.data() : nullptr, mode));
+			if (dL_dinput) {
+				const uint32_t ne = (uint32_t)dL_dinput->n_elements();
+				hipLaunchKernelGGL(detail::narrow_from_float<T>, dim3((ne + 255) / 256), dim3(256), 0, stream, ne, din32.data(), dL_dinput->data());
+				HIP_CHECK_THROW(hipStreamSynchronize(stream));  // din32 is freed on return
+			}
+		}
 	}
 	void backward(const ForwardContext& ctx, const GPUMatrixDynamic<T>& input, GPUMatrixDynamic<T>* dL_dinput = nullptr,
 	              bool use_inference_params = false, GradientMode param_gradients_mode = GradientMode::Overwrite) {
@@ -163,7 +184,8 @@ public:
 		CHECK_THROW(target.m() == m_model->output_width());
 		CHECK_THROW(input.n() == target.n());
 		CHECK_THROW(target.layout() == CM && target.is_contiguous());
-		detail::check_rc(tcnn_trainer_training_step(m_h, stream, input.n(), input.data(), target.data(), run_optimizer ? 1 : 0));
+		const float* in = detail::engine_input(stream, input, m_input_scratch);
+		detail::check_rc(tcnn_trainer_training_step(m_h, stream, input.n(), in, target.data(), run_optimizer ? 1 : 0));
 		auto ctx = std::make_unique<ForwardContext>();
 		ctx->owner = this;
 		ctx->step = ++m_n_steps;
@@ -289,6 +311,7 @@ private:
 	uint32_t m_seed;
 	tcnn_trainer* m_h = nullptr;
 	uint64_t m_n_steps = 0;
+	GPUMemory<float> m_input_scratch;  // Trainer<__half, ...>: the widened batch of training_step
 	std::shared_ptr<LossSlots> m_loss_slots = std::make_shared<LossSlots>();
 };
 

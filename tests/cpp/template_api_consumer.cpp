@@ -33,6 +33,12 @@ __global__ void field(uint32_t n, const float* __restrict__ xy, float* __restric
 	rgb[3 * i + 2] = 0.5f + 0.3f * cosf(31.0f * x) * sinf(17.0f * y);
 }
 
+__global__ void field16(uint32_t n, const __half* __restrict__ x, float* __restrict__ y) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	for (int k = 0; k < 3; ++k) y[3 * i + k] = 0.5f + 0.4f * sinf(3.0f * (float)x[16 * i + k] + 2.0f * (float)x[16 * i + k + 3]);
+}
+
 int main(int argc, char** argv) {
 	if (argc < 2) {
 		std::printf("usage: %s <config_hash.json>\n", argv[0]);
@@ -327,6 +333,61 @@ int main(int argc, char** argv) {
 				threw = true;
 			}
 			EXPECT(threw);
+		}
+		// Trainer over any DifferentiableObject (trainer.h:50): a Network alone from create_network
+		// (network.h:141-158), fp16 inputs (Trainer<__half, __half, __half>), and an Encoding alone refused
+		{
+			const uint32_t n = 1 << 14;
+			std::shared_ptr<Network<network_precision_t>> net{create_network<network_precision_t>(
+			    {{"otype", "FullyFusedMLP"}, {"activation", "ReLU"}, {"output_activation", "None"}, {"n_neurons", 64},
+			     {"n_hidden_layers", 2}, {"n_input_dims", 16}, {"n_output_dims", 3}})};
+			EXPECT(net->input_width() == 16 && net->output_width() == 3 && net->width(1) == 64 && net->num_forward_activations() == 2);
+			std::shared_ptr<Loss<network_precision_t>> l{create_loss<network_precision_t>({{"otype", "L2"}})};
+			std::shared_ptr<Optimizer<network_precision_t>> o{
+			    create_optimizer<network_precision_t>({{"otype", "Adam"}, {"learning_rate", 1e-2f}})};
+			auto tr = std::make_shared<Trainer<network_precision_t, network_precision_t, network_precision_t>>(net, o, l);
+			EXPECT(tr->n_params() == net->n_params() && net->n_params() == 64 * 16 + 64 * 64 + 16 * 64);
+			GPUMemory<float> x32(16 * n);
+			default_rng_t r{42};
+			generate_random_uniform<float>(stream, r, 16 * n, x32.data(), -1.0f, 1.0f);
+			GPUMatrix<network_precision_t> x(16, n);
+			hipLaunchKernelGGL(detail::narrow_from_float<network_precision_t>, dim3(16 * n / 256), dim3(256), 0, stream, 16 * n,
+			                   x32.data(), x.data());
+			GPUMatrix<float> y(3, n);
+			hipLaunchKernelGGL(field16, dim3(n / 256), dim3(256), 0, stream, n, x.data(), y.data());
+			float l0 = 0, l1 = 0;
+			for (int i = 0; i < 300; ++i) {
+				auto ctx = tr->training_step(stream, x, y);
+				if (i == 0) l0 = tr->loss(stream, *ctx);
+				if (i == 299) l1 = tr->loss(stream, *ctx);
+			}
+			std::printf("create_network fp16 inputs: L2 %.5f -> %.5f\n", l0, l1);
+			EXPECT(std::isfinite(l1) && l1 < 0.25f * l0);
+			// inference on the trainer's parameters equals forward's output
+			GPUMatrix<float> yi(3, n);
+			net->inference(stream, x, yi);
+			auto ctx = tr->forward(stream, 1.0f, x, y, nullptr, false, true);
+			HIP_CHECK_THROW(hipStreamSynchronize(stream));
+			EXPECT(std::isfinite(yi.to_cpu_vector()[0]));
+			// dL/dinput narrowed to fp16 for a fp16-input trainer
+			GPUMatrix<network_precision_t> dx(16, n);
+			tr->backward(stream, *ctx, x, &dx, false, GradientMode::Ignore);
+			HIP_CHECK_THROW(hipStreamSynchronize(stream));
+			std::vector<network_precision_t> hdx(16 * n);
+			HIP_CHECK_THROW(hipMemcpy(hdx.data(), dx.data(), hdx.size() * 2, hipMemcpyDeviceToHost));
+			bool nonzero = false;
+			for (auto v : hdx) nonzero = nonzero || (float)v != 0.0f;
+			EXPECT(nonzero);
+
+			std::shared_ptr<Encoding<network_precision_t>> enc{create_encoding<network_precision_t>(2, config["encoding"])};
+			EXPECT(enc->input_width() == 2 && enc->output_width() == 32);
+			bool refused = false;
+			try {
+				Trainer<float, network_precision_t, network_precision_t> bad(enc, o, l);
+			} catch (const std::runtime_error&) {
+				refused = true;
+			}
+			EXPECT(refused);
 		}
 		free_all_gpu_memory_arenas();
 		HIP_CHECK_THROW(hipStreamDestroy(stream));

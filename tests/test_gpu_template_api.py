@@ -28,8 +28,13 @@ def test_template_headers_declare_reference_interface():
                       "set_params_full_precision(", "void update_hyperparams(const json& params)", "void initialize_params()",
                       "std::unique_ptr<ForwardContext> forward(hipStream_t stream, const float loss_scale",
                       "void backward(hipStream_t stream, const ForwardContext& ctx"],
-        "network_with_input_encoding.h": ["class NetworkWithInputEncoding", "void inference(hipStream_t stream",
+        "network_with_input_encoding.h": ["class NetworkWithInputEncoding", "public DifferentiableObject<float, T, T>",
                                           "padded_output_width()", "size_t n_params()"],
+        "object.h": ["class DifferentiableObject", "void inference(hipStream_t stream", "virtual uint32_t input_width()",
+                     "virtual uint32_t output_width()", "virtual size_t n_params()"],
+        "network.h": ["class Network : public DifferentiableObject<T, PARAMS_T, PARAMS_T>", "create_network(const json& network)",
+                      "uint32_t width(uint32_t layer)", "num_forward_activations()"],
+        "encoding.h": ["class Encoding", "create_encoding(uint32_t n_dims_to_encode"],
         "gpu_matrix.h": ["class GPUMatrixDynamic", "class GPUMatrix : public GPUMatrixDynamic<T>", "uint32_t m() const",
                          "uint32_t n() const", "transposed()"],
         "gpu_memory.h": ["class GPUMemory", "void copy_from_host(", "void copy_to_host(", "void resize(", "size_t get_bytes()",
