@@ -168,8 +168,10 @@ struct ModuleNWIE : ModuleBase {
 		const bool use = c && c->keep && c->layout != NetworkHost::KEEP_NONE && c->in == in && c->params == params;
 		const void* dout = dL_dout;
 		const bool fused = model.fused_ok() && !dL_din;
+		model.grad_fin_done = false;
 		if (fused) {
 			model.ext_dout_scale = s;
+			if (dL_dparams) model.grad_fin = GradFinalize{dL_dparams, s, dparams_f32 ? 1 : 0};
 		} else {
 			const size_t n_out = (size_t)n * model.mlp.padded_output;
 			dout_scaled.reserve(n_out * 2);
@@ -181,11 +183,13 @@ struct ModuleNWIE : ModuleBase {
 			              use ? c->keep->p : nullptr, use ? c->layout : NetworkHost::KEEP_NONE);
 		} catch (...) {
 			model.ext_dout_scale = 1.0f;
+			model.grad_fin = {};
 			throw;
 		}
 		model.ext_dout_scale = 1.0f;
+		model.grad_fin = {};
 		if (dL_din) launch_div_f32(st, dL_din, s, (size_t)n * model.n_input_dims);
-		if (dL_dparams) launch_grad_finalize(st, grad32.as<float>(), dL_dparams, s, n_params(), dparams_f32);
+		if (dL_dparams && !model.grad_fin_done) launch_grad_finalize(st, grad32.as<float>(), dL_dparams, s, n_params(), dparams_f32);
 		return true;
 	}
 	DevBuf dout_scaled;

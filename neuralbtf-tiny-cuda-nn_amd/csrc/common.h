@@ -85,6 +85,15 @@ __device__ __forceinline__ _Float16 f16_rn(float x) {
 	return (_Float16)x;
 }
 
+// The torch binding's parameter gradient from the engine's fp32 sum g of loss-scaled gradients:
+// fp16(fp16(g) / s) -- the reference's fp16 gradient divided by the loss scale in fp16 arithmetic
+// (modules.py:128-138). One definition for k_grad_finalize and the reductions that fold it in.
+__device__ __forceinline__ void grad_finalize_store(float g, float s, void* out, size_t i, int out_f32) {
+	const _Float16 h = f16_rn((float)(_Float16)g / s);
+	if (out_f32) ((float*)out)[i] = (float)h;
+	else ((_Float16*)out)[i] = h;
+}
+
 // N fp32 values (N even) -> fp16, each rounded once from its fp32 value, as pairs: a two-element
 // conversion selects v_cvt_pk_f16_f32, which hipcc does not fold with the producing multiplies into
 // a v_fma_mix (a lone scalar conversion of a product it does fold, even under `fp contract(off)`).

@@ -128,6 +128,7 @@ void launch_fused_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, ui
                         Interp interp, uint32_t n_blocks, const void* dout16, const void* wimage, uint32_t loss_l2,
                         bool inrange_index, const void* enc16, float dout_scale) {
 	TCNN_CHECK(B % 32 == 0, "fused train: batch must be a multiple of 32");
+	TCNN_CHECK(wimage || ((uintptr_t)params16 & 15) == 0, "fused train: parameters must be 16-byte aligned");
 	FusedTrainArgs a;
 	a.enc = (const _Float16*)enc16;
 	a.loss_l2 = loss_l2;
@@ -192,6 +193,58 @@ void launch_mlp_infer(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, int 
 	TCNN_FUSED_SHAPES(X)
 #undef X
 	throw std::runtime_error("mlp inference: unsupported shape");
+}
+
+template <int W, int IN, int NH, uint32_t D, HashType H, Act A>
+static void launch_fused_fwd_t(hipStream_t st, const FusedFwdArgs& a) {
+	constexpr size_t bytes = (((size_t)FusedLayout<W, IN, NH>::oStage * 2 + 15) & ~(size_t)15) + (size_t)(IN / 2) * sizeof(LevelInfo);
+	static uint64_t done = 0;
+	set_dyn_lds((const void*)k_fused_fwd_grid<W, IN, NH, D, H, A>, (int)bytes, done);
+	uint32_t nb = div_round_up(a.B, 64u);
+	const uint32_t cap = 8 * device_cu_count();  // 54 VGPRs, 17 KB of LDS: 8 workgroups per CU
+	if (nb > cap) nb = cap;
+	hipLaunchKernelGGL((k_fused_fwd_grid<W, IN, NH, D, H, A>), dim3(nb), dim3(256), bytes, st, a);
+	TCNN_HIP_CHECK(hipGetLastError());
+}
+
+template <int W, int IN, int NH>
+static void launch_fused_fwd_shape(hipStream_t st, uint32_t D, HashType h, int act, const FusedFwdArgs& a) {
+#define DISPATCH_H(DD, AA)                                                                                   \
+	switch (h) {                                                                                          \
+		case HashType::Prime: launch_fused_fwd_t<W, IN, NH, DD, HashType::Prime, AA>(st, a); break;       \
+		case HashType::ReversedPrime: launch_fused_fwd_t<W, IN, NH, DD, HashType::ReversedPrime, AA>(st, a); break; \
+		default: launch_fused_fwd_t<W, IN, NH, DD, HashType::CoherentPrime, AA>(st, a); break;            \
+	}
+	if (D == 2) {
+		if (act == 1) { DISPATCH_H(2, Act::ReLU) } else { DISPATCH_H(2, Act::None) }
+	} else {
+		if (act == 1) { DISPATCH_H(3, Act::ReLU) } else { DISPATCH_H(3, Act::None) }
+	}
+#undef DISPATCH_H
+}
+
+void launch_fused_fwd(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, uint32_t D, HashType h, int act, uint32_t B,
+                      const void* wimage, const void* params16, const void* table16, const float* pos, const LevelInfo* levels, bool hash_grid,
+                      Interp interp, bool inrange_index, void* enc16, void* out16) {
+	TCNN_CHECK(B % 16 == 0, "fused forward: batch must be a multiple of 16");
+	if (B == 0) return;
+	FusedFwdArgs a;
+	a.B = B;
+	TCNN_CHECK(wimage || ((uintptr_t)params16 & 15) == 0, "fused forward: parameters must be 16-byte aligned");
+	a.wimage = (const _Float16*)wimage;
+	a.params = (const _Float16*)params16;
+	a.table = (const uint32_t*)table16;
+	a.pos = pos;
+	a.levels = levels;
+	a.hash_grid = hash_grid ? 1u : 0u;
+	a.interp = (uint32_t)interp;
+	a.inrange_index = inrange_index ? 1u : 0u;
+	a.enc = (_Float16*)enc16;
+	a.out = (_Float16*)out16;
+#define X(w, in, nh) if (W == w && IN == in && NH == nh) { launch_fused_fwd_shape<w, in, nh>(st, D, h, act, a); return; }
+	TCNN_FUSED_SHAPES(X)
+#undef X
+	throw std::runtime_error("fused forward: unsupported shape");
 }
 
 __global__ void k_trim_cast(uint32_t B, uint32_t in_stride, uint32_t n_out, const _Float16* __restrict__ in, float* __restrict__ out) {

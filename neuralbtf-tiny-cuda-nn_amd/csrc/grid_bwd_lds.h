@@ -350,6 +350,10 @@ __device__ __forceinline__ void grid_bwd_mlp_tail(const GridBwdEpilogue& ep, uin
 		for (uint32_t t = threadIdx.x; t < ncol; t += blockDim.x) {
 			const uint32_t i = c0 + t;
 			const float s = out[t];
+			if (ep.fin.out) {
+				grad_finalize_store(s, ep.fin.s, ep.fin.out, i, ep.fin.out_f32);
+				continue;
+			}
 			ep.buf.g32[i] = s;
 			if (!ep.apply_adam) continue;
 			const _Float16 h = adam_update(ep.adam_mlp, ep.buf, i, s);

@@ -106,6 +106,14 @@ struct AdamBuffers {
 // workgroups, on CUs the grid items leave free, each reduce one column block of the fused kernel's
 // network-gradient slabs, run Adam on those network parameters and write them into the next step's
 // fused weight image; workgroup 0 also sums the loss partials.
+// Where a reduction writes the torch binding's finalised parameter gradient (grad_finalize_store,
+// common.h) instead of fp32 sums: out (nullable; fp16, or fp32 if out_f32) at the parameter's index.
+struct GradFinalize {
+	void* out = nullptr;
+	float s = 1.0f;
+	int out_f32 = 0;
+};
+
 struct GridBwdEpilogue {
 	int enabled;
 	int apply_adam;          // 0: only the reduction (network gradients -> buf.g32, loss), for the
@@ -122,6 +130,7 @@ struct GridBwdEpilogue {
 	// at oWh, output rows of RSW at oWo
 	_Float16* wimage;
 	uint32_t W, IN, NH, RSI, RSW, oWh, oWo;
+	GradFinalize fin;        // apply_adam == 0: network gradients finalised into fin.out instead of buf.g32
 };
 
 // Fused train step (grid encoding -> MLP fwd -> RelativeL2 -> MLP bwd -> dW partials, dL/denc).
@@ -144,6 +153,11 @@ void launch_pack_weights(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, c
 
 // Forward-only MLP (inference): in fp16 SoA [IN][B] or AoS [B][IN] -> out fp16 [B][16].
 bool mlp_infer_supported(uint32_t W, uint32_t IN, uint32_t NH, uint32_t OUTP, int act);
+// grid encoding + MLP forward in one kernel (k_fused_fwd_grid); wimage null: the LDS image is built from
+// params16 (16-byte aligned); enc16 (nullable) receives the SoA encoding
+void launch_fused_fwd(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, uint32_t D, HashType h, int act, uint32_t B,
+                      const void* wimage, const void* params16, const void* table16, const float* pos, const LevelInfo* levels, bool hash_grid,
+                      Interp interp, bool inrange_index, void* enc16, void* out16);
 void launch_mlp_infer(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, int act, bool soa, uint32_t B,
                       const void* wimage, const void* in16, void* out16);
 // out[b*n_out + o] = (float)in[b*in_stride + o]  (reference trim_and_cast_from, object.cu:60-67)
@@ -200,7 +214,7 @@ void launch_column_sums(hipStream_t st, const float* in, uint32_t n_parts, uint3
 constexpr uint32_t MLP_TAIL_GROUPS = 16;
 // out[p] = sum_j in[j*stride + grid_slab_index(map, p)] (the grid backward's slabs, fixed order)
 void launch_grid_slab_reduce(hipStream_t st, const float* in, uint32_t n_parts, uint32_t stride, uint32_t n, float* out,
-                             const GridSlabMap* map);
+                             const GridSlabMap* map, GradFinalize fin = {});
 // out[p] = sum_j in[j*stride + p] (p < n). tmp: caller-owned device scratch of
 // reduce_partials_tmp_floats(n_parts, n) floats (per workspace, so concurrent modules / streams /
 // devices never share it)

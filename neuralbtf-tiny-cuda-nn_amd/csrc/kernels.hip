@@ -37,17 +37,20 @@ __global__ __launch_bounds__(256) void k_reduce_groups(const float* __restrict__
 	}
 }
 
+// fin.out: the sum goes out finalised for the torch binding (grad_finalize_store) instead of as fp32
 __global__ __launch_bounds__(256) void k_grid_slab_reduce(const float* __restrict__ in, uint32_t n_parts, uint32_t stride, uint32_t n,
-                                                           float* __restrict__ out, const GridSlabMap* __restrict__ map) {
+                                                           float* __restrict__ out, const GridSlabMap* __restrict__ map, GradFinalize fin) {
 	const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
 	if (p >= n) return;
-	out[p] = slab_sum(in + grid_slab_index(map, p), stride, n_parts);
+	const float s = slab_sum(in + grid_slab_index(map, p), stride, n_parts);
+	if (fin.out) grad_finalize_store(s, fin.s, fin.out, p, fin.out_f32);
+	else out[p] = s;
 }
 
 void launch_grid_slab_reduce(hipStream_t st, const float* in, uint32_t n_parts, uint32_t stride, uint32_t n, float* out,
-                             const GridSlabMap* map) {
+                             const GridSlabMap* map, GradFinalize fin) {
 	if (!n) return;
-	hipLaunchKernelGGL(k_grid_slab_reduce, dim3(div_round_up(n, 256)), dim3(256), 0, st, in, n_parts, stride, n, out, map);
+	hipLaunchKernelGGL(k_grid_slab_reduce, dim3(div_round_up(n, 256)), dim3(256), 0, st, in, n_parts, stride, n, out, map, fin);
 	TCNN_HIP_CHECK(hipGetLastError());
 }
 
@@ -202,9 +205,7 @@ __global__ void k_div_f16(const _Float16* __restrict__ in, void* __restrict__ ou
 __global__ void k_grad_finalize(const float* __restrict__ g, void* __restrict__ out, float s, size_t n, int out_f32) {
 	const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
 	if (i >= n) return;
-	const _Float16 h = f16_rn((float)(_Float16)g[i] / s);
-	if (out_f32) ((float*)out)[i] = (float)h;
-	else ((_Float16*)out)[i] = h;
+	grad_finalize_store(g[i], s, out, i, out_f32);
 }
 void launch_grad_finalize(hipStream_t st, const float* g, void* out, float s, size_t n, bool out_f32) {
 	if (!n) return;

@@ -264,6 +264,33 @@ __device__ __forceinline__ void load_weights_lds(_Float16* smem, const _Float16*
 	for (int idx = tid; idx < 16 * W; idx += nthreads) s[L::oWo + out_row(idx / W) * L::RSW + idx % W] = p[idx];
 }
 
+// The same image built straight from the fp16 parameters, 8 halves per load: every row of every
+// matrix is a multiple of 8 halves long and starts 16-byte aligned in the image (FusedLayout), so a
+// 16-byte chunk of the parameters lands in one image row. Used when no packed image matches the
+// parameters (the Module path, the first step after a parameter change): no k_pack_weights launch.
+// `params` must be 16-byte aligned (the callers check).
+template <int W, int IN, int NH>
+__device__ __forceinline__ void load_weights_lds_v(_Float16* smem, const _Float16* __restrict__ params, int tid, int nthreads) {
+	using L = FusedLayout<W, IN, NH>;
+	static_assert(IN % 8 == 0 && W % 8 == 0 && L::RSI % 8 == 0 && L::RSW % 8 == 0, "16-byte rows");
+	constexpr int N0 = W * IN, NHW = L::NHM * W * W;
+	const uint4* p = (const uint4*)params;
+	for (int v = tid; v < L::N_MLP / 8; v += nthreads) {
+		const int idx = 8 * v;
+		int o;
+		if (idx < N0) {
+			o = L::oW0 + (idx / IN) * L::RSI + idx % IN;
+		} else if (idx < N0 + NHW) {
+			const int k = idx - N0;
+			o = L::oWh + (k / W) * L::RSW + k % W;  // rows of all hidden matrices are consecutive
+		} else {
+			const int k = idx - N0 - NHW;
+			o = L::oWo + out_row(k / W) * L::RSW + k % W;
+		}
+		*(uint4*)(smem + o) = p[v];
+	}
+}
+
 // The LDS weight image is built once per step by k_pack_weights into global memory; every
 // workgroup then copies it with 16-byte loads.
 template <int W, int IN, int NH>
@@ -279,7 +306,7 @@ __device__ __forceinline__ void copy_image_to_lds(_Float16* smem, const _Float16
 }
 
 struct FusedTrainArgs {
-	const _Float16* wimage; // packed LDS weight image (k_pack_weights)
+	const _Float16* wimage; // packed LDS weight image (k_pack_weights), or null: built from params
 	uint32_t B;
 	uint32_t dims;          // target width (n_output_dims)
 	float loss_scale;
@@ -625,7 +652,8 @@ __global__ __launch_bounds__(64 * FUSED_WAVES, 8 / FUSED_WAVES) void k_fused_tra
 	const int c = lane & 15, q = lane >> 4;
 
 	constexpr int NTHR = 64 * FUSED_WAVES;
-	copy_image_to_lds(smem, a.wimage, L::oStage, tid, NTHR);
+	if (a.wimage) copy_image_to_lds(smem, a.wimage, L::oStage, tid, NTHR);
+	else load_weights_lds_v<W, IN, NH>(smem, a.params, tid, NTHR);
 	LevelInfo* sLvl = (LevelInfo*)((char*)smem + RL::LVL_BYTES);
 	for (int l = tid; l < NLVL; l += NTHR) sLvl[l] = a.levels[l];
 	__syncthreads();
@@ -798,6 +826,117 @@ __global__ __launch_bounds__(256, 2) void k_mlp_infer(uint32_t B, const _Float16
 		const h4 yh = __builtin_convertvector(y, h4);
 #pragma unroll
 		for (int r = 0; r < 4; ++r) out[(size_t)i * 16 + 4 * r + q] = yh[r];  // out_row
+	}
+}
+
+
+// Grid encoding + MLP forward in one pass (inference, and the forward of a training context):
+// each lane gathers its sample's levels straight into the MFMA B-operand registers -- the same
+// encode_level_f2(_inrange) arithmetic as k_fused_train_grid, so the output and the kept encoding are
+// bit-identical to what the training kernel computes -- and the network runs as in k_mlp_infer.
+// `enc` (optional) receives the encoding SoA [IN][B], the layout the ENC_MEM training kernel reads.
+// Replaces the separate SoA grid forward (16.8 MB written and re-read at config_hash 2^18) plus
+// k_mlp_infer. Reference: the encoding's forward (grid.h:48-212) feeding kernel_mlp_fused<...,
+// INFERENCE=true> (fully_fused_mlp.cu:499-557).
+struct FusedFwdArgs {
+	uint32_t B;
+	const _Float16* wimage;  // packed image, or null: built from params
+	const _Float16* params;  // fp16 network weights [W0 | hidden | Wout]
+	const uint32_t* table;
+	const float* pos;
+	const LevelInfo* levels;
+	uint32_t hash_grid, interp, inrange_index;
+	_Float16* enc;  // nullable
+	_Float16* out;  // [B][16]
+};
+
+template <int W, int IN, int NH, uint32_t D, HashType H, Act ACT>
+__global__ __launch_bounds__(256, 4) void k_fused_fwd_grid(const FusedFwdArgs a) {
+	using L = FusedLayout<W, IN, NH>;
+	constexpr int NT = L::NT, KW = L::KW, NTI = L::NTI, KI = L::KI;
+	constexpr int NLVL = IN / 2;
+	extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
+	const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+	const int c = lane & 15, q = lane >> 4;
+	if (a.wimage) copy_image_to_lds(smem, a.wimage, L::oStage, tid, 256);
+	else load_weights_lds_v<W, IN, NH>(smem, a.params, tid, 256);
+	LevelInfo* sLvl = (LevelInfo*)((char*)smem + ((L::oStage * 2 + 15) & ~15));
+	for (int l = tid; l < NLVL; l += 256) sLvl[l] = a.levels[l];
+	__syncthreads();
+	const _Float16* sW0 = smem + L::oW0;
+	const _Float16* sWh = smem + L::oWh;
+	const _Float16* sWo = smem + L::oWo;
+	const bool hash_grid = a.hash_grid != 0;
+	const Interp interp = (Interp)a.interp;
+	const f4 fz = {0.0f, 0.0f, 0.0f, 0.0f};
+	const uint32_t B = a.B, n_chunks = B / 16;
+	for (uint32_t chunk = blockIdx.x * 4 + wave; chunk < n_chunks; chunk += gridDim.x * 4) {
+		const uint32_t i = chunk * 16 + c;
+		float xs[D];
+		bool inr = true;
+#pragma unroll
+		for (uint32_t d = 0; d < D; ++d) {
+			xs[d] = a.pos[(size_t)i * D + d];
+			inr = inr && xs[d] >= 0.0f && xs[d] <= 1.0f;
+		}
+		// xt[u][r] = feature 16 u + 4 q + r = feature (r & 1) of level 8 u + 2 q + (r >> 1)
+		h4 xt[NTI];
+		if (a.inrange_index && __builtin_amdgcn_ballot_w64(!inr) == 0) {
+#pragma unroll
+			for (int u = 0; u < NTI; ++u)
+#pragma unroll
+				for (int r2 = 0; r2 < 2; ++r2) {
+					const h2 e = encode_level_f2_inrange<D, H>(a.table, level_consts<D>(sLvl[8 * u + 2 * q + r2], hash_grid), xs);
+					xt[u][2 * r2] = e[0];
+					xt[u][2 * r2 + 1] = e[1];
+				}
+		} else {
+#pragma unroll
+			for (int u = 0; u < NTI; ++u)
+#pragma unroll
+				for (int r2 = 0; r2 < 2; ++r2) {
+					const h2 e = encode_level_f2<D, H>(a.table, sLvl[8 * u + 2 * q + r2], hash_grid, interp, xs);
+					xt[u][2 * r2] = e[0];
+					xt[u][2 * r2 + 1] = e[1];
+				}
+		}
+		if (a.enc) {
+#pragma unroll
+			for (int u = 0; u < NTI; ++u)
+#pragma unroll
+				for (int r = 0; r < 4; ++r) a.enc[(size_t)(16 * u + 4 * q + r) * B + i] = xt[u][r];
+		}
+		h4 act[NT];
+		{
+			f4 acc[NT];
+#pragma unroll
+			for (int t = 0; t < NT; ++t) {
+				acc[t] = fz;
+#pragma unroll
+				for (int s = 0; s < KI; ++s) acc[t] = mfma16(lds_afrag(sW0, L::RSI, 16 * t + c, 32 * s + 4 * q), cat8(xt[2 * s], xt[2 * s + 1]), acc[t]);
+			}
+#pragma unroll
+			for (int t = 0; t < NT; ++t) act[t] = act_fwd<ACT>(acc[t]);
+		}
+#pragma unroll
+		for (int j = 1; j < NH; ++j) {
+			const _Float16* Wm = sWh + (j - 1) * W * L::RSW;
+			f4 acc[NT];
+#pragma unroll
+			for (int t = 0; t < NT; ++t) {
+				acc[t] = fz;
+#pragma unroll
+				for (int s = 0; s < KW; ++s) acc[t] = mfma16(lds_afrag(Wm, L::RSW, 16 * t + c, 32 * s + 4 * q), cat8(act[2 * s], act[2 * s + 1]), acc[t]);
+			}
+#pragma unroll
+			for (int t = 0; t < NT; ++t) act[t] = act_fwd<ACT>(acc[t]);
+		}
+		f4 y = fz;
+#pragma unroll
+		for (int s = 0; s < KW; ++s) y = mfma16(lds_afrag(sWo, L::RSW, c, 32 * s + 4 * q), cat8(act[2 * s], act[2 * s + 1]), y);
+		const h4 yh = __builtin_convertvector(y, h4);
+#pragma unroll
+		for (int r = 0; r < 4; ++r) a.out[(size_t)i * 16 + 4 * r + q] = yh[r];  // out_row
 	}
 }
 

@@ -100,6 +100,7 @@ EngineSwitches EngineSwitches::from_env() {
 	s.no_inrange_index = on("TCNN_NO_INRANGE_INDEX");
 	s.split_encode = on("TCNN_SPLIT_ENCODE");
 	s.no_forward_keep = on("TCNN_NO_FORWARD_KEEP");
+	s.split_forward = on("TCNN_SPLIT_FORWARD");
 	const char* bin = std::getenv("TCNN_GRID_BIN");
 	s.grid_bin_all = bin && std::string(bin) == "all";
 	if (const char* e = std::getenv("TCNN_GRID_BWD_CHUNKS"))
@@ -326,9 +327,9 @@ void GridEncodingHost::backward_acc(hipStream_t st, GridBwdBufs& w, uint32_t B, 
 	launch_grid_acc(st, desc.n_pos_dims, desc.n_features_per_level, B, dy, layout, dy_stride, dev_levels(), a, grad32, adam);
 }
 
-void GridEncodingHost::reduce_items(hipStream_t st, GridBwdBufs& w, float* grad32) const {
+void GridEncodingHost::reduce_items(hipStream_t st, GridBwdBufs& w, float* grad32, GradFinalize fin) const {
 	if (slices.empty()) return;
-	launch_grid_slab_reduce(st, w.partial.as<float>(), w.n_chunks, n_lds_params, n_lds_params, grad32, slab_map());
+	launch_grid_slab_reduce(st, w.partial.as<float>(), w.n_chunks, n_lds_params, n_lds_params, grad32, slab_map(), fin);
 }
 
 void GridEncodingHost::backward(hipStream_t st, GridBwdBufs& w, uint32_t B, const float* pos, uint32_t pstride, const void* dy,
@@ -591,16 +592,9 @@ void NetworkHost::inference(hipStream_t st, StepWorkspace& ws, uint32_t B, const
 	const uint32_t IN = mlp.n_input;
 	const uint8_t* eparams = (const uint8_t*)params16 + (size_t)mlp.n_params() * 2;
 	if (fused_ok() && mlp_infer_supported(mlp.width, IN, mlp.n_hidden_layers, mlp.padded_output, mlp.activation)) {
-		ws.enc16.reserve((size_t)IN * B * 2);
-		launch_grid_fwd(st, grid->desc.n_pos_dims, grid->desc.n_features_per_level, grid->desc.hash_type, B, grid->desc.n_levels,
-		                pos, grid->desc.n_pos_dims, eparams, ws.enc16.p, true, 0, grid->dev_levels(), grid->hash_grid(), grid->desc.interp,
-		                grid->opts());
-		if (!(trust_image && ws.wimage_valid)) {
-			ws.wimage.reserve(fused_weight_image_bytes(mlp.width, IN, mlp.n_hidden_layers));
-			launch_pack_weights(st, mlp.width, IN, mlp.n_hidden_layers, params16, ws.wimage.p);
-			if (trust_image) ws.wimage_valid = true;  // the image now matches the trainer's parameters
-		}
-		launch_mlp_infer(st, mlp.width, IN, mlp.n_hidden_layers, mlp.activation, true, B, ws.wimage.p, ws.enc16.p, out16);
+		// the trainer's packed image when it matches its parameters, else the kernel builds its LDS
+		// image from the parameters themselves (no pack launch)
+		fused_forward(st, ws, B, pos, params16, trust_image && ws.wimage_valid, nullptr, out16);
 		return;
 	}
 	ws.enc16.reserve((size_t)IN * B * 2);
@@ -612,6 +606,35 @@ void NetworkHost::inference(hipStream_t st, StepWorkspace& ws, uint32_t B, const
 	TCNN_CHECK(layered_ok(), "inference: network shape not supported by the MI355X engine");
 	enc->forward_aos(st, B, pos, eparams, ws.enc16.p);
 	forward_layers(st, ws, B, params16, out16, false);
+}
+
+// grid encoding + MLP forward on the packed weight image (ws.wimage): one kernel (k_fused_fwd_grid),
+// or under TCNN_SPLIT_FORWARD the SoA grid forward then k_mlp_infer. enc_soa (nullable) receives the
+// encoding [IN][B] for a training context's backward.
+void NetworkHost::fused_forward(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const void* params16, bool use_image,
+                                void* enc_soa, void* out16) {
+	const uint32_t IN = mlp.n_input;
+	const uint8_t* eparams = (const uint8_t*)params16 + (size_t)mlp.n_params() * 2;
+	if (sw.split_forward) {
+		if (!use_image) {
+			ws.wimage.reserve(fused_weight_image_bytes(mlp.width, IN, mlp.n_hidden_layers));
+			launch_pack_weights(st, mlp.width, IN, mlp.n_hidden_layers, params16, ws.wimage.p);
+			ws.wimage_valid = false;  // packed from these parameters, which need not be the trainer's
+		}
+		void* enc = enc_soa;
+		if (!enc) {
+			ws.enc16.reserve((size_t)IN * B * 2);
+			enc = ws.enc16.p;
+		}
+		launch_grid_fwd(st, grid->desc.n_pos_dims, grid->desc.n_features_per_level, grid->desc.hash_type, B, grid->desc.n_levels, pos,
+		                grid->desc.n_pos_dims, eparams, enc, true, 0, grid->dev_levels(), grid->hash_grid(), grid->desc.interp,
+		                grid->opts());
+		launch_mlp_infer(st, mlp.width, IN, mlp.n_hidden_layers, mlp.activation, true, B, ws.wimage.p, enc, out16);
+		return;
+	}
+	launch_fused_fwd(st, mlp.width, IN, mlp.n_hidden_layers, grid->desc.n_pos_dims, grid->desc.hash_type, mlp.activation, B,
+	                 use_image ? ws.wimage.p : nullptr, params16, eparams, pos, grid->dev_levels(), grid->hash_grid(), grid->desc.interp,
+	                 grid->inrange_index_ok && grid->desc.interp == Interp::Linear && !sw.no_inrange_index, enc_soa, out16);
 }
 
 int NetworkHost::backward_engine_keep(bool with_dinput) const {
@@ -627,12 +650,7 @@ int NetworkHost::forward_keep(hipStream_t st, StepWorkspace& ws, uint32_t B, con
 	const uint8_t* eparams = (const uint8_t*)params16 + (size_t)mlp.n_params() * 2;
 	if (layout == KEEP_FUSED_SOA && mlp_infer_supported(mlp.width, IN, mlp.n_hidden_layers, mlp.padded_output, mlp.activation)) {
 		keep.reserve((size_t)IN * B * 2);
-		launch_grid_fwd(st, grid->desc.n_pos_dims, grid->desc.n_features_per_level, grid->desc.hash_type, B, grid->desc.n_levels, pos,
-		                grid->desc.n_pos_dims, eparams, keep.p, true, 0, grid->dev_levels(), grid->hash_grid(), grid->desc.interp,
-		                grid->opts());
-		ws.wimage.reserve(fused_weight_image_bytes(mlp.width, IN, mlp.n_hidden_layers));
-		launch_pack_weights(st, mlp.width, IN, mlp.n_hidden_layers, params16, ws.wimage.p);
-		launch_mlp_infer(st, mlp.width, IN, mlp.n_hidden_layers, mlp.activation, true, B, ws.wimage.p, keep.p, out16);
+		fused_forward(st, ws, B, pos, params16, false, keep.p, out16);
 		return KEEP_FUSED_SOA;
 	}
 	if (layout == KEEP_TILE_AOS && tile_infer_ok()) {
@@ -675,12 +693,16 @@ void NetworkHost::fused_kernel(hipStream_t st, StepWorkspace& ws, uint32_t B, co
 	ws.dLdenc.reserve((size_t)L * F * B * 2);
 	ws.wgrad_partial.reserve((size_t)nb * n_mlp * 4);
 	ws.loss_partial.reserve((size_t)nb * 4);
-	if (pack || !ws.wimage_valid) pack_weights(st, ws, params16);
+	// without a packed image that matches params16, every workgroup builds its LDS image from the
+	// parameters (load_weights_lds_v) -- no k_pack_weights launch; the Adam tail of the grid backward
+	// still writes the next step's image into ws.wimage
+	ws.wimage.reserve(fused_weight_image_bytes(mlp.width, mlp.n_input, mlp.n_hidden_layers));
+	const bool use_image = !pack && ws.wimage_valid;
 	const uint8_t* table = (const uint8_t*)params16 + (size_t)n_mlp * 2;
 	launch_fused_train(st, mlp.width, mlp.n_input, mlp.n_hidden_layers, grid->desc.n_pos_dims, grid->desc.hash_type,
 	                   mlp.activation, B, dims, loss_scale, params16, table, pos, target, out16, ws.dLdenc.p,
 	                   ws.wgrad_partial.as<float>(), ws.loss_partial.as<float>(), grid->dev_levels(), grid->hash_grid(),
-	                   grid->desc.interp, nb, dout16, ws.wimage.p, loss_l2,
+	                   grid->desc.interp, nb, dout16, use_image ? ws.wimage.p : nullptr, loss_l2,
 	                   grid->inrange_index_ok && grid->desc.interp == Interp::Linear && !sw.no_inrange_index, enc_soa,
 	                   dout16 ? ext_dout_scale : 1.0f);
 }
@@ -718,10 +740,20 @@ void NetworkHost::fwd_bwd_fused(hipStream_t st, StepWorkspace& ws, uint32_t B, c
 	ws.loss_sum.reserve(16);
 	ep.d_loss = ws.loss_sum.as<float>();
 	TCNN_CHECK(n_mlp % 4 == 0, "network parameter count must be a multiple of 4");
+	// the torch binding's finalised gradient straight from the two reductions (no k_grad_finalize
+	// pass) when every grid level goes through the slabs
+	const bool fin = grad_fin.out && grid->bin_levels.empty();
+	GradFinalize fin_grid{};
+	if (fin) {
+		ep.fin = grad_fin;
+		fin_grid = grad_fin;
+		fin_grid.out = (char*)grad_fin.out + (size_t)n_mlp * (grad_fin.out_f32 ? 4 : 2);
+	}
+	grad_fin_done = fin;
 	grid_backward(st, ws, B, pos, &ep);
 	grid->backward_acc(st, ws.gbw, B, ws.dLdenc.p, 0, 0, grad32 + n_mlp);
 	if (mark) mark(2);
-	grid->reduce_items(st, ws.gbw, grad32 + n_mlp);
+	grid->reduce_items(st, ws.gbw, grad32 + n_mlp, fin_grid);
 	if (mark) mark(3);
 }
 

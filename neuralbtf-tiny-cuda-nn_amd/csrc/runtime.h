@@ -63,6 +63,7 @@ struct EngineSwitches {
 	bool no_inrange_index = false;  // TCNN_NO_INRANGE_INDEX: the generic grid index in every kernel
 	bool split_encode = false;      // TCNN_SPLIT_ENCODE: the encoding as its own pass (experiment)
 	bool no_forward_keep = false;   // TCNN_NO_FORWARD_KEEP: Module backward recomputes the forward
+	bool split_forward = false;     // TCNN_SPLIT_FORWARD: grid forward + k_mlp_infer instead of k_fused_fwd_grid
 	bool grid_bin_all = false;      // TCNN_GRID_BIN=all: bin every grid level that does not fit whole
 	uint32_t grid_bwd_chunks = 0;   // TCNN_GRID_BWD_CHUNKS: grid backward point chunks (0: automatic)
 	static EngineSwitches from_env();
@@ -135,7 +136,7 @@ struct GridEncodingHost {
 	                  uint32_t dy_stride) const;
 	void backward_acc(hipStream_t st, GridBwdBufs& w, uint32_t B, const void* dy, int layout, uint32_t dy_stride, float* grad32,
 	                  const GridAccAdam* adam = nullptr) const;
-	void reduce_items(hipStream_t st, GridBwdBufs& w, float* grad32) const;
+	void reduce_items(hipStream_t st, GridBwdBufs& w, float* grad32, GradFinalize fin = {}) const;
 	void backward(hipStream_t st, GridBwdBufs& w, uint32_t B, const float* pos, uint32_t pstride, const void* dy, int layout,
 	              uint32_t dy_stride, float* grad32) const;
 };
@@ -211,6 +212,10 @@ struct NetworkHost {
 	// the fused kernel reads an external dL/dy as fp16(dL/dy * ext_dout_scale): the torch binding's loss
 	// scale folded into the load (set only around a Module backward, tcnn_module_backward_scaled)
 	float ext_dout_scale = 1.0f;
+	// set by the torch binding's backward (tcnn_module_backward_scaled): the fused engine writes the
+	// finalised parameter gradient there from its reductions; grad_fin_done reports that it did
+	GradFinalize grad_fin{};
+	bool grad_fin_done = false;
 	std::unique_ptr<EncodingHost> enc;
 	GridEncodingHost* grid = nullptr;  // enc->grid when the encoding is a grid
 	MlpHost mlp;
@@ -239,6 +244,8 @@ struct NetworkHost {
 	// layer-wise engine keeps nothing (its backward recomputes the forward).
 	enum : int { KEEP_NONE = 0, KEEP_FUSED_SOA = 1, KEEP_TILE_AOS = 2 };
 	int backward_engine_keep(bool with_dinput) const;
+	void fused_forward(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const void* params16, bool use_image, void* enc_soa,
+	                   void* out16);
 	int forward_keep(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const void* params16, void* out16, bool with_dinput,
 	                 DevBuf& keep);
 	// forward+backward; dout16 == nullptr -> RelativeL2 on target, else external dL/dout.

@@ -14,13 +14,28 @@ from helpers import CONFIG_HASH
 pytestmark = pytest.mark.gpu
 
 
-def _grads(torch, model, x, create_graph):
+def _grads(torch, model, x, create_graph, input_grad=True):
     model.zero_grad(set_to_none=True)
-    xi = x.clone().requires_grad_(True)
+    xi = x.clone().requires_grad_(input_grad)
     out = model(xi)
     loss = ((out.float() - 0.25) ** 2).sum()
     loss.backward(create_graph=create_graph)
-    return model.params.grad.detach().clone(), xi.grad.detach().clone()
+    return model.params.grad.detach().clone(), (xi.grad.detach().clone() if input_grad else None)
+
+
+def test_fused_engine_fast_path_matches_differentiable_path():
+    """Without input gradients the network runs the fused engine, whose reductions write the finalised
+    fp16(fp16(g) / s) gradient themselves (GradFinalize) -- the same bits as the differentiable path's
+    scale / backward / divide sequence."""
+    import torch
+    import tinycudann as tcnn
+    torch.manual_seed(4)
+    model = tcnn.NetworkWithInputEncoding(2, 3, CONFIG_HASH["encoding"], CONFIG_HASH["network"]).cuda()
+    x = torch.rand(1 << 15, 2, device="cuda")
+    gp_fast, _ = _grads(torch, model, x, False, input_grad=False)
+    gp_ref, _ = _grads(torch, model, x, True, input_grad=False)
+    assert float(gp_fast.abs().max()) > 0
+    np.testing.assert_array_equal(gp_fast.cpu().numpy(), gp_ref.cpu().numpy())
 
 
 @pytest.mark.parametrize("kind", ["network", "grid"])
