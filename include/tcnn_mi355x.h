@@ -55,6 +55,9 @@ void tcnn_set_log_callback(tcnn_log_callback_t callback, void* user);
 /* generate_random_uniform<float>(stream, rng, n, out, lower, upper) (random.h:57-70): n floats in the
  * reference's strided order (4 per thread, thread i jumps 4i) from the pcg32 stream {*rng_state,
  * *rng_inc} (dependencies/pcg32/pcg32.h); the state is advanced by n on return, as rng.advance(n). */
+/* generate_random_logistic (random.h:77-80): logit(u) * stddev * 0.551328895 + mean over the uniform
+ * stream of tcnn_generate_random_uniform; the state advances by n. */
+int tcnn_generate_random_logistic(void* stream, uint64_t* rng_state, uint64_t* rng_inc, uint64_t n, float* out, float mean, float stddev);
 int tcnn_generate_random_uniform(void* stream, uint64_t* rng_state, uint64_t* rng_inc, uint64_t n, float* out, float lower,
                                  float upper);
 
@@ -154,6 +157,12 @@ int tcnn_trainer_optimizer_step(tcnn_trainer* t, void* stream);
 typedef struct tcnn_trainer_context tcnn_trainer_context;  /* Trainer::ForwardContext (trainer.h:89-95) */
 tcnn_trainer_context* tcnn_trainer_forward(tcnn_trainer* t, void* stream, uint32_t n, const float* input, const float* target,
                                            const float* data_pdf, const void* external_dL_dy, int prepare_input_gradients);
+/* Trainer::forward with output perturbation (trainer.h:114-123): perturbation fp32 [n x padded_output_width]
+ * (the caller's noise, e.g. tcnn_generate_random_logistic with stddev = perturbation_sigma) is added to
+ * the output and the loss and its dL/doutput are evaluated on the perturbed output; the context's
+ * output stays the unperturbed one. */
+tcnn_trainer_context* tcnn_trainer_forward_perturbed(tcnn_trainer* t, void* stream, uint32_t n, const float* input, const float* target,
+                                                     const float* data_pdf, const float* perturbation, int prepare_input_gradients);
 /* gradient_mode: GradientMode (common.h) -- 0 Overwrite, 1 Accumulate, 2 Ignore (dL/dinput only; the
  * parameter gradients are left as they are) */
 int tcnn_trainer_backward(tcnn_trainer* t, void* stream, const tcnn_trainer_context* ctx, uint32_t n, const float* input,

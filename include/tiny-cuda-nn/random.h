@@ -1,5 +1,6 @@
 // tiny-cuda-nn/random.h -- default_rng_t (= pcg32, reference common_device.h:331,
-// dependencies/pcg32/pcg32.h) and generate_random_uniform (random.h:57-75) for the MI355X engine.
+// dependencies/pcg32/pcg32.h), generate_random_uniform and generate_random_logistic (random.h:57-85)
+// for the MI355X engine.
 //
 // pcg32: the PCG-XSH-RR 64/32 generator (O'Neill 2014) with the reference's conventions: default
 // stream 1 (inc = 2 * initseq + 1), seeding by two steps around adding initstate, next_float() as the
@@ -85,6 +86,21 @@ void generate_random_uniform(hipStream_t stream, RNG& rng, size_t n_elements, T*
 template <typename T, typename RNG>
 void generate_random_uniform(RNG& rng, size_t n_elements, T* out, const T lower = (T)0.0, const T upper = (T)1.0) {
 	generate_random_uniform<T>(nullptr, rng, n_elements, out, lower, upper);
+}
+
+// random.h:77-85: logistic values (logit(u) * stddev * 0.551328895 + mean) over the same stream
+inline void generate_random_logistic(hipStream_t stream, default_rng_t& rng, size_t n_elements, float* out, const float mean = 0.0f,
+                                     const float stddev = 1.0f) {
+	detail::check_rc(tcnn_generate_random_logistic(stream, &rng.state, &rng.inc, (uint64_t)n_elements, out, mean, stddev));
+}
+template <typename T, typename RNG>
+void generate_random_logistic(hipStream_t stream, RNG& rng, size_t n_elements, T* out, const T mean = (T)0.0, const T stddev = (T)1.0) {
+	static_assert(std::is_same<T, float>::value, "generate_random_logistic: the engine generates float");
+	generate_random_logistic(stream, (default_rng_t&)rng, n_elements, out, mean, stddev);
+}
+template <typename T, typename RNG>
+void generate_random_logistic(RNG& rng, size_t n_elements, T* out, const T mean = (T)0.0, const T stddev = (T)1.0) {
+	generate_random_logistic<T>(nullptr, rng, n_elements, out, mean, stddev);
 }
 
 }  // namespace tcnn

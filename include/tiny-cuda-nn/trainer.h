@@ -8,16 +8,19 @@
 // (trainer.h:205-211 reduces the context's loss values). With any of the reference's options (data_pdf, external dL/dy, dL/dinput,
 // Accumulate gradients) training_step runs as the reference's does: forward() (network output +
 // loss, or the caller's dL/dy) then backward() (tcnn_trainer_forward / _backward), then the optimizer;
-// loss(ctx) then reads the context's own loss.
+// loss(ctx) then reads the context's own loss. Output perturbation (perturbation_sigma > 0) runs the
+// same way, with the reference's logistic noise on the output the loss sees.
 #pragma once
 
 #include <memory>
+#include <random>
 #include <vector>
 
 #include "encoding.h"
 #include "network.h"
 #include "network_with_input_encoding.h"
 #include "optimizer.h"
+#include "random.h"
 
 namespace tcnn {
 
@@ -31,9 +34,9 @@ public:
 	// trainer.h:50-57: the trainer owns the parameters (seeded pcg32{seed_seq{seed}[0]})
 	Trainer(std::shared_ptr<Model> model, std::shared_ptr<Optimizer<PARAMS_T>> optimizer, std::shared_ptr<Loss<COMPUTE_T>> loss,
 	        uint32_t seed = 1337, float perturbation_sigma = 0)
-	    : m_model{std::move(model)}, m_optimizer{std::move(optimizer)}, m_loss{std::move(loss)}, m_seed{seed} {
+	    : m_model{std::move(model)}, m_optimizer{std::move(optimizer)}, m_loss{std::move(loss)}, m_seed{seed},
+	      m_perturbation_sigma{perturbation_sigma} {
 		static_assert(std::is_same<T, float>::value || std::is_same<T, __half>::value, "Trainer: inputs are fp32 or fp16");
-		if (perturbation_sigma != 0) throw std::runtime_error{"Trainer: output perturbation is not supported by the MI355X engine"};
 		if (m_model->engine_network().is_null())
 			throw std::runtime_error{"Trainer: " + m_model->name() + " has no network; this engine trains a network behind an encoding "
 			                         "(NetworkWithInputEncoding, or Network for the network alone)"};
@@ -46,6 +49,7 @@ public:
 		m_h = detail::check_handle(tcnn_trainer_create(m_model->input_width(), m_model->output_width(), cfg.dump().c_str(), seed));
 		m_model->attach(m_h);
 		m_optimizer->attach(m_h);
+		reset_rng();
 	}
 	virtual ~Trainer() {
 		if (m_model->trainer_handle() == m_h) m_model->attach(nullptr);
@@ -115,9 +119,19 @@ public:
 		ctx->owner = this;
 		ctx->step = ++m_n_steps;
 		const float* in = detail::engine_input(stream, input, ctx->input_f32);
-		ctx->h = tcnn_trainer_forward(m_h, stream, n, in, external_dL_dy ? nullptr : target.data(),
-		                              data_pdf ? data_pdf->data() : nullptr, external_dL_dy ? external_dL_dy->data() : nullptr,
-		                              prepare_input_gradients ? 1 : 0);
+		if (m_perturbation_sigma > 0 && !external_dL_dy) {
+			// trainer.h:114-123: logistic noise (m_rng) added to the output; the loss and dL/dy see the
+			// perturbed output, the context's output stays unperturbed
+			const size_t n_el = (size_t)padded_output_width() * n;
+			m_perturbation.enlarge(n_el);
+			generate_random_logistic(stream, m_rng, n_el, m_perturbation.data(), 0.0f, m_perturbation_sigma);
+			ctx->h = tcnn_trainer_forward_perturbed(m_h, stream, n, in, target.data(), data_pdf ? data_pdf->data() : nullptr,
+			                                        m_perturbation.data(), prepare_input_gradients ? 1 : 0);
+		} else {
+			ctx->h = tcnn_trainer_forward(m_h, stream, n, in, external_dL_dy ? nullptr : target.data(),
+			                              data_pdf ? data_pdf->data() : nullptr, external_dL_dy ? external_dL_dy->data() : nullptr,
+			                              prepare_input_gradients ? 1 : 0);
+		}
 		if (!ctx->h) throw std::runtime_error{tcnn_last_error()};
 		const uint32_t w = padded_output_width();
 		ctx->output = GPUMatrix<COMPUTE_T>{(COMPUTE_T*)tcnn_trainer_context_output(ctx->h), w, n};
@@ -160,6 +174,7 @@ public:
 	// trainer.h:68-87
 	void initialize_params() {
 		detail::check_rc(tcnn_trainer_initialize_params(m_h, m_seed));
+		reset_rng();
 		++m_n_steps;  // contexts of earlier steps no longer describe the parameters
 	}
 
@@ -173,7 +188,7 @@ public:
 		CHECK_THROW(input.m() == m_model->input_width());
 		CHECK_THROW(input.n() % BATCH_SIZE_GRANULARITY == 0);
 		CHECK_THROW(input.layout() == CM && input.is_contiguous());
-		if (data_pdf || dL_dinput || external_dL_dy || param_gradients_mode != GradientMode::Overwrite) {
+		if (data_pdf || dL_dinput || external_dL_dy || param_gradients_mode != GradientMode::Overwrite || m_perturbation_sigma > 0) {
 			// trainer.h:163-203 as written: forward, backward, optimizer
 			auto ctx = forward(stream, default_loss_scale<PARAMS_T>(), input, target, data_pdf, use_inference_params, dL_dinput != nullptr,
 			                   external_dL_dy);
@@ -303,12 +318,28 @@ public:
 	// which of the engine's paths trains this model ("fused" / "layered")
 	std::string engine() const { return tcnn_trainer_engine(m_h); }
 	tcnn_trainer* handle() const { return m_h; }
+	float perturbation_sigma() const { return m_perturbation_sigma; }
 
 private:
+	// trainer.h:52-55, 68-87: the trainer's pcg32{seed_seq{seed}[0]} after the parameter initialisation
+	// drew its n_params uniforms (generate_random_uniform advances by n_elements, random.h:64) -- the
+	// engine initialises from the same seed, so this is the state the reference's m_rng has when the
+	// first perturbation is drawn
+	void reset_rng() {
+		std::seed_seq seq{m_seed};
+		std::vector<uint32_t> seeds(2);
+		seq.generate(std::begin(seeds), std::end(seeds));
+		m_rng = default_rng_t{seeds.front()};
+		m_rng.advance((int64_t)n_params());
+	}
+
 	std::shared_ptr<Model> m_model;
 	std::shared_ptr<Optimizer<PARAMS_T>> m_optimizer;
 	std::shared_ptr<Loss<COMPUTE_T>> m_loss;
 	uint32_t m_seed;
+	float m_perturbation_sigma;
+	default_rng_t m_rng;
+	GPUMemory<float> m_perturbation;
 	tcnn_trainer* m_h = nullptr;
 	uint64_t m_n_steps = 0;
 	GPUMemory<float> m_input_scratch;  // Trainer<__half, ...>: the widened batch of training_step

@@ -325,6 +325,17 @@ void tcnn_free_temporary_memory(void) {  // free_all_gpu_memory_arenas (gpu_memo
 }
 int tcnn_has_networks(void) { return 1; }
 
+int tcnn_generate_random_logistic(void* stream, uint64_t* rng_state, uint64_t* rng_inc, uint64_t n, float* out, float mean, float stddev) {
+	return guard([&] {
+		TCNN_CHECK(rng_state && rng_inc, "generate_random_logistic: rng state missing");
+		launch_generate_logistic((hipStream_t)stream, n, *rng_state, *rng_inc, out, mean, stddev);
+		Pcg32 r;
+		r.state = *rng_state;
+		r.inc = *rng_inc;
+		r.advance((int64_t)n);  // random.h:64
+		*rng_state = r.state;
+	});
+}
 int tcnn_generate_random_uniform(void* stream, uint64_t* rng_state, uint64_t* rng_inc, uint64_t n, float* out, float lower, float upper) {
 	return guard([&] {
 		TCNN_CHECK(rng_state && rng_inc, "generate_random_uniform: rng state missing");
@@ -525,6 +536,17 @@ tcnn_trainer_context* tcnn_trainer_forward(tcnn_trainer* t, void* stream, uint32
 	const int rc = guard([&] {
 		TCNN_CHECK(n > 0, "forward: empty batch");
 		auto c = t->t->forward((hipStream_t)stream, n, in, target, pdf, ext, prep != 0);
+		r = new tcnn_trainer_context{std::move(c)};
+	});
+	return rc == 0 ? r : nullptr;
+}
+tcnn_trainer_context* tcnn_trainer_forward_perturbed(tcnn_trainer* t, void* stream, uint32_t n, const float* in, const float* target,
+                                                     const float* pdf, const float* perturbation, int prep) {
+	tcnn_trainer_context* r = nullptr;
+	const int rc = guard([&] {
+		TCNN_CHECK(n > 0, "forward: empty batch");
+		TCNN_CHECK(target != nullptr, "forward_perturbed: a target is required");
+		auto c = t->t->forward((hipStream_t)stream, n, in, target, pdf, nullptr, prep != 0, perturbation);
 		r = new tcnn_trainer_context{std::move(c)};
 	});
 	return rc == 0 ? r : nullptr;

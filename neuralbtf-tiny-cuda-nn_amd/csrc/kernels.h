@@ -246,6 +246,9 @@ void launch_mlp_tile_infer(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH,
 
 // generate_random_uniform<float> (random.h:57-70) from pcg32 {state, inc} (not advanced here)
 void launch_generate_uniform(hipStream_t st, uint64_t n, uint64_t state, uint64_t inc, float* out, float lo, float hi);
+void launch_generate_logistic(hipStream_t st, uint64_t n, uint64_t state, uint64_t inc, float* out, float mean, float stddev);
+// pert16[i] = fp16(out16[i] + noise[i]) (the Trainer's output perturbation)
+void launch_add_perturbation(hipStream_t st, uint32_t n, const void* out16, const float* noise, void* pert16);
 void launch_adam(hipStream_t st, const AdamArgs& a, float* w32, void* w16, const float* grad32, void* grad16,
                  float* m1, float* m2, uint32_t* steps);
 

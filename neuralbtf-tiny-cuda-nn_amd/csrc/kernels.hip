@@ -139,6 +139,41 @@ __global__ __launch_bounds__(128) void k_generate_uniform(uint64_t n, uint64_t s
 	}
 }
 
+// random.h:77-80 generate_random_logistic: logit(u) * stddev * 0.551328895 + mean over the same
+// strided uniform stream (common_device.h:46-48 logit, its clamp to [1e-9, 1 - 1e-9])
+__global__ __launch_bounds__(128) void k_generate_logistic(uint64_t n, uint64_t state, uint64_t inc, float* __restrict__ out, float mean,
+                                                           float stddev) {
+	const uint64_t i = threadIdx.x + (uint64_t)blockIdx.x * blockDim.x;
+	const uint64_t n_threads = (uint64_t)blockDim.x * gridDim.x;
+	pcg32_advance(state, inc, i * 4);
+#pragma unroll
+	for (uint32_t j = 0; j < 4; ++j) {
+		const uint64_t idx = i + n_threads * j;
+		if (idx >= n) return;
+		const float u = pcg32_next_float(state, inc);
+		const float l = -logf(1.0f / fminf(fmaxf(u, 1e-9f), 1.0f - 1e-9f) - 1.0f);
+		out[idx] = __builtin_fmaf(l * stddev, 0.551328895f, mean);
+	}
+}
+
+void launch_generate_logistic(hipStream_t st, uint64_t n, uint64_t state, uint64_t inc, float* out, float mean, float stddev) {
+	if (n == 0) return;
+	const uint64_t n_thr = (n + 3) / 4;
+	hipLaunchKernelGGL(k_generate_logistic, dim3((uint32_t)((n_thr + 127) / 128)), dim3(128), 0, st, n, state, inc, out, mean, stddev);
+	TCNN_HIP_CHECK(hipGetLastError());
+}
+
+// trainer.h:114-121: the perturbed output the loss sees, add<<<>>> (common_device.h:963-968)
+__global__ void k_add_perturbation(uint32_t n, const _Float16* __restrict__ out, const float* __restrict__ noise, _Float16* __restrict__ pert) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i < n) pert[i] = (_Float16)((float)out[i] + noise[i]);
+}
+void launch_add_perturbation(hipStream_t st, uint32_t n, const void* out16, const float* noise, void* pert16) {
+	if (!n) return;
+	hipLaunchKernelGGL(k_add_perturbation, dim3(div_round_up(n, 256u)), dim3(256), 0, st, n, (const _Float16*)out16, noise, (_Float16*)pert16);
+	TCNN_HIP_CHECK(hipGetLastError());
+}
+
 void launch_generate_uniform(hipStream_t st, uint64_t n, uint64_t state, uint64_t inc, float* out, float lo, float hi) {
 	if (n == 0) return;
 	const uint64_t n_thr = (n + 3) / 4;

@@ -1285,7 +1285,7 @@ void TrainerHost::optimizer_step(hipStream_t st) {  // AdamOptimizer::step, adam
 }
 
 std::unique_ptr<TrainerFwdCtx> TrainerHost::forward(hipStream_t st, uint32_t B, const float* input, const float* target, const float* pdf,
-                                                    const void* ext_dLdy16, bool prep_dinput) {
+                                                    const void* ext_dLdy16, bool prep_dinput, const float* perturbation) {
 	TCNN_CHECK(B % BATCH_GRANULARITY == 0, "forward: batch size must be a multiple of 256");
 	TCNN_CHECK(ext_dLdy16 || target, "forward: a target (or an external dL/dy) is required");
 	NetworkHost& m = *model;
@@ -1300,7 +1300,13 @@ std::unique_ptr<TrainerFwdCtx> TrainerHost::forward(hipStream_t st, uint32_t B, 
 		c->dLdy16.reserve((size_t)B * OUTP * 2);
 		c->n_lpart = relative_l2_n_blocks(B, OUTP);
 		c->lpart.reserve((size_t)c->n_lpart * 4);
-		launch_relative_l2_partial(st, B, OUTP, n_output_dims, loss_scale, c->out16.p, target, c->dLdy16.p, c->lpart.as<float>(),
+		const void* loss_in = c->out16.p;
+		if (perturbation) {  // trainer.h:114-123: the loss (and its dL/dy) on the perturbed output
+			c->pert16.reserve((size_t)B * OUTP * 2);
+			launch_add_perturbation(st, B * OUTP, c->out16.p, perturbation, c->pert16.p);
+			loss_in = c->pert16.p;
+		}
+		launch_relative_l2_partial(st, B, OUTP, n_output_dims, loss_scale, loss_in, target, c->dLdy16.p, c->lpart.as<float>(),
 		                           m.loss_l2, pdf);
 	}
 	ws.wimage_valid = false;  // forward_keep may have packed the image in place

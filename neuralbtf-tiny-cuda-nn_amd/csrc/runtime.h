@@ -324,6 +324,7 @@ struct TrainerFwdCtx {
 	DevBuf keep;
 	int layout = 0;
 	DevBuf out16, dLdy16, lpart;
+	DevBuf pert16;              // output + perturbation, what the loss saw (trainer.h:114-123)
 	const void* ext = nullptr;  // external dL/dy (not owned)
 	uint32_t n_lpart = 0;
 	const void* dLdy() const { return ext ? ext : dLdy16.p; }
@@ -379,8 +380,9 @@ struct TrainerHost {
 	// output], loss-scaled like the loss's own), dL/dinput (fp32 [B][n_input_dims]) and Accumulate
 	// gradients (added to gradients_fp32() instead of overwriting it). Gradients land in the buffer
 	// optimizer_step() reads.
+	// perturbation (nullable): fp32 [B][padded output] noise added to the output before the loss
 	std::unique_ptr<TrainerFwdCtx> forward(hipStream_t st, uint32_t B, const float* input, const float* target, const float* pdf,
-	                                       const void* ext_dLdy16, bool prep_dinput);
+	                                       const void* ext_dLdy16, bool prep_dinput, const float* perturbation = nullptr);
 	// gradient_mode: 0 Overwrite, 1 Accumulate, 2 Ignore (GradientMode, common.h)
 	void backward(hipStream_t st, const TrainerFwdCtx& c, uint32_t B, const float* input, float* dL_dinput, int gradient_mode);
 	float ctx_loss(hipStream_t st, const TrainerFwdCtx& c);

@@ -30,6 +30,7 @@ _SIGS = {
     "tcnn_preferred_precision": (c_int, []),
     "tcnn_set_log_callback": (None, [LOG_CALLBACK, c_void_p]),
     "tcnn_generate_random_uniform": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_float, c_float]),
+    "tcnn_generate_random_logistic": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_float, c_float]),
     "tcnn_create_network_with_input_encoding": (c_void_p, [c_uint32, c_uint32, c_char_p, c_char_p]),
     "tcnn_create_network": (c_void_p, [c_uint32, c_uint32, c_char_p]),
     "tcnn_create_encoding": (c_void_p, [c_uint32, c_char_p, c_int]),
@@ -57,6 +58,7 @@ _SIGS = {
     "tcnn_trainer_training_step": (c_int, [c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_int]),
     "tcnn_trainer_optimizer_step": (c_int, [c_void_p, c_void_p]),
     "tcnn_trainer_forward": (c_void_p, [c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_int]),
+    "tcnn_trainer_forward_perturbed": (c_void_p, [c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_int]),
     "tcnn_trainer_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_int]),
     "tcnn_trainer_context_loss": (c_float, [c_void_p, c_void_p, c_void_p]),
     "tcnn_trainer_context_output": (c_void_p, [c_void_p]),

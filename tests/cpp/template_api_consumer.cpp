@@ -334,6 +334,62 @@ int main(int argc, char** argv) {
 			}
 			EXPECT(threw);
 		}
+		// output perturbation (trainer.h:50-57, 114-123): logistic noise of scale sigma on the output the
+		// loss sees; the generator is random.h:77-80 over the uniform stream
+		{
+			const uint32_t n = 1 << 12;
+			GPUMemory<float> noise(n);
+			default_rng_t r{7};
+			generate_random_logistic<float>(stream, r, n, noise.data(), 0.0f, 1.0f);
+			std::vector<float> hn(n);
+			noise.copy_to_host(hn);
+			default_rng_t adv{7};
+			adv.advance(n);
+			EXPECT(r == adv);
+			const uint32_t n_thr = (n + 3) / 4, n_threads = (n_thr + 127) / 128 * 128;
+			default_rng_t base{7};
+			int bad = 0;
+			for (uint32_t i = 0; i < n_threads; ++i) {
+				default_rng_t q = base;
+				q.advance(4 * i);
+				for (uint32_t j = 0; j < 4; ++j) {
+					const uint32_t idx = i + n_threads * j;
+					if (idx >= n) break;
+					const float u = q.next_float();
+					const float l = -std::log(1.0f / std::fmin(std::fmax(u, 1e-9f), 1.0f - 1e-9f) - 1.0f);
+					if (std::fabs(hn[idx] - l * 0.551328895f) > 1e-5f * (1.0f + std::fabs(l))) ++bad;
+				}
+			}
+			EXPECT(bad == 0);
+
+			std::shared_ptr<NetworkWithInputEncoding<network_precision_t>> pnet{
+			    new NetworkWithInputEncoding<network_precision_t>(2, 3, config["encoding"], config["network"])};
+			std::shared_ptr<Loss<network_precision_t>> pl{create_loss<network_precision_t>(config["loss"])};
+			std::shared_ptr<Optimizer<network_precision_t>> po{create_optimizer<network_precision_t>(config["optimizer"])};
+			Trainer<float, network_precision_t, network_precision_t> pt(pnet, po, pl, 1337, 0.05f);
+			EXPECT(pt.perturbation_sigma() == 0.05f);
+			float p0 = 0, p1 = 0;
+			for (int i = 0; i < 100; ++i) {
+				auto ctx = pt.training_step(stream, batch, target);
+				if (i == 0) p0 = pt.loss(stream, *ctx);
+				if (i == 99) p1 = pt.loss(stream, *ctx);
+			}
+			std::printf("perturbed training (sigma 0.05): loss %g -> %g\n", p0, p1);
+			EXPECT(std::isfinite(p1) && p1 < 0.7f * p0);
+			// the context keeps the unperturbed output: it equals inference on the same parameters
+			auto fc = pt.forward(stream, 128.0f, probe, probe_out);
+			GPUMatrix<float> inf(3, 4096);
+			pnet->inference(stream, probe, inf);
+			HIP_CHECK_THROW(hipStreamSynchronize(stream));
+			std::vector<__half> o16(16 * 4096);
+			HIP_CHECK_THROW(hipMemcpy(o16.data(), fc->output.data(), o16.size() * 2, hipMemcpyDeviceToHost));
+			const std::vector<float> hi = inf.to_cpu_vector();
+			int diff = 0;
+			for (uint32_t i = 0; i < 4096; ++i)
+				for (uint32_t k = 0; k < 3; ++k) diff += (float)o16[(size_t)i * 16 + k] != hi[(size_t)i * 3 + k];
+			EXPECT(diff == 0);
+		}
+
 		// Trainer over any DifferentiableObject (trainer.h:50): a Network alone from create_network
 		// (network.h:141-158), fp16 inputs (Trainer<__half, __half, __half>), and an Encoding alone refused
 		{
