@@ -288,6 +288,89 @@ __device__ __forceinline__ h2 encode_level_f2_inrange(const uint32_t* __restrict
 	return r;
 }
 
+// Lane-pair gathers (r04). The vector L1 costs one tag lookup per distinct cache line of an
+// instruction (tools/gather_bench.hip, profiles/r04_gather_bench.json: 64 random lines per
+// instruction take twice as long as 32 lines shared by lane pairs, whichever lanes share). A
+// point's two x-neighbour corners sit in one line (CoherentPrime's x term is x * 1; dense levels
+// are x-contiguous), so lanes L and L^1 fetch them in the same instruction: per level, the pair
+// gathers point A (the even lane's sample) then point B (the odd lane's), each lane the corners of
+// its own x parity `par`, then swaps half of the values (DPP quad_perm [1,0,3,2]) so each lane holds
+// all 2^D corners of its own point and runs the same fp16 FMA chain in the same corner order as
+// encode_level_f2_inrange -- bit-identical, with half the L1 line work.
+// xA / xB: the positions of the even / odd lane's sample (the lane's own is xB if par, else xA).
+// The whole wave must be active (the callers' in-range branch is wave-uniform).
+__device__ __forceinline__ uint32_t dpp_swap_pair(uint32_t v) {
+	return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+}
+__device__ __forceinline__ float dpp_swap_pair(float v) { return __builtin_bit_cast(float, dpp_swap_pair(__builtin_bit_cast(uint32_t, v))); }
+
+template <uint32_t D, HashType H>
+__device__ __forceinline__ h2 encode_level_f2_pair(const uint32_t* __restrict__ table_u32, const LevelConsts<D>& lc, const float* xA,
+                                                   const float* xB, uint32_t par) {
+	constexpr uint32_t NC = 1u << D, NR = NC / 2;
+	const uint32_t m = lc.m, hmask = lc.hmask, obytes = lc.obytes;
+	float posA[D], posB[D];
+	uint32_t vA[NR], vB[NR];
+	// the corners with x bit = par of one point: rows r = corner >> 1
+	auto gather_rows = [&](const float* x, float (&pos)[D], uint32_t (&v)[NR]) {
+		uint32_t pg[D];
+#pragma unroll
+		for (uint32_t d = 0; d < D; ++d) pos_fract(x[d], lc.scale, Interp::Linear, pos[d], pg[d]);
+		uint32_t th[D][2], td[D][2];
+		th[0][0] = th[0][1] = (pg[0] + par) * hash_prime<H>(0);
+		td[0][0] = td[0][1] = (pg[0] + par) * lc.sd[0];
+#pragma unroll
+		for (uint32_t d = 1; d < D; ++d) {
+			th[d][0] = pg[d] * hash_prime<H>(d);
+			th[d][1] = th[d][0] + hash_prime<H>(d);
+			td[d][0] = pg[d] * lc.sd[d];
+			td[d][1] = td[d][0] + lc.sd[d];
+		}
+#pragma unroll
+		for (uint32_t r = 0; r < NR; ++r) {
+			uint32_t h = th[0][0], dn = td[0][0];
+#pragma unroll
+			for (uint32_t d = 1; d < D; ++d) {
+				const uint32_t b = (r >> (d - 1)) & 1u;
+				h ^= th[d][b];
+				dn += td[d][b];
+			}
+			const uint32_t dm = __builtin_elementwise_min(dn, dn - lc.size);  // dn % size for dn < 2 size
+			const uint32_t idx = ((h & hmask) & m) | (dm & ~m);
+			v[r] = *(const uint32_t*)((const char*)table_u32 + (obytes + (idx << 2)));
+		}
+	};
+	gather_rows(xA, posA, vA);
+	gather_rows(xB, posB, vB);
+	uint32_t v[NC];
+#pragma unroll
+	for (uint32_t r = 0; r < NR; ++r) {
+		const uint32_t recv = dpp_swap_pair(par ? vA[r] : vB[r]);  // the partner's corners of my point
+		v[2 * r] = par ? recv : vA[r];
+		v[2 * r + 1] = par ? vB[r] : recv;
+	}
+	_Float16 w16[NC];
+	float wf[NC];
+#pragma unroll
+	for (uint32_t c = 0; c < NC; ++c) {
+		float w = 1.0f;
+#pragma unroll
+		for (uint32_t d = 0; d < D; ++d) {
+			const float p = par ? posB[d] : posA[d];
+			w *= ((c >> d) & 1u) ? p : 1.0f - p;
+		}
+		wf[c] = w;  // as encode_level_f2
+	}
+	f16_rn_pairs(wf, w16);
+	h2 res = {(_Float16)0.0f, (_Float16)0.0f};
+#pragma unroll
+	for (uint32_t c = 0; c < NC; ++c) {
+		h2 wv = {w16[c], w16[c]};
+		res = pk_fma_f16(wv, __builtin_bit_cast(h2, v[c]), res);
+	}
+	return res;
+}
+
 template <uint32_t D, HashType H>
 __device__ __forceinline__ h2 encode_level_f2_inrange(const uint32_t* __restrict__ table_u32, const LevelInfo& li, bool hash_grid,
                                                       const float* x) {

@@ -232,6 +232,12 @@ struct FusedLayout {
 // limit). 8 waves = one workgroup per CU halves the network-gradient partial slabs (256 x 28 KB for
 // config_hash instead of 512) but measured slower: fused kernel 66.6 -> 68.7 us, step 7,425 ->
 // 7,363 steps/s (the 8-wave slab reduction at the end is longer than the traffic it saves).
+// Lane-pair grid gathers in the fused kernels' in-range encode (grid_device.h encode_level_f2_pair);
+// 0 builds the one-lane-per-point gathers (A/B builds).
+#ifndef TCNN_PAIR_GATHER
+#define TCNN_PAIR_GATHER 1
+#endif
+
 #ifndef TCNN_FUSED_WAVES
 #define TCNN_FUSED_WAVES 4
 #endif
@@ -722,6 +728,20 @@ __global__ __launch_bounds__(64 * FUSED_WAVES, 8 / FUSED_WAVES) void k_fused_tra
 		// next slice's positions one slice ahead (no change)
 		if constexpr (ENC_MEM) {
 		} else if (a.inrange_index && __builtin_amdgcn_ballot_w64(!inr) == 0) {
+#if TCNN_PAIR_GATHER
+			// lane pairs (c, c^1) share their levels: gather both samples' x-neighbour corners in one
+			// instruction each (encode_level_f2_pair)
+			const uint32_t par = (uint32_t)lane & 1u;
+			float xA[2][D], xB[2][D];
+#pragma unroll
+			for (int tau = 0; tau < 2; ++tau)
+#pragma unroll
+				for (uint32_t d = 0; d < D; ++d) {
+					const float o = dpp_swap_pair(xs[tau][d]);
+					xA[tau][d] = par ? o : xs[tau][d];
+					xB[tau][d] = par ? xs[tau][d] : o;
+				}
+#endif
 			// level constants once per level, shared by the lane's two samples
 #pragma unroll
 			for (int s = 0; s < KI; ++s)
@@ -731,7 +751,11 @@ __global__ __launch_bounds__(64 * FUSED_WAVES, 8 / FUSED_WAVES) void k_fused_tra
 					const LevelConsts<D> lc = level_consts<D>(sLvl[level], hash_grid);
 #pragma unroll
 					for (int tau = 0; tau < 2; ++tau) {
+#if TCNN_PAIR_GATHER
+						const h2 e = encode_level_f2_pair<D, H>(a.table, lc, xA[tau], xB[tau], par);
+#else
 						const h2 e = encode_level_f2_inrange<D, H>(a.table, lc, xs[tau]);
+#endif
 						xt[tau][2 * s + (pp >> 1)][2 * (pp & 1) + 0] = e[0];
 						xt[tau][2 * s + (pp >> 1)][2 * (pp & 1) + 1] = e[1];
 					}
@@ -882,11 +906,25 @@ __global__ __launch_bounds__(256, 4) void k_fused_fwd_grid(const FusedFwdArgs a)
 		// xt[u][r] = feature 16 u + 4 q + r = feature (r & 1) of level 8 u + 2 q + (r >> 1)
 		h4 xt[NTI];
 		if (a.inrange_index && __builtin_amdgcn_ballot_w64(!inr) == 0) {
+#if TCNN_PAIR_GATHER
+			const uint32_t par = (uint32_t)lane & 1u;  // lane pairs (c, c^1) share their levels
+			float xA[D], xB[D];
+#pragma unroll
+			for (uint32_t d = 0; d < D; ++d) {
+				const float o = dpp_swap_pair(xs[d]);
+				xA[d] = par ? o : xs[d];
+				xB[d] = par ? xs[d] : o;
+			}
+#endif
 #pragma unroll
 			for (int u = 0; u < NTI; ++u)
 #pragma unroll
 				for (int r2 = 0; r2 < 2; ++r2) {
+#if TCNN_PAIR_GATHER
+					const h2 e = encode_level_f2_pair<D, H>(a.table, level_consts<D>(sLvl[8 * u + 2 * q + r2], hash_grid), xA, xB, par);
+#else
 					const h2 e = encode_level_f2_inrange<D, H>(a.table, level_consts<D>(sLvl[8 * u + 2 * q + r2], hash_grid), xs);
+#endif
 					xt[u][2 * r2] = e[0];
 					xt[u][2 * r2 + 1] = e[1];
 				}
