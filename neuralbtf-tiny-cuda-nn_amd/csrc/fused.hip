@@ -197,13 +197,13 @@ void launch_mlp_infer(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, int 
 
 template <int W, int IN, int NH, uint32_t D, HashType H, Act A>
 static void launch_fused_fwd_t(hipStream_t st, const FusedFwdArgs& a) {
-	constexpr size_t bytes = (((size_t)FusedLayout<W, IN, NH>::oStage * 2 + 15) & ~(size_t)15) + (size_t)(IN / 2) * sizeof(LevelInfo);
+	constexpr size_t bytes = FwdLayout<W, IN, NH>::BYTES;
 	static uint64_t done = 0;
 	set_dyn_lds((const void*)k_fused_fwd_grid<W, IN, NH, D, H, A>, (int)bytes, done);
-	uint32_t nb = div_round_up(a.B, 64u);
-	const uint32_t cap = 8 * device_cu_count();  // 54 VGPRs, 17 KB of LDS: 8 workgroups per CU
+	uint32_t nb = div_round_up(a.B, 16u * FWD_WAVES);
+	const uint32_t cap = 3 * device_cu_count();  // 41 KB of LDS per 8-wave workgroup: 3 per CU
 	if (nb > cap) nb = cap;
-	hipLaunchKernelGGL((k_fused_fwd_grid<W, IN, NH, D, H, A>), dim3(nb), dim3(256), bytes, st, a);
+	hipLaunchKernelGGL((k_fused_fwd_grid<W, IN, NH, D, H, A>), dim3(nb), dim3(64 * FWD_WAVES), bytes, st, a);
 	TCNN_HIP_CHECK(hipGetLastError());
 }
 

@@ -121,13 +121,23 @@ __global__ __launch_bounds__(256) void k_grid_fwd_aos_f2(uint32_t B, const float
 	const bool fast = o.inrange_index && !o.active && __builtin_amdgcn_ballot_w64(!inr) == 0;
 	if (fast) {
 		// four levels per wave at a time with all their gathers in flight together (a level past L
-		// encodes level 0 into a discarded register, so the body has no branch to split the batch)
+		// encodes level 0 into a discarded register, so the body has no branch to split the batch);
+		// lanes L, L^1 (neighbouring points, same level) fetch each other's x-neighbour corners in one
+		// instruction (encode_level_f2_pair)
+		const uint32_t par = lane & 1u;
+		float xA[D], xB[D];
+#pragma unroll
+		for (uint32_t d = 0; d < D; ++d) {
+			const float ox = dpp_swap_pair(x[d]);
+			xA[d] = par ? ox : x[d];
+			xB[d] = par ? x[d] : ox;
+		}
 		for (uint32_t l0 = 0; l0 < L; l0 += 16) {
 			h2 r[4];
 #pragma unroll
 			for (uint32_t k = 0; k < 4; ++k) {
 				const uint32_t level = l0 + wave + 4 * k;
-				r[k] = encode_level_f2_inrange<D, H>(table, levels[level < L ? level : 0], hash_grid != 0, x);
+				r[k] = encode_level_f2_pair<D, H>(table, level_consts<D>(levels[level < L ? level : 0], hash_grid != 0), xA, xB, par);
 			}
 #pragma unroll
 			for (uint32_t k = 0; k < 4; ++k) {
@@ -178,10 +188,19 @@ __global__ __launch_bounds__(256) void k_grid_fwd_soa_f2(uint32_t B, const float
 	const uint32_t l0 = blockIdx.y * 4;
 	h2 r[4];
 	if (fast) {
+		// lanes L, L^1 (neighbouring points) share their gathers' lines (encode_level_f2_pair)
+		const uint32_t par = threadIdx.x & 1u;
+		float xA[D], xB[D];
+#pragma unroll
+		for (uint32_t d = 0; d < D; ++d) {
+			const float ox = dpp_swap_pair(x[d]);
+			xA[d] = par ? ox : x[d];
+			xB[d] = par ? x[d] : ox;
+		}
 #pragma unroll
 		for (uint32_t k = 0; k < 4; ++k) {
 			const uint32_t level = l0 + k;
-			r[k] = encode_level_f2_inrange<D, H>(table, levels[level < L ? level : 0], hash_grid != 0, x);
+			r[k] = encode_level_f2_pair<D, H>(table, level_consts<D>(levels[level < L ? level : 0], hash_grid != 0), xA, xB, par);
 		}
 	} else {
 #pragma unroll

@@ -299,6 +299,36 @@ __device__ __forceinline__ h2 encode_level_f2_inrange(const uint32_t* __restrict
 // encode_level_f2_inrange -- bit-identical, with half the L1 line work.
 // xA / xB: the positions of the even / odd lane's sample (the lane's own is xB if par, else xA).
 // The whole wave must be active (the callers' in-range branch is wave-uniform).
+// Coarse dense levels staged in LDS (r04): levels 0..k-1 of the table prefix, while they are dense
+// (not hashed) and their entries fit `budget_bytes`; the fused kernels then read those levels
+// through a per-lane table pointer into LDS (a flat load: lanes of one instruction may mix LDS and
+// global levels). Every sample touches every level, so the small dense tables -- evicted from the
+// 32 KB L1 by the hashed levels' stream -- otherwise cost two L2 requests per sample and level.
+// Returns the staged entry count (0: none); `k` = the number of staged levels.
+template <uint32_t D>
+__device__ __forceinline__ uint32_t stage_dense_levels(uint32_t* __restrict__ sT, const uint32_t* __restrict__ table, const LevelInfo* sLvl,
+                                                       uint32_t n_levels, bool hash_grid, uint32_t budget_bytes, int tid, int nthreads,
+                                                       uint32_t& k) {
+	uint32_t entries = 0;
+	k = 0;
+	for (uint32_t l = 0; l < n_levels; ++l) {
+		const LevelInfo li = sLvl[l];
+		uint64_t full = 1;
+		for (uint32_t d = 0; d < D; ++d) full *= li.res;
+		const bool dense = !hash_grid || full <= li.size;
+		if (!dense || li.offset != entries || (uint64_t)(li.offset + li.size) * 4 > budget_bytes) break;
+		entries = li.offset + li.size;
+		k = l + 1;
+	}
+	if (((uintptr_t)table & 15) == 0) {
+		for (uint32_t j = tid; j < entries / 4; j += nthreads) ((uint4*)sT)[j] = ((const uint4*)table)[j];
+		for (uint32_t j = entries / 4 * 4 + tid; j < entries; j += nthreads) sT[j] = table[j];
+	} else {
+		for (uint32_t j = tid; j < entries; j += nthreads) sT[j] = table[j];
+	}
+	return entries;
+}
+
 __device__ __forceinline__ uint32_t dpp_swap_pair(uint32_t v) {
 	return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
 }

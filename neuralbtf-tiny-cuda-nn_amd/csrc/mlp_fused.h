@@ -237,6 +237,12 @@ struct FusedLayout {
 #ifndef TCNN_PAIR_GATHER
 #define TCNN_PAIR_GATHER 1
 #endif
+// Coarse dense grid levels staged in LDS by the fused forward (grid_device.h stage_dense_levels);
+// needs TCNN_PAIR_GATHER. 0 for A/B builds. (Measured in the training kernel too: 49.3 -> 50.0 us,
+// not kept there; the forward gains 43.0 -> 41.9 us, profiles/r04_lds_levels_ab.txt.)
+#ifndef TCNN_LDS_LEVELS
+#define TCNN_LDS_LEVELS 1
+#endif
 
 #ifndef TCNN_FUSED_WAVES
 #define TCNN_FUSED_WAVES 4
@@ -874,19 +880,40 @@ struct FusedFwdArgs {
 	_Float16* out;  // [B][16]
 };
 
+// 8 waves per workgroup share one LDS weight image and one copy of the coarse dense levels
+// (stage_dense_levels): 3 workgroups (24 waves) per CU.
+constexpr int FWD_WAVES = 8;
+constexpr int FWD_TBL_BUDGET = 24 * 1024;
+template <int W, int IN, int NH>
+struct FwdLayout {
+	static constexpr int LVL_BYTES = (FusedLayout<W, IN, NH>::oStage * 2 + 15) & ~15;
+	static constexpr int TBL_BYTES = LVL_BYTES + (int)MAX_LEVELS * 16;
+	static constexpr int BYTES = TBL_BYTES + FWD_TBL_BUDGET;
+};
+
 template <int W, int IN, int NH, uint32_t D, HashType H, Act ACT>
-__global__ __launch_bounds__(256, 4) void k_fused_fwd_grid(const FusedFwdArgs a) {
+__global__ __launch_bounds__(64 * FWD_WAVES, 3) void k_fused_fwd_grid(const FusedFwdArgs a) {
 	using L = FusedLayout<W, IN, NH>;
 	constexpr int NT = L::NT, KW = L::KW, NTI = L::NTI, KI = L::KI;
 	constexpr int NLVL = IN / 2;
 	extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
 	const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 	const int c = lane & 15, q = lane >> 4;
-	if (a.wimage) copy_image_to_lds(smem, a.wimage, L::oStage, tid, 256);
-	else load_weights_lds_v<W, IN, NH>(smem, a.params, tid, 256);
-	LevelInfo* sLvl = (LevelInfo*)((char*)smem + ((L::oStage * 2 + 15) & ~15));
-	for (int l = tid; l < NLVL; l += 256) sLvl[l] = a.levels[l];
+	constexpr int NTHR = 64 * FWD_WAVES;
+	using FL = FwdLayout<W, IN, NH>;
+	if (a.wimage) copy_image_to_lds(smem, a.wimage, L::oStage, tid, NTHR);
+	else load_weights_lds_v<W, IN, NH>(smem, a.params, tid, NTHR);
+	LevelInfo* sLvl = (LevelInfo*)((char*)smem + FL::LVL_BYTES);
+	for (int l = tid; l < NLVL; l += NTHR) sLvl[l] = a.levels[l];
 	__syncthreads();
+	uint32_t k_lds = 0;
+	const uint32_t* sT = (const uint32_t*)((char*)smem + FL::TBL_BYTES);
+	if constexpr (TCNN_LDS_LEVELS) {
+		if (a.inrange_index) {
+			stage_dense_levels<D>((uint32_t*)sT, a.table, sLvl, NLVL, a.hash_grid != 0, FWD_TBL_BUDGET, tid, NTHR, k_lds);
+			__syncthreads();
+		}
+	}
 	const _Float16* sW0 = smem + L::oW0;
 	const _Float16* sWh = smem + L::oWh;
 	const _Float16* sWo = smem + L::oWo;
@@ -894,7 +921,7 @@ __global__ __launch_bounds__(256, 4) void k_fused_fwd_grid(const FusedFwdArgs a)
 	const Interp interp = (Interp)a.interp;
 	const f4 fz = {0.0f, 0.0f, 0.0f, 0.0f};
 	const uint32_t B = a.B, n_chunks = B / 16;
-	for (uint32_t chunk = blockIdx.x * 4 + wave; chunk < n_chunks; chunk += gridDim.x * 4) {
+	for (uint32_t chunk = blockIdx.x * FWD_WAVES + wave; chunk < n_chunks; chunk += gridDim.x * FWD_WAVES) {
 		const uint32_t i = chunk * 16 + c;
 		float xs[D];
 		bool inr = true;
@@ -921,7 +948,8 @@ __global__ __launch_bounds__(256, 4) void k_fused_fwd_grid(const FusedFwdArgs a)
 #pragma unroll
 				for (int r2 = 0; r2 < 2; ++r2) {
 #if TCNN_PAIR_GATHER
-					const h2 e = encode_level_f2_pair<D, H>(a.table, level_consts<D>(sLvl[8 * u + 2 * q + r2], hash_grid), xA, xB, par);
+					const uint32_t level = 8 * u + 2 * q + r2;
+					const h2 e = encode_level_f2_pair<D, H>(level < k_lds ? sT : a.table, level_consts<D>(sLvl[level], hash_grid), xA, xB, par);
 #else
 					const h2 e = encode_level_f2_inrange<D, H>(a.table, level_consts<D>(sLvl[8 * u + 2 * q + r2], hash_grid), xs);
 #endif
