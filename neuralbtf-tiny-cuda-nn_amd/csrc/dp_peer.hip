@@ -46,7 +46,10 @@ constexpr uint32_t PEER_MAGIC = 0x50454552u;  // "PEER"
 constexpr int PEER_MAX_RANKS = 64;  // one wave polls the ranks' counters
 constexpr int PEER_NBUF = 4;                  // exported: gradient sums, fp16 shard mirror, state staging, counters
 enum PeerBuf { PB_G32 = 0, PB_W16, PB_STATE, PB_FLAGS };
-enum PeerSlot { SLOT_GRAD = 0, SLOT_WEIGHTS = 1, SLOT_GATHER = 2, SLOT_DETACH = 3 };
+enum PeerSlot { SLOT_GRAD = 0, SLOT_WEIGHTS = 1, SLOT_GATHER = 2, SLOT_DETACH = 3, SLOT_PROBE = 4 };
+constexpr int PROBE_WORD = 16;  // the attach probe's token in each rank's counter page
+
+__host__ __device__ inline uint32_t probe_token(int rank) { return PEER_MAGIC ^ (0x9e3779b9u * (uint32_t)(rank + 1)); }
 enum PeerCtr { CTR_STEP = 0, CTR_SYNC = 1 };
 
 struct PeerBlob {
@@ -88,6 +91,18 @@ __global__ void k_peer_wait(const PeerFlags fl, int nranks, int slot, uint32_t* 
 		}
 		__builtin_amdgcn_s_sleep(1);
 	}
+}
+
+// attach probe: this rank's token into its own counter page; after a barrier every rank reads every
+// rank's token through the peer mappings (a mapping that does not reach the peer's memory shows up
+// here, once, instead of as a step that never completes)
+__global__ void k_peer_token(uint32_t* __restrict__ my_flags, uint32_t token) {
+	if (threadIdx.x == 0) __hip_atomic_store(my_flags + PROBE_WORD, token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__global__ void k_peer_probe(const PeerFlags fl, int nranks, int* __restrict__ err) {
+	const int p = threadIdx.x;
+	if (p < nranks && load_sys(fl.f[p] + PROBE_WORD) != probe_token(p))
+		__hip_atomic_store(err, 1000 + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Adam on this rank's shard [a.begin, a.n) with the gradient summed over the ranks' gradient sums in
@@ -171,8 +186,12 @@ struct TrainerHost::PeerDp {
 	template <typename T>
 	T* const* table(int b) const { return (T* const*)(ptrs.as<void*>() + (size_t)b * nranks); }
 	void check() const {
-		if (err_host && *(volatile int*)err_host)
-			throw std::runtime_error("data-parallel peer exchange: rank " + std::to_string(*(volatile int*)err_host - 1) +
+		const int e = err_host ? *(volatile int*)err_host : 0;
+		if (e >= 1000)
+			throw std::runtime_error("data-parallel peer exchange: rank " + std::to_string(e - 1000) +
+			                         "'s memory is not readable through its mapping (attach probe)");
+		if (e)
+			throw std::runtime_error("data-parallel peer exchange: rank " + std::to_string(e - 1) +
 			                         " did not arrive within the timeout (a rank stopped, or the ranks' steps diverged)");
 	}
 };
@@ -262,6 +281,15 @@ void TrainerHost::dp_peer_attach(const void* blobs) {
 	for (int p = 0; p < N; ++p) pd.flags_arg.f[p] = (uint32_t*)host[(size_t)PB_FLAGS * N + p];
 	pd.ptrs.reserve(host.size() * sizeof(void*));
 	TCNN_HIP_CHECK(hipMemcpy(pd.ptrs.p, host.data(), host.size() * sizeof(void*), hipMemcpyHostToDevice));
+	// probe (collective): every rank's token readable through every mapping, checked once here so a
+	// broken mapping fails the attach (and the caller falls back) instead of a step
+	hipLaunchKernelGGL(k_peer_token, dim3(1), dim3(64), 0, nullptr, (uint32_t*)pd.x[PB_FLAGS], probe_token(pd.rank));
+	TCNN_HIP_CHECK(hipGetLastError());
+	peer_wait(nullptr, CTR_SYNC, SLOT_PROBE, 1);
+	hipLaunchKernelGGL(k_peer_probe, dim3(1), dim3(64), 0, nullptr, pd.flags_arg, N, pd.err_dev);
+	TCNN_HIP_CHECK(hipGetLastError());
+	TCNN_HIP_CHECK(hipDeviceSynchronize());
+	pd.check();
 	pd.attached = true;
 	peer_attached = true;
 	dp_sharded = true;
