@@ -1,5 +1,5 @@
 """The engine's peer-memory data-parallel exchange (csrc/dp_peer.hip, tinycudann.parallel.PeerExchange)
-with two ranks on one GPU (IPC within a device): every rank exports IPC handles of its buffers, the
+with two (and four) ranks on one GPU (IPC within a device): every rank exports IPC handles of its buffers, the
 blobs are all-gathered over gloo, and each training_step sums the ranks' gradients for its shard
 straight from the other rank's memory, runs Adam on the shard and copies the other shard's fp16
 parameters. For two ranks the result must equal the replicated all-reduce schedule bit for bit
@@ -65,9 +65,13 @@ def _worker(rank, world, port, B, q):
     dist.destroy_process_group()
 
 
-def test_two_rank_peer_exchange_equals_allreduce():
+@pytest.mark.parametrize("world", [2, 4])
+def test_peer_exchange_equals_allreduce(world):
+    """2 ranks: bit-identical to the all-reduce. 4 ranks (1024 points each, padded shards of 178,888
+    parameters): the peer sum runs in rank order g0+g1+g2+g3 while gloo's ring sums in its own order,
+    so the comparison is within fp32 rounding; the replicas must still agree bit for bit."""
     import torch.multiprocessing as mp
-    B, world = 4096, 2
+    B = 4096
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -80,9 +84,15 @@ def test_two_rank_peer_exchange_equals_allreduce():
         assert p.exitcode == 0
     for r in res:
         _, w_ref, h_ref, snap_ref, l_ref, w_peer, h_peer, snap_peer, l_peer, finite = r
-        np.testing.assert_array_equal(w_peer, w_ref)
-        np.testing.assert_array_equal(h_peer, h_ref)
-        assert snap_peer == snap_ref
-        assert l_peer == l_ref
         assert finite
-    np.testing.assert_array_equal(res[0][5], res[1][5])  # the replicas agree
+        if world == 2:
+            np.testing.assert_array_equal(w_peer, w_ref)
+            np.testing.assert_array_equal(h_peer, h_ref)
+            assert snap_peer == snap_ref
+            assert l_peer == l_ref
+        else:
+            np.testing.assert_allclose(w_peer, w_ref, rtol=1e-3, atol=1e-6)
+            np.testing.assert_allclose(np.asarray(l_peer), np.asarray(l_ref), rtol=1e-3)
+    for r in res[1:]:  # the replicas agree
+        np.testing.assert_array_equal(res[0][5], r[5])
+        np.testing.assert_array_equal(res[0][6], r[6])
