@@ -181,6 +181,7 @@ __device__ __forceinline__ void accum_point_2d_fast(const float (&x)[2], const f
 // into dyb (GRID_BWD_PR points per thread, point i0 + threadIdx.x + p * blockDim.x in slot p) for the
 // scale pre-pass and are reused here; positions stream in batches of 8 with the next batch in flight.
 constexpr uint32_t GRID_BWD_PR = 32, GRID_BWD_PU = 8;
+static_assert(GRID_BWD_THREADS * GRID_BWD_PR == GRID_BWD_REG_POINTS, "kernels.h GRID_BWD_REG_POINTS");
 template <uint32_t D>
 __device__ __forceinline__ void load_pos_batch(const float* __restrict__ pos, uint32_t pstride, uint32_t i0, uint32_t i1, uint32_t k,
                                                float (&dst)[GRID_BWD_PU][D]) {

@@ -51,6 +51,10 @@ enum : int {
 // within a level whose work items hold nf < F features the slab is feature-group-major
 // ([F/nf][size][nf]) so every item writes one contiguous range. slab index of grid parameter p,
 // level l, entry e, feature f (f0 = f - f % nf):  pbase[l] + f0 * size[l] + e * nf[l] + (f - f0).
+// Points per chunk up to which the LDS grid backward keeps a chunk's dL/dy in registers
+// (GRID_BWD_THREADS x GRID_BWD_PR, grid_bwd_lds.h): the faster path, so large batches take more chunks.
+constexpr uint32_t GRID_BWD_REG_POINTS = 1024u * 32u;
+
 struct GridSlabMap {
 	uint32_t n_levels, log2F;
 	uint32_t pbase[MAX_LEVELS + 1];  // offset_l * F

@@ -118,6 +118,10 @@ struct GridEncodingHost {
 		const uint32_t n_cu = 256;
 		const uint32_t fit = (n_cu > reserved ? n_cu - reserved : 1u) / (uint32_t)slices.size();
 		uint32_t c = std::max(1u, fit > 2 ? fit - 1 : fit);
+		// large batches: chunks small enough for the register-resident path, over several rounds
+		// (configs[3], 2^20 points: 8 -> 32 chunks, grid backward 170 -> 99 us, step -4 %,
+		// profiles/r04_grid_bwd_chunks.txt); config_hash at 2^18 keeps its 8
+		c = std::max(c, (B + GRID_BWD_REG_POINTS - 1) / GRID_BWD_REG_POINTS);
 		if (sw.grid_bwd_chunks) c = sw.grid_bwd_chunks;  // tuning override
 		return std::max(1u, std::min(std::min(c, 32u), B / 4096));
 	}
