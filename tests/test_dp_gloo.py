@@ -216,3 +216,88 @@ def test_two_rank_exchange_schedule_and_sharding():
         np.testing.assert_array_equal(m2, w32 * np.float32(0.01))
         np.testing.assert_array_equal(steps, np.ones(41, np.int32))
         assert partial and not partial_after
+
+
+class _FakePeerLib:
+    """The peer-exchange C-ABI as PeerExchange calls it, with scripted failures per rank."""
+
+    def __init__(self, rank, fail_export=(), fail_attach=()):
+        self.rank, self.fail_export, self.fail_attach = rank, fail_export, fail_attach
+        self.calls = []
+        self.err = b""
+
+    def tcnn_dp_peer_blob_bytes(self):
+        return 16
+
+    def tcnn_trainer_dp_peer_export(self, h, world, rank, blob):
+        self.calls.append("export")
+        if rank in self.fail_export:
+            self.err = b"hipIpcGetMemHandle failed (scripted)"
+            return 1
+        return 0
+
+    def tcnn_trainer_dp_peer_attach(self, h, blobs):
+        self.calls.append("attach")
+        if self.rank in self.fail_attach:
+            self.err = b"hipIpcOpenMemHandle failed (scripted)"
+            return 1
+        return 0
+
+    def tcnn_trainer_dp_peer_abandon(self, h):
+        self.calls.append("abandon")
+        return 0
+
+    def tcnn_last_error(self):
+        return self.err
+
+
+def _peer_verdict_worker(rank, world, port, out_q):
+    import sys
+    import types
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    sys.path[:0] = [repo, os.path.join(repo, "neuralbtf-tiny-cuda-nn_amd"), here]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tinycudann import _lib as L
+    from tinycudann.parallel import PeerExchange
+    res = {}
+    for case, kw in (("ok", {}), ("export", {"fail_export": (1,)}), ("attach", {"fail_attach": (0,)})):
+        fake = _FakePeerLib(rank, **kw)
+        L.lib = lambda fake=fake: fake
+        t = types.SimpleNamespace(h=None, _dp_state_partial=True)
+        try:
+            PeerExchange(t)
+            res[case] = ("attached", fake.calls, t._dp_state_partial)
+        except RuntimeError as e:
+            res[case] = (str(e), fake.calls, t._dp_state_partial)
+    out_q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_peer_exchange_collective_verdict():
+    """PeerExchange (tinycudann/parallel.py) attaches on every rank or on none: an export failure on
+    rank 1, or an attach failure on rank 0, makes BOTH ranks raise (naming the failing rank) and drop
+    what they had (abandon), so DataParallelTrainer(peer_fallback=True) falls back on every rank
+    together; the C-ABI is scripted (CPU, gloo world 2)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_peer_verdict_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        msg, calls, partial = res[r]["ok"]
+        assert msg == "attached" and calls == ["export", "attach"] and partial is False
+        msg, calls, _ = res[r]["export"]
+        assert "rank 1" in msg and "hipIpcGetMemHandle" in msg
+        assert calls[-1] == "abandon" and "attach" not in calls  # nobody attaches when an export failed
+        msg, calls, _ = res[r]["attach"]
+        assert "rank 0" in msg and "hipIpcOpenMemHandle" in msg and calls[-1] == "abandon"
