@@ -72,7 +72,10 @@ public:
 		CHECK_THROW(input.n() % BATCH_SIZE_GRANULARITY == 0);
 		CHECK_THROW(input.n() == output.n());
 		CHECK_THROW(input.layout() == CM && input.is_contiguous() && output.layout() == CM && output.is_contiguous());
-		if (!m_trainer) throw std::runtime_error{name() + "::inference: no parameters (the object is not owned by a Trainer)"};
+		if (!m_trainer) {
+			if (inference_standalone(stream, input, output)) return;
+			throw std::runtime_error{name() + "::inference: no parameters (the object is not owned by a Trainer)"};
+		}
 		const float* in = detail::engine_input(stream, input, m_input_scratch);
 		detail::check_rc(tcnn_trainer_inference(m_trainer, stream, input.n(), in, output.data()));
 	}
@@ -81,6 +84,8 @@ public:
 	}
 
 protected:
+	// an object that holds its own parameters (Encoding) runs inference without a Trainer
+	virtual bool inference_standalone(hipStream_t, const GPUMatrixDynamic<T>&, GPUMatrixDynamic<float>&) { return false; }
 	tcnn_trainer* m_trainer = nullptr;
 	GPUMemory<float> m_input_scratch;
 };

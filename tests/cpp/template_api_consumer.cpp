@@ -437,6 +437,20 @@ int main(int argc, char** argv) {
 
 			std::shared_ptr<Encoding<network_precision_t>> enc{create_encoding<network_precision_t>(2, config["encoding"])};
 			EXPECT(enc->input_width() == 2 && enc->output_width() == 32);
+			// an Encoding holds its own (initialised) parameters: inference runs without a Trainer
+			{
+				GPUMatrix<float> eo(32, 4096);
+				enc->inference(stream, probe, eo);
+				HIP_CHECK_THROW(hipStreamSynchronize(stream));
+				const std::vector<float> ev = eo.to_cpu_vector();
+				float emax = 0.0f;
+				bool efin = true;
+				for (float v : ev) {
+					efin = efin && std::isfinite(v);
+					emax = std::fmax(emax, std::fabs(v));
+				}
+				EXPECT(efin && emax > 0.0f && emax <= 2e-4f);  // grid init: uniform in +-1e-4, weights sum to 1
+			}
 			bool refused = false;
 			try {
 				Trainer<float, network_precision_t, network_precision_t> bad(enc, o, l);
