@@ -185,12 +185,16 @@ int tcnn_trainer_optimizer_step_range(tcnn_trainer* t, void* stream, uint64_t be
  * from the peers' memory, runs Adam on that shard (gradient scale 1/N) and copies the other shards'
  * updated fp16 parameters -- one C-ABI call per step, no host synchronisation. The optimizer state
  * is sharded like the RCCL sharded schedule (tcnn_trainer_dp_gather_state completes it). Detach is
- * collective (every rank calls it). A rank that does not arrive within 10 s raises an error at the
- * next call instead of hanging the GPU. */
+ * collective (every rank calls it); a trainer attached to peers must be detached by every rank before
+ * it is destroyed. A rank that does not arrive within the timeout (tcnn_trainer_dp_peer_set_timeout;
+ * default TCNN_PEER_TIMEOUT_S or 300 s) raises an error at the next call instead of hanging the GPU,
+ * and the step that timed out leaves the parameters untouched. */
 uint64_t tcnn_dp_peer_blob_bytes(void);
 int tcnn_trainer_dp_peer_export(tcnn_trainer* t, int nranks, int rank, void* blob);
 int tcnn_trainer_dp_peer_attach(tcnn_trainer* t, const void* blobs);
 int tcnn_trainer_dp_peer_detach(tcnn_trainer* t);
+/* seconds a peer wait polls before it gives up (also changes the current attachment's waits) */
+int tcnn_trainer_dp_peer_set_timeout(tcnn_trainer* t, double seconds);
 /* Drop this rank's export / attachment without the collective barrier -- only before any exchange
  * step ran, e.g. when another rank failed to attach (the caller then falls back to another exchange). */
 int tcnn_trainer_dp_peer_abandon(tcnn_trainer* t);

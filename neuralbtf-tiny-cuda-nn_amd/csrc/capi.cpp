@@ -598,6 +598,9 @@ int tcnn_trainer_dp_peer_attach(tcnn_trainer* t, const void* blobs) {
 int tcnn_trainer_dp_peer_detach(tcnn_trainer* t) {
 	return guard([&] { t->t->dp_peer_detach(); });
 }
+int tcnn_trainer_dp_peer_set_timeout(tcnn_trainer* t, double seconds) {
+	return guard([&] { t->t->dp_peer_set_timeout(seconds); });
+}
 int tcnn_trainer_dp_peer_abandon(tcnn_trainer* t) {
 	return guard([&] { t->t->dp_peer_abandon(); });
 }
@@ -630,7 +633,7 @@ int tcnn_trainer_optimizer_state(tcnn_trainer* t, float** m1, float** m2, uint32
 int tcnn_trainer_set_gradient_scale(tcnn_trainer* t, float s) {
 	TrainerHost& h = *t->t;
 	h.grad_scale_user = s;
-	h.grad_scale = s * (h.dp ? 1.0f / (float)h.dp->nranks : 1.0f);
+	h.grad_scale = s / (float)h.dp_nranks();  // the RCCL communicator's or the peer exchange's N
 	return 0;
 }
 int tcnn_trainer_set_graph(tcnn_trainer* t, int on) {

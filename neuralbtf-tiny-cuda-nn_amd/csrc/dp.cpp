@@ -119,14 +119,16 @@ void TrainerHost::set_dp(DpComm* c, bool sharded) {
 	// step's Adam would run on state that is stale outside this rank's shard and overwrite the gathered
 	// fp16 weights of the other shards. This makes set_dp collective whenever state is partial: every
 	// rank of the old communicator calls it (as every rank calls the sharded step).
+	// any call while a peer exchange is attached (attach or detach) would reset its scale and shard
+	// state under it: refused, detach the peer exchange first
+	TCNN_CHECK(!peer_attached, "set_dp: the trainer is attached to a peer exchange (detach it first)");
 	if (dp && dp_sharded && dp_state_partial) dp_gather_state(nullptr);
-	TCNN_CHECK(!(c && peer_attached), "set_dp: the trainer is attached to a peer exchange (detach it first)");
 	TCNN_HIP_CHECK(hipDeviceSynchronize());
 	dp = c;
 	dp_sharded = c && sharded;
 	dp_state_partial = false;
 	// Adam reads the SUM over ranks: the caller's own scale (tcnn_trainer_set_gradient_scale) times 1/N
-	grad_scale = grad_scale_user * (c ? 1.0f / (float)c->nranks : 1.0f);
+	grad_scale = grad_scale_user / (float)dp_nranks();
 	if (graph) set_graph(use_graph);  // drop captured graphs (their keys do not hold the exchange)
 	if (!dp_sharded) return;
 	// shard s owns parameters [s per, (s + 1) per); every per-parameter buffer is padded to N per so

@@ -32,6 +32,7 @@
 // rank never occupies the CUs another rank on the same GPU needs to make progress (the 2-process
 // test shares one GPU). Every wait gives up after a timeout, raising an error flag in host-mapped
 // memory that the next step (or gather) turns into an exception -- a dead peer cannot hang the GPU.
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -50,7 +51,7 @@ enum PeerSlot { SLOT_GRAD = 0, SLOT_WEIGHTS = 1, SLOT_GATHER = 2, SLOT_DETACH = 
 constexpr int PROBE_WORD = 16;  // the attach probe's token in each rank's counter page
 
 __host__ __device__ inline uint32_t probe_token(int rank) { return PEER_MAGIC ^ (0x9e3779b9u * (uint32_t)(rank + 1)); }
-enum PeerCtr { CTR_STEP = 0, CTR_SYNC = 1 };
+enum PeerCtr { CTR_STEP = 0, CTR_SYNC = 1, CTR_ERR = 2 };
 
 struct PeerBlob {
 	uint32_t magic, nranks, rank, device;
@@ -69,9 +70,12 @@ __device__ __forceinline__ uint32_t load_sys(const uint32_t* p) {
 struct PeerFlags {  // the ranks' counter arrays, by value (no dependent pointer load before the polls)
 	uint32_t* f[PEER_MAX_RANKS];
 };
+// ctr[CTR_ERR] is the device-side copy of the error flag: the step's data kernels read it and leave
+// the parameters untouched once a wait has failed (the host-mapped *err raises at the next call)
 __global__ void k_peer_wait(const PeerFlags fl, int nranks, int slot, uint32_t* __restrict__ ctr, int c, long long timeout_ticks,
                             int* __restrict__ err, uint32_t* __restrict__ my_flags, int bump) {
 	if (threadIdx.x >= 64) return;
+	if (ctr[CTR_ERR]) return;  // an earlier wait failed: no signal, no wait (the step is abandoned)
 	uint32_t target = ctr[c];
 	if (my_flags && threadIdx.x == 0) {
 		if (bump) ctr[c] = target + 1u;
@@ -86,7 +90,10 @@ __global__ void k_peer_wait(const PeerFlags fl, int nranks, int slot, uint32_t* 
 		const uint64_t pending = __builtin_amdgcn_ballot_w64(!ok);
 		if (pending == 0) return;
 		if (wall_clock64() - t0 > timeout_ticks) {
-			if (p == (int)__builtin_ctzll(pending)) __hip_atomic_store(err, 1 + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+			if (p == (int)__builtin_ctzll(pending)) {
+				__hip_atomic_store(err, 1 + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+				ctr[CTR_ERR] = 1u + (uint32_t)p;
+			}
 			return;
 		}
 		__builtin_amdgcn_s_sleep(1);
@@ -99,17 +106,20 @@ __global__ void k_peer_wait(const PeerFlags fl, int nranks, int slot, uint32_t* 
 __global__ void k_peer_token(uint32_t* __restrict__ my_flags, uint32_t token) {
 	if (threadIdx.x == 0) __hip_atomic_store(my_flags + PROBE_WORD, token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__global__ void k_peer_probe(const PeerFlags fl, int nranks, int* __restrict__ err) {
+__global__ void k_peer_probe(const PeerFlags fl, int nranks, int* __restrict__ err, uint32_t* __restrict__ ctr) {
 	const int p = threadIdx.x;
-	if (p < nranks && load_sys(fl.f[p] + PROBE_WORD) != probe_token(p))
+	if (p < nranks && load_sys(fl.f[p] + PROBE_WORD) != probe_token(p)) {
 		__hip_atomic_store(err, 1000 + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+		ctr[CTR_ERR] = 1000u + (uint32_t)p;
+	}
 }
 
 // Adam on this rank's shard [a.begin, a.n) with the gradient summed over the ranks' gradient sums in
 // rank order (g_0 + g_1 + ...); the updated fp16 parameter also goes to the uncached mirror the other
 // ranks gather from
 __global__ __launch_bounds__(256) void k_peer_adam(const AdamArgs a, const AdamBuffers s, const float* const* __restrict__ gptrs,
-                                                   int nranks, _Float16* __restrict__ w16_mirror) {
+                                                   int nranks, _Float16* __restrict__ w16_mirror, const uint32_t* __restrict__ ctr) {
+	if (ctr[CTR_ERR]) return;  // a peer did not arrive: its gradient sums are not this step's
 	const uint32_t i = a.begin + blockIdx.x * blockDim.x + threadIdx.x;
 	if (i >= a.n) return;
 	float v[8];
@@ -135,8 +145,10 @@ struct PeerGatherArgs {
 	uint32_t elem_bytes[4];
 	uint32_t nranks, rank;
 	uint64_t per;  // elements per shard
+	const uint32_t* ctr;  // CTR_ERR set: the peers' mirrors are not this step's, copy nothing
 };
 __global__ __launch_bounds__(256) void k_peer_gather(const PeerGatherArgs g) {
+	if (g.ctr[CTR_ERR]) return;
 	const uint32_t b = blockIdx.y;
 	const uint64_t shard_bytes = g.per * g.elem_bytes[b];
 	const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // 16-byte unit over all ranks' shards
@@ -150,7 +162,8 @@ __global__ __launch_bounds__(256) void k_peer_gather(const PeerGatherArgs g) {
 // this rank's shard of the optimizer state into its uncached staging mirror (for the peers' gather)
 __global__ __launch_bounds__(256) void k_peer_stage(const float* __restrict__ w32, const float* __restrict__ m1, const float* __restrict__ m2,
                                                     const uint32_t* __restrict__ steps, uint32_t* __restrict__ stage, uint64_t lo,
-                                                    uint64_t cnt, uint64_t stride) {
+                                                    uint64_t cnt, uint64_t stride, const uint32_t* __restrict__ ctr) {
+	if (ctr[CTR_ERR]) return;
 	const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
 	if (k >= cnt) return;
 	const uint64_t i = lo + k;
@@ -175,9 +188,14 @@ struct TrainerHost::PeerDp {
 	int* err_host = nullptr;
 	int* err_dev = nullptr;
 	long long timeout_ticks = 0;
+	int clock_khz = 1;  // wall_clock64 rate
 	PeerFlags flags_arg{};  // the ranks' counter arrays (k_peer_wait's argument)
 	PeerDp() = default;
 	~PeerDp() {
+		// this rank's kernels may still read the peers' mappings (an asynchronous step just issued):
+		// finish them before unmapping (the collective part -- peers done reading OUR mirrors -- is
+		// dp_peer_detach's SLOT_DETACH wait)
+		(void)hipDeviceSynchronize();
 		for (void* p : opened) (void)hipIpcCloseMemHandle(p);
 		for (void* p : x)
 			if (p) (void)hipFree(p);
@@ -198,6 +216,21 @@ struct TrainerHost::PeerDp {
 
 uint64_t dp_peer_blob_bytes() { return sizeof(PeerBlob); }
 
+// the peer waits' timeout (default TCNN_PEER_TIMEOUT_S or 300 s -- long enough for rank-0-only work
+// between steps such as a snapshot or a render; RCCL's own default is 30 min); applies to the current
+// attachment too
+void TrainerHost::dp_peer_set_timeout(double seconds) {
+	TCNN_CHECK(seconds > 0.0, "peer exchange: the timeout must be positive");
+	peer_timeout_s = seconds;
+	if (peer) peer->timeout_ticks = (long long)((double)peer->clock_khz * 1000.0 * seconds);
+}
+
+double peer_default_timeout_s() {
+	const char* e = std::getenv("TCNN_PEER_TIMEOUT_S");
+	const double v = e ? std::atof(e) : 0.0;
+	return v > 0.0 ? v : 300.0;
+}
+
 static void grow_keep(DevBuf& b, size_t bytes, size_t valid) {
 	if (b.bytes >= bytes) return;
 	DevBuf n;
@@ -212,7 +245,6 @@ void TrainerHost::dp_peer_export(int nranks, int rank, void* blob_out) {
 	TCNN_CHECK(!dp, "peer exchange: detach the RCCL communicator first (set_dp(NULL))");
 	TCNN_CHECK(nranks >= 1 && rank >= 0 && rank < nranks, "peer exchange: rank outside [0, nranks)");
 	TCNN_CHECK(nranks <= PEER_MAX_RANKS, "peer exchange: at most 64 ranks (the ranks of one node)");
-	TCNN_CHECK(overlapped_ok(), "peer exchange: needs the fused grid engine (the step's gradient sums in one buffer)");
 	if (peer) dp_peer_detach();
 	TCNN_HIP_CHECK(hipDeviceSynchronize());
 	auto pd = std::make_shared<PeerDp>();
@@ -242,7 +274,8 @@ void TrainerHost::dp_peer_export(int nranks, int rank, void* blob_out) {
 	int dev = 0, khz = 0;
 	TCNN_HIP_CHECK(hipGetDevice(&dev));
 	TCNN_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
-	pd->timeout_ticks = (long long)std::max(khz, 1) * 1000LL * 10;  // 10 s
+	pd->clock_khz = std::max(khz, 1);
+	pd->timeout_ticks = (long long)((double)pd->clock_khz * 1000.0 * peer_timeout_s);
 	PeerBlob b;
 	std::memset(&b, 0, sizeof(b));
 	b.magic = PEER_MAGIC;
@@ -286,16 +319,17 @@ void TrainerHost::dp_peer_attach(const void* blobs) {
 	hipLaunchKernelGGL(k_peer_token, dim3(1), dim3(64), 0, nullptr, (uint32_t*)pd.x[PB_FLAGS], probe_token(pd.rank));
 	TCNN_HIP_CHECK(hipGetLastError());
 	peer_wait(nullptr, CTR_SYNC, SLOT_PROBE, 1);
-	hipLaunchKernelGGL(k_peer_probe, dim3(1), dim3(64), 0, nullptr, pd.flags_arg, N, pd.err_dev);
+	hipLaunchKernelGGL(k_peer_probe, dim3(1), dim3(64), 0, nullptr, pd.flags_arg, N, pd.err_dev, pd.ctr.as<uint32_t>());
 	TCNN_HIP_CHECK(hipGetLastError());
 	TCNN_HIP_CHECK(hipDeviceSynchronize());
 	pd.check();
 	pd.attached = true;
 	peer_attached = true;
+	peer_nranks = N;
 	dp_sharded = true;
 	dp_state_partial = false;
 	dp_per = pd.per;
-	grad_scale = grad_scale_user / (float)N;
+	grad_scale = grad_scale_user / (float)dp_nranks();
 	if (graph) set_graph(use_graph);
 }
 
@@ -311,8 +345,17 @@ void TrainerHost::peer_wait(hipStream_t st, int c, int slot, int signal_bump) {
 void TrainerHost::training_step_peer(hipStream_t st, uint32_t B, const float* input, const float* target) {
 	PeerDp& pd = *peer;
 	pd.check();
-	// this rank's gradient sums, straight into its uncached exchange buffer
-	training_step_overlapped(st, B, input, target, false, (float*)pd.x[PB_G32]);
+	// this rank's gradient sums, straight into its uncached exchange buffer: the fused grid engine's
+	// two-launch step, or any other engine's pass (tile, layer-wise) with its reductions writing there
+	float* gx = (float*)pd.x[PB_G32];
+	if (overlapped_ok()) {
+		training_step_overlapped(st, B, input, target, false, gx);
+	} else {
+		mark(st, 0);
+		model->fwd_bwd(st, ws, B, input, target, n_output_dims, loss_scale, w16.p, nullptr, nullptr, gx, [&](int ph) { mark(st, ph); });
+		launch_sum(st, ws.loss_partial.as<float>(), ws.n_loss_partials, d_loss.as<float>());
+		mark(st, 4);
+	}
 	peer_wait(st, CTR_STEP, SLOT_GRAD, 1);  // signal "gradients ready" and wait for every rank's
 	const uint64_t lo = std::min<uint64_t>(n_params, (uint64_t)pd.rank * pd.per), hi = std::min<uint64_t>(n_params, lo + pd.per);
 	++adam_step;
@@ -323,7 +366,7 @@ void TrainerHost::training_step_peer(hipStream_t st, uint32_t B, const float* in
 	                    steps.as<uint32_t>()};
 	if (hi > lo)
 		hipLaunchKernelGGL(k_peer_adam, dim3(div_round_up(hi - lo, 256)), dim3(256), 0, st, a, s, pd.table<const float>(PB_G32), pd.nranks,
-		                   (_Float16*)pd.x[PB_W16]);
+		                   (_Float16*)pd.x[PB_W16], pd.ctr.as<uint32_t>());
 	TCNN_HIP_CHECK(hipGetLastError());
 	peer_wait(st, CTR_STEP, SLOT_WEIGHTS, 0);  // signal "weights ready" and wait
 	peer_gather(st, 1);
@@ -337,6 +380,7 @@ void TrainerHost::training_step_peer(hipStream_t st, uint32_t B, const float* in
 void TrainerHost::peer_gather(hipStream_t st, int what) {
 	PeerDp& pd = *peer;
 	PeerGatherArgs g{};
+	g.ctr = pd.ctr.as<uint32_t>();
 	g.nranks = (uint32_t)pd.nranks;
 	g.rank = (uint32_t)pd.rank;
 	g.per = pd.per;
@@ -367,7 +411,7 @@ void TrainerHost::dp_peer_gather_state(hipStream_t st) {
 	const uint64_t lo = std::min<uint64_t>(n_params, (uint64_t)pd.rank * pd.per), hi = std::min<uint64_t>(n_params, lo + pd.per);
 	if (hi > lo)
 		hipLaunchKernelGGL(k_peer_stage, dim3(div_round_up(hi - lo, 256)), dim3(256), 0, st, w32.as<float>(), m1.as<float>(), m2.as<float>(),
-		                   steps.as<uint32_t>(), (uint32_t*)pd.x[PB_STATE], lo, hi - lo, pd.per * (uint64_t)pd.nranks);
+		                   steps.as<uint32_t>(), (uint32_t*)pd.x[PB_STATE], lo, hi - lo, pd.per * (uint64_t)pd.nranks, pd.ctr.as<uint32_t>());
 	TCNN_HIP_CHECK(hipGetLastError());
 	peer_wait(st, CTR_SYNC, SLOT_GATHER, 1);
 	peer_gather(st, 4);
@@ -387,6 +431,7 @@ void TrainerHost::dp_peer_detach() {
 	}
 	peer.reset();
 	peer_attached = false;
+	peer_nranks = 1;
 	dp_sharded = false;
 	dp_state_partial = false;
 	grad_scale = grad_scale_user;
@@ -398,6 +443,7 @@ void TrainerHost::dp_peer_abandon() {
 	TCNN_HIP_CHECK(hipDeviceSynchronize());
 	peer.reset();
 	peer_attached = false;
+	peer_nranks = 1;
 	dp_sharded = false;
 	dp_state_partial = false;
 	grad_scale = grad_scale_user;

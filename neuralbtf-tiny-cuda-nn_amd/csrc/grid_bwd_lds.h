@@ -472,6 +472,7 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 			}
 		}
 	}
+	if (dbg_times && threadIdx.x == 0) dbg_times[6 * blockIdx.x + 5] = wall_clock64() + (m != m ? 1 : 0);  // dL/dy loads done
 #pragma unroll
 	for (int o = 32; o > 0; o >>= 1) m += __shfl_xor(m, o);
 	if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;

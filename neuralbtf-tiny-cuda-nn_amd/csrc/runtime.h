@@ -340,6 +340,7 @@ void workspace_free(hipStream_t st, void* p);
 void workspace_arena_free(hipStream_t st);
 void workspace_arena_free_all();
 uint64_t dp_peer_blob_bytes();  // bytes of one rank's peer-exchange blob (dp_peer.hip)
+double peer_default_timeout_s();  // TCNN_PEER_TIMEOUT_S or 300 s
 void workspace_arena_info(hipStream_t st, uint64_t* mapped_bytes, int* vmm);
 
 struct TrainerHost {
@@ -410,6 +411,11 @@ struct TrainerHost {
 	void dp_peer_attach(const void* blobs);
 	void dp_peer_detach();
 	void dp_peer_abandon();  // local, no barrier: only before any exchange step (a failed attach on some rank)
+	double peer_timeout_s = peer_default_timeout_s();
+	void dp_peer_set_timeout(double seconds);
+	int peer_nranks = 1;  // ranks of the attached peer exchange
+	// ranks whose gradients Adam's input sums (RCCL communicator or peer exchange): grad_scale = user / N
+	int dp_nranks() const { return dp ? dp->nranks : (peer_attached ? peer_nranks : 1); }
 	void dp_peer_gather_state(hipStream_t st);
 	void training_step_peer(hipStream_t st, uint32_t B, const float* input, const float* target);
 	void peer_wait(hipStream_t st, int c, int slot, int signal_bump = -1);

@@ -100,6 +100,7 @@ _SIGS = {
     "tcnn_trainer_dp_peer_attach": (c_int, [c_void_p, c_void_p]),
     "tcnn_trainer_dp_peer_detach": (c_int, [c_void_p]),
     "tcnn_trainer_dp_peer_abandon": (c_int, [c_void_p]),
+    "tcnn_trainer_dp_peer_set_timeout": (c_int, [c_void_p, ctypes.c_double]),
     "tcnn_trainer_inference_engine": (c_char_p, [c_void_p]),
     "tcnn_module_engine": (c_char_p, [c_void_p]),
     "tcnn_module_inference_engine": (c_char_p, [c_void_p]),

@@ -21,13 +21,17 @@ collective, and Adam reads it with scale 1. The default fp32 exchange keeps the 
 numerics (one fp16 rounding of the reduced sum).
 
 exchange="peer": the exchange through the ranks' peer-mapped memory (PeerExchange, csrc/dp_peer.hip):
-sharded, no collective library in the step, one C-ABI call per step.
+sharded, no collective library in the step, one C-ABI call per step. It is the default on GPU ranks
+(exchange="auto": "peer" when the process group's backend is nccl/RCCL, else "torch", e.g. the gloo
+rehearsal on CPU), with a collective fallback to "engine" when some rank cannot map its peers.
+Teardown of a peer attachment is collective: call close() (or gather_state() and close()) on every
+rank before the trainer goes away.
 
 exchange="engine": the same exchange runs inside the engine instead (EngineComm, tcnn_trainer_set_dp):
 one RCCL communicator created from a unique id broadcast over torch.distributed, the collectives
 issued by the training step itself on its stream (network part overlapped with the grid backward),
-so a data-parallel step is one C-ABI call that a hipGraph can capture. exchange="torch" (default)
-drives torch.distributed collectives from Python -- also the gloo rehearsal on CPU.
+so a data-parallel step is one C-ABI call that a hipGraph can capture. exchange="torch" drives
+torch.distributed collectives from Python -- also the gloo rehearsal on CPU.
 
 shard_optimizer=True (ZeRO-1 style): instead of the all-reduce,
 the fp32 gradient sums are reduce-scattered (each rank receives the sum of one contiguous 1/N of the
@@ -102,12 +106,15 @@ class PeerExchange:
     through the peers' memory by itself: sharded Adam on the sum of the ranks' gradients read over
     xGMI, then a gather of the other shards' fp16 parameters -- no collective launch per step."""
 
-    def __init__(self, trainer, group=None):
+    def __init__(self, trainer, group=None, timeout_s=None):
         from tinycudann import _lib as L
         self._L = L
         self.trainer = trainer
+        self.attached = False
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        if timeout_s is not None:  # default: TCNN_PEER_TIMEOUT_S or 300 s
+            L.check(L.lib().tcnn_trainer_dp_peer_set_timeout(trainer.h, float(timeout_s)))
         n = int(L.lib().tcnn_dp_peer_blob_bytes())
         blob = (ctypes.c_uint8 * n)()
         ok = L.lib().tcnn_trainer_dp_peer_export(trainer.h, self.world, self.rank, ctypes.byref(blob)) == 0
@@ -128,19 +135,36 @@ class PeerExchange:
             L.lib().tcnn_trainer_dp_peer_abandon(trainer.h)
             raise RuntimeError("peer exchange unavailable: " + "; ".join(f"rank {r}: {o[1]}" for r, o in enumerate(oks) if not o[0]))
         trainer._dp_state_partial = False
+        self.attached = True
 
     def detach(self):
-        """collective: completes the sharded optimizer state, then closes the peer mappings"""
-        self._L.check(self._L.lib().tcnn_trainer_dp_peer_detach(self.trainer.h))
+        """collective: completes the sharded optimizer state, then closes the peer mappings (every
+        rank calls it; idempotent)"""
+        if self.attached:
+            self.attached = False
+            self._L.check(self._L.lib().tcnn_trainer_dp_peer_detach(self.trainer.h))
+
+    close = detach
+
+    def __del__(self):
+        # last resort: a collective detach from a finaliser only works when every rank drops its
+        # exchange at the same point; call close() explicitly
+        try:
+            self.detach()
+        except Exception:
+            pass
 
 
 class DataParallelTrainer:
     """Wraps tinycudann.Trainer: training_step = local fwd/bwd, all-reduce (overlapped), Adam."""
 
-    def __init__(self, trainer, group=None, overlap=True, allreduce_dtype="fp32", shard_optimizer=False, exchange="torch",
-                 peer_fallback=False):
+    def __init__(self, trainer, group=None, overlap=True, allreduce_dtype="fp32", shard_optimizer=False, exchange="auto",
+                 peer_fallback=True, peer_timeout_s=None):
         assert allreduce_dtype in ("fp32", "fp16")
-        assert exchange in ("torch", "engine", "peer")
+        assert exchange in ("auto", "torch", "engine", "peer")
+        if exchange == "auto":  # the peer exchange on GPU ranks (RCCL process group), torch.distributed otherwise
+            gpu = dist.is_initialized() and dist.get_backend(group) == "nccl"
+            exchange = "peer" if gpu and allreduce_dtype == "fp32" else "torch"
         assert not (shard_optimizer and allreduce_dtype == "fp16"), "the sharded optimizer exchanges fp32 gradient sums"
         assert not (exchange in ("engine", "peer") and allreduce_dtype == "fp16"), "the engine exchanges sum fp32 gradients"
         self.trainer = trainer
@@ -154,7 +178,7 @@ class DataParallelTrainer:
         if self.world > 1 and exchange == "peer":
             self.shard_optimizer = True  # the peer exchange is the sharded schedule
             try:
-                self.comm = PeerExchange(trainer, group)
+                self.comm = PeerExchange(trainer, group, timeout_s=peer_timeout_s)
             except RuntimeError as e:
                 if not peer_fallback:
                     raise
@@ -238,6 +262,15 @@ class DataParallelTrainer:
         self.trainer._dp_state_partial = False
 
     gather_master = gather_state  # the round-2 name (it gathered only the masters)
+
+    def close(self):
+        """collective teardown: detaches the peer exchange (completing the sharded optimizer state) or
+        the engine communicator; every rank calls it before its trainer goes away"""
+        if isinstance(self.comm, PeerExchange):
+            self.comm.close()
+        elif isinstance(self.comm, EngineComm):
+            self.trainer.set_dp(None)
+        self.comm = None
 
     def training_step(self, input, target):
         if self.world == 1 or self.exchange in ("engine", "peer"):

@@ -23,7 +23,23 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, B, q):
+def _cfg(name):
+    import copy
+    from helpers import CONFIG_HASH, CONFIG_ONEBLOB
+    if name == "hash":  # the register-resident fused engine (configs[2])
+        return CONFIG_HASH
+    if name == "hash_w128h4":  # the tile engine (configs[3]'s network)
+        c = copy.deepcopy(CONFIG_HASH)
+        c["network"].update({"n_neurons": 128, "n_hidden_layers": 4})
+        return c
+    if name == "oneblob_cutlass":  # the layer-wise engine (CutlassMLP)
+        c = copy.deepcopy(CONFIG_ONEBLOB)
+        c["network"].update({"otype": "CutlassMLP", "n_neurons": 64, "n_hidden_layers": 2})
+        return c
+    raise KeyError(name)
+
+
+def _worker(rank, world, port, B, q, cfg_name="hash"):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     repo = os.path.dirname(here)
@@ -34,13 +50,14 @@ def _worker(rank, world, port, B, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from helpers import CONFIG_HASH, make_batch, trainer_arrays
+    from helpers import make_batch, trainer_arrays
     from tinycudann import Trainer
     from tinycudann.parallel import DataParallelTrainer, shard_bounds
     lo, hi = shard_bounds(B, rank, world)
+    cfg = _cfg(cfg_name)
 
     def run(**kw):
-        tr = Trainer(2, 3, CONFIG_HASH, seed=1337)
+        tr = Trainer(2, 3, cfg, seed=1337)
         dp = DataParallelTrainer(tr, **kw)
         losses = []
         for s in range(4):
@@ -52,10 +69,11 @@ def _worker(rank, world, port, B, q):
         a = trainer_arrays(tr)
         return tr, dp, a["w32"], a["w16"], bytes(tr.serialize(optimizer=True)), losses
 
-    _, _, w_ref, h_ref, snap_ref, l_ref = run()  # replicated all-reduce (gloo), overlapped
-    tr, dp, w_peer, h_peer, snap_peer, l_peer = run(exchange="peer")
+    _, _, w_ref, h_ref, snap_ref, l_ref = run(exchange="torch")  # replicated all-reduce (gloo), overlapped
+    tr, dp, w_peer, h_peer, snap_peer, l_peer = run(exchange="peer", peer_fallback=False, peer_timeout_s=60)
+    assert tr.engine == ("fused" if cfg_name != "oneblob_cutlass" else "layered")
     # detach (collective), then this rank trains on alone from the gathered state
-    dp.comm.detach()
+    dp.close()
     pos_s, tgt_s = make_batch(B, step=9)
     tr.training_step(torch.from_numpy(pos_s[lo:hi]).cuda(), torch.from_numpy(tgt_s[lo:hi]).cuda())
     torch.cuda.synchronize()
@@ -65,17 +83,19 @@ def _worker(rank, world, port, B, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_peer_exchange_equals_allreduce(world):
-    """2 ranks: bit-identical to the all-reduce. 4 ranks (1024 points each, padded shards of 178,888
-    parameters): the peer sum runs in rank order g0+g1+g2+g3 while gloo's ring sums in its own order,
-    so the comparison is within fp32 rounding; the replicas must still agree bit for bit."""
+@pytest.mark.parametrize("world,cfg_name", [(2, "hash"), (4, "hash"), (2, "hash_w128h4"), (2, "oneblob_cutlass")])
+def test_peer_exchange_equals_allreduce(world, cfg_name):
+    """2 ranks: bit-identical to the all-reduce, on every engine -- the register-resident fused kernel
+    (config_hash), the tile kernel (HashGrid + W128/H4, configs[3]'s network) and the layer-wise engine
+    (OneBlob + CutlassMLP). 4 ranks (1024 points each, padded shards of 178,888 parameters): the peer
+    sum runs in rank order g0+g1+g2+g3 while gloo's ring sums in its own order, so the comparison is
+    within fp32 rounding; the replicas must still agree bit for bit."""
     import torch.multiprocessing as mp
     B = 4096
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, B, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, B, q, cfg_name)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda r: r[0])
@@ -96,3 +116,102 @@ def test_peer_exchange_equals_allreduce(world):
     for r in res[1:]:  # the replicas agree
         np.testing.assert_array_equal(res[0][5], r[5])
         np.testing.assert_array_equal(res[0][6], r[6])
+
+
+def _worker8(rank, world, port, B, q):
+    """configs[4]'s exchange: rank's 2^18/8 shard of the global batch, peer exchange, 3 steps."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    sys.path[:0] = [repo, os.path.join(repo, "neuralbtf-tiny-cuda-nn_amd"), here]
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from helpers import CONFIG_HASH, make_batch, trainer_arrays
+    from tinycudann import Trainer
+    from tinycudann.parallel import DataParallelTrainer, shard_bounds
+    lo, hi = shard_bounds(B, rank, world)
+    tr = Trainer(2, 3, CONFIG_HASH, seed=1337)
+    dp = DataParallelTrainer(tr, exchange="peer", peer_fallback=False, peer_timeout_s=60)
+    out = {}
+    for s in range(3):
+        pos_s, tgt_s = make_batch(B, step=s)
+        dp.training_step(torch.from_numpy(pos_s[lo:hi]).cuda(), torch.from_numpy(tgt_s[lo:hi]).cuda())
+        if s == 0:
+            a = trainer_arrays(tr)
+            n = tr.n_params
+            per = ((n + world - 1) // world + 7) // 8 * 8
+            plo, phi = min(n, rank * per), min(n, rank * per + per)
+            out["g_shard"] = (plo, phi, a["g32"][plo:phi].copy())  # this rank's shard of the summed gradient
+            out["w16_1"] = a["w16"]
+    torch.cuda.synchronize()
+    out["w16_3"] = trainer_arrays(tr)["w16"]
+    dp.close()
+    if rank == 0:  # the single-process step on the whole 2^18 batch (same seed, same batch)
+        ref = Trainer(2, 3, CONFIG_HASH, seed=1337)
+        pos_s, tgt_s = make_batch(B, step=0)
+        p, t = torch.from_numpy(pos_s).cuda(), torch.from_numpy(tgt_s).cuda()
+        ref.training_step(p, t, run_optimizer=False)
+        a = trainer_arrays(ref)
+        out["ref_g32"], out["ref_w16_0"] = a["g32"], a["w16"]
+        ref.optimizer_step()
+        out["ref_w16_1"] = trainer_arrays(ref)["w16"]
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_peer_exchange_8_ranks_equals_single_gpu_step():
+    """BASELINE configs[4] (config_hash batch-sharded over 8 ranks, 2^18 / 8 = 2^15 points each) through
+    the peer exchange, 8 processes sharing one GPU: the replicas stay bit-identical over 3 steps, and the
+    summed gradient of the first step equals the single-process 2^18 step's (N GPUs x B/N
+    = 1 GPU x B within summation-order tolerance).
+
+    Tolerance, per element: each rank's loss normalises by its own B/8 * dims, so the shards' fp16
+    loss-scaled dL/dy are exactly 8x the single step's (a power of two; neither side is subnormal at the
+    initial outputs ~1e-5 against targets ~0.5) and every per-sample term of the network gradient is the
+    same up to that factor: what differs is the fp32 summation order (8 shard sums of 2^15 terms + one
+    8-term sum vs 2^18 terms) -- bounded by 2^-20 * sum|terms| (relative 1e-6 of the gradient scale here)
+    -- and, in the grid, the per-chunk int32 fixed-point steps (2^-31 of the chunk's sum |dL/dy| per
+    update, 8x finer chunks on the shards). Checked as |g_peer / 8 - g_single| <= 1e-5 |g_single| +
+    1e-6 max|g| per part (network, grid), and Adam's first update agrees wherever the gradients round to
+    the same fp16 value (elsewhere step 1 of Adam moves by +-lr sign(g) and may legitimately differ)."""
+    import torch.multiprocessing as mp
+    world, B = 8, 1 << 18
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker8, args=(r, world, port, B, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(1, world):  # replicas bit-identical after 1 and 3 steps
+        np.testing.assert_array_equal(res[0]["w16_1"], res[r]["w16_1"])
+        np.testing.assert_array_equal(res[0]["w16_3"], res[r]["w16_3"])
+    ref = res[0]["ref_g32"].astype(np.float64)
+    n = ref.size
+    g = np.zeros(n)
+    covered = np.zeros(n, bool)
+    for r in range(world):
+        plo, phi, gs = res[r]["g_shard"]
+        g[plo:phi] = gs.astype(np.float64) / world
+        covered[plo:phi] = True
+    assert covered.all()
+    from helpers import CONFIG_HASH, O
+    W, NH = CONFIG_HASH["network"]["n_neurons"], CONFIG_HASH["network"]["n_hidden_layers"]
+    nm = O.mlp_n_params(W, 32, NH, 16)
+    for part in (slice(0, nm), slice(nm, n)):
+        d = np.abs(g[part] - ref[part])
+        bound = 1e-5 * np.abs(ref[part]) + 1e-6 * np.abs(ref[part]).max()
+        k = int(np.argmax(d / bound))
+        assert d[k] <= bound[k], (part, k, g[part][k], ref[part][k])
+    # Adam's first step: equal wherever the two gradients round to the same fp16 (the g16 Adam reads)
+    same16 = g.astype(np.float32).astype(np.float16) == ref.astype(np.float32).astype(np.float16)
+    assert same16.mean() > 0.99, same16.mean()
+    np.testing.assert_array_equal(res[0]["w16_1"][same16], res[0]["ref_w16_1"][same16])
