@@ -236,6 +236,10 @@ float* tcnn_trainer_gradients_fp32(tcnn_trainer* t);
 int tcnn_trainer_optimizer_state(tcnn_trainer* t, float** first_moments, float** second_moments, uint32_t** steps);
 /* Data-parallel support: Adam reads grad_fp32 * grad_scale (set 1/N after a sum all-reduce). */
 int tcnn_trainer_set_gradient_scale(tcnn_trainer* t, float scale);
+/* The loss scale training_step / forward / optimizer_step use -- the reference's loss_scale argument of
+ * Trainer::forward and Trainer::optimizer_step (trainer.h:97-160); default default_loss_scale<__half>
+ * = 128 (common.h:232). */
+int tcnn_trainer_set_loss_scale(tcnn_trainer* t, float loss_scale);
 /* hipGraph replay of the single-GPU training step (the reference Trainer's CUDA graph,
  * trainer.h:163-190 / cuda_graph.h:52-178): off by default. While on, training_step with
  * run_optimizer = 1 replays a captured graph as long as the batch size, the input / target pointers,

@@ -636,6 +636,12 @@ int tcnn_trainer_set_gradient_scale(tcnn_trainer* t, float s) {
 	h.grad_scale = s / (float)h.dp_nranks();  // the RCCL communicator's or the peer exchange's N
 	return 0;
 }
+int tcnn_trainer_set_loss_scale(tcnn_trainer* t, float loss_scale) {
+	return guard([&] {
+		TCNN_CHECK(loss_scale > 0.0f && std::isfinite(loss_scale), "set_loss_scale: the loss scale must be positive and finite");
+		t->t->loss_scale = loss_scale;
+	});
+}
 int tcnn_trainer_set_graph(tcnn_trainer* t, int on) {
 	return guard([&] { t->t->set_graph(on != 0); });
 }

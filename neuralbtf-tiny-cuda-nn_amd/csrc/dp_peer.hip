@@ -225,6 +225,10 @@ void TrainerHost::dp_peer_set_timeout(double seconds) {
 	if (peer) peer->timeout_ticks = (long long)((double)peer->clock_khz * 1000.0 * seconds);
 }
 
+void TrainerHost::peer_check() const {
+	if (peer) peer->check();
+}
+
 double peer_default_timeout_s() {
 	const char* e = std::getenv("TCNN_PEER_TIMEOUT_S");
 	const double v = e ? std::atof(e) : 0.0;

@@ -218,10 +218,16 @@ __global__ __launch_bounds__(256, 2) void k_layer_bwd(uint32_t B, uint32_t N, co
 // the HBM latency overlaps the math); wave w owns output tiles w, w+8, ... (MT x KT tiles of
 // 16x16) with fp32 accumulators for the whole chunk.
 constexpr int WG_WAVES = 8, WG_STEP = 64;
+// Widths above 128 (wgrad_blocks): blockIdx.y / blockIdx.z pick the output block [n0, n0 + 16 MT) x
+// [k0, k0 + 16 KT) of a dW of ldp = ldx columns; dy rows have ldd halves, x rows ldx.
 template <int MT, int KT>
 __global__ __launch_bounds__(WG_WAVES * 64) void k_wgrad(uint32_t B, uint32_t pts_per_chunk, const _Float16* __restrict__ dy,
-                                                         const _Float16* __restrict__ x, float* __restrict__ partial) {
+                                                         const _Float16* __restrict__ x, float* __restrict__ partial, uint32_t ldd,
+                                                         uint32_t ldx, uint32_t n_rows, uint32_t nb0, uint32_t kb0) {
 	constexpr int N = 16 * MT, K = 16 * KT, RSD = N + 8, RSX = K + 8, NTHR = WG_WAVES * 64;
+	const uint32_t n0 = nb0 + blockIdx.y * N, k0 = kb0 + blockIdx.z * K;
+	dy += n0;
+	x += k0;
 	constexpr int TILES = MT * KT, TPW = (TILES + WG_WAVES - 1) / WG_WAVES;
 	constexpr int VD = WG_STEP * N / 8, VX = WG_STEP * K / 8;  // 16-byte vectors per step
 	constexpr int PD = (VD + NTHR - 1) / NTHR, PX = (VX + NTHR - 1) / NTHR;
@@ -241,13 +247,13 @@ __global__ __launch_bounds__(WG_WAVES * 64) void k_wgrad(uint32_t B, uint32_t pt
 		for (int j = 0; j < PD; ++j) {
 			const int idx = tid + j * NTHR;
 			const int r = idx / (N / 8), c8 = idx % (N / 8);
-			rd[j] = (idx < VD && b0 + r < i1) ? *(const h8*)(dy + (size_t)(b0 + r) * N + 8 * c8) : h8{0, 0, 0, 0, 0, 0, 0, 0};
+			rd[j] = (idx < VD && b0 + r < i1) ? *(const h8*)(dy + (size_t)(b0 + r) * ldd + 8 * c8) : h8{0, 0, 0, 0, 0, 0, 0, 0};
 		}
 #pragma unroll
 		for (int j = 0; j < PX; ++j) {
 			const int idx = tid + j * NTHR;
 			const int r = idx / (K / 8), c8 = idx % (K / 8);
-			rx[j] = (idx < VX && b0 + r < i1) ? *(const h8*)(x + (size_t)(b0 + r) * K + 8 * c8) : h8{0, 0, 0, 0, 0, 0, 0, 0};
+			rx[j] = (idx < VX && b0 + r < i1) ? *(const h8*)(x + (size_t)(b0 + r) * ldx + 8 * c8) : h8{0, 0, 0, 0, 0, 0, 0, 0};
 		}
 	};
 	auto store = [&](int buf) {
@@ -288,16 +294,150 @@ __global__ __launch_bounds__(WG_WAVES * 64) void k_wgrad(uint32_t B, uint32_t pt
 		__syncthreads();
 		buf ^= 1;
 	}
-	float* dst = partial + (size_t)blockIdx.x * N * K;
+	float* dst = partial + (size_t)blockIdx.x * n_rows * ldx + (size_t)n0 * ldx + k0;
 #pragma unroll
 	for (int m = 0; m < TPW; ++m) {
 		const int j = wave + WG_WAVES * m;
 		if (j < TILES) {
 			const int mt = j / KT, kt = j % KT;
 #pragma unroll
-			for (int r = 0; r < 4; ++r) dst[(16 * mt + 4 * q + r) * K + 16 * kt + c] = acc[m][r];
+			for (int r = 0; r < 4; ++r) dst[(size_t)(16 * mt + 4 * q + r) * ldx + 16 * kt + c] = acc[m][r];
 		}
 	}
+}
+
+// Layers wider than the register kernels above (CutlassMLP widths above 128, encodings wider than 128,
+// padded outputs above 128; reference cutlass_mlp.cu:41-81, fully_fused_mlp.cu:591): one output block
+// of 16 NT features per blockIdx.y, its A rows staged once in dynamic LDS over the whole contraction
+// C (zero-filled to a multiple of 32), persistent 32-sample slices per wave with the contraction as a
+// runtime loop (the next 32-wide step's input rows in flight during this step's MFMAs).
+//   TR = false (forward):  Out[i][o] = act( sum_c W[o][c] In[i][c] ),         W [n_out][C]
+//   TR = true  (backward): Out[i][o] = act'(H[i][o]) * sum_c W[c][o] In[i][c], W [C][n_out]
+template <int NT, bool TR>
+__global__ __launch_bounds__(256, 1) void k_wide_layer(uint32_t B, uint32_t C, uint32_t n_out, const _Float16* __restrict__ w,
+                                                     const _Float16* __restrict__ in, _Float16* __restrict__ out,
+                                                     const _Float16* __restrict__ h, int act, uint32_t pairs) {
+	extern __shared__ __attribute__((aligned(16))) _Float16 sA[];
+	const uint32_t Cp = (C + 31) / 32 * 32, rs = Cp + 8;
+	const uint32_t o0 = blockIdx.y * 16 * NT;
+	const uint32_t ntv = min((uint32_t)NT, (n_out - o0) / 16);  // valid 16-row tiles of this block
+	const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+	const int c = lane & 15, q = lane >> 4;
+	// stage A = rows o0 .. o0 + 16 NT of W (TR: of W^T), zero outside [n_out) x [C)
+	if (!TR) {
+		const uint32_t c8n = Cp / 8;
+		for (uint32_t idx = tid; idx < 16u * NT * c8n; idx += 256) {
+			const uint32_t r = idx / c8n, c8 = idx % c8n;
+			h8 v = h8{0, 0, 0, 0, 0, 0, 0, 0};
+			if (o0 + r < n_out && 8 * c8 < C) v = *(const h8*)(w + (size_t)(o0 + r) * C + 8 * c8);
+			*(h8*)(sA + r * rs + 8 * c8) = v;
+		}
+	} else {
+		constexpr uint32_t R8 = 2 * NT;  // 8-wide row groups of the block
+		for (uint32_t idx = tid; idx < Cp * R8; idx += 256) {
+			const uint32_t cc = idx / R8, r0 = 8 * (idx % R8);
+			h8 v = h8{0, 0, 0, 0, 0, 0, 0, 0};
+			if (cc < C && o0 + r0 < n_out) v = *(const h8*)(w + (size_t)cc * n_out + o0 + r0);
+#pragma unroll
+			for (int e = 0; e < 8; ++e) sA[(r0 + e) * rs + cc] = v[e];
+		}
+	}
+	__syncthreads();
+	const uint32_t n_slices = B / 32, stride = gridDim.x * 4;
+	const f4 fz = {0.0f, 0.0f, 0.0f, 0.0f};
+	const uint32_t steps = Cp / 32;
+	auto load = [&](h8 (&xb)[2], uint32_t base, uint32_t s) {
+#pragma unroll
+		for (int tau = 0; tau < 2; ++tau) {
+			const uint32_t k = 32 * s + 8 * q;
+			xb[tau] = k < C ? *(const h8*)(in + (size_t)(base + 16 * tau + c) * C + k) : h8{0, 0, 0, 0, 0, 0, 0, 0};
+		}
+	};
+	with_act(act, [&](auto A) {
+		constexpr int AC = decltype(A)::value;
+		for (uint32_t sl = blockIdx.x * 4 + wave; sl < n_slices; sl += stride) {
+			const uint32_t base = sl * 32;
+			f4 acc[NT][2];
+#pragma unroll
+			for (int t = 0; t < NT; ++t) acc[t][0] = acc[t][1] = fz;
+			h8 xb[2], xn[2];
+			load(xb, base, 0);
+			for (uint32_t s = 0; s < steps; ++s) {
+				if (s + 1 < steps) load(xn, base, s + 1);
+#pragma unroll
+				for (int t = 0; t < NT; ++t) {
+					if ((uint32_t)t < ntv) {
+						const h8 af = *(const h8*)(sA + (16 * t + c) * rs + 32 * s + 8 * q);
+						acc[t][0] = mfma16(af, xb[0], acc[t][0]);
+						acc[t][1] = mfma16(af, xb[1], acc[t][1]);
+					}
+				}
+				xb[0] = xn[0];
+				xb[1] = xn[1];
+			}
+#pragma unroll
+			for (int t = 0; t < NT; ++t) {
+				if ((uint32_t)t >= ntv) continue;
+#pragma unroll
+				for (int tau = 0; tau < 2; ++tau) {
+					const uint32_t i = base + 16 * tau + c, o = o0 + 16 * t + 4 * q;
+					const f4 v = acc[t][tau];
+					h4 r4;
+					if constexpr (!TR) {
+#pragma unroll
+						for (int r = 0; r < 4; ++r) r4[r] = f16_rn(act_fwd_sel<AC>(act, v[r]));
+					} else if constexpr (AC != ACT_NONE) {
+						const h4 hv = *(const h4*)(h + (size_t)i * n_out + o);
+#pragma unroll
+						for (int r = 0; r < 4; ++r) r4[r] = f16_rn(act_bwd_sel<AC>(act, v[r], (float)hv[r]));
+					} else {
+#pragma unroll
+						for (int r = 0; r < 4; ++r) r4[r] = (_Float16)v[r];
+						if (pairs) {  // level-major feature pairs [n_out / 2][B] (grid F = 2)
+							uint32_t* d2 = (uint32_t*)out;
+							d2[(size_t)(o / 2) * B + i] = __builtin_bit_cast(uint32_t, h2{r4[0], r4[1]});
+							d2[(size_t)(o / 2 + 1) * B + i] = __builtin_bit_cast(uint32_t, h2{r4[2], r4[3]});
+							continue;
+						}
+					}
+					*(h4*)(out + (size_t)i * n_out + o) = r4;
+				}
+			}
+		}
+	});
+}
+
+// NT (output rows per block / 16) of the wide kernel: the staged rows of the whole contraction must fit
+// 160 KB of LDS: 128 rows up to C = 512, 64 up to 1024, 32 up to 2048, 16 up to 4096
+static uint32_t wide_nt(uint32_t C) {
+	const uint32_t rs = (C + 31) / 32 * 32 + 8;
+	for (uint32_t nt = 8; nt >= 1; nt /= 2)
+		if (16 * nt * rs * 2 <= 160 * 1024) return nt;
+	return 0;
+}
+
+static void launch_wide_layer(hipStream_t st, bool tr, uint32_t B, uint32_t C, uint32_t n_out, const void* w16, const void* in16, void* out16,
+                              const void* h16, int act, bool pairs) {
+	const uint32_t nt = wide_nt(C);
+	TCNN_CHECK(nt > 0, "layer: contraction width " + std::to_string(C) + " exceeds the wide layer kernel's LDS (4096)");
+	const uint32_t ny = div_round_up(n_out, 16 * nt);
+	const uint32_t gx = std::max(1u, std::min(div_round_up(B / 32, 4), std::max(1u, 512u / ny)));
+	const size_t lds = (size_t)16 * nt * ((C + 31) / 32 * 32 + 8) * 2;
+	const dim3 g(gx, ny);
+#define WIDE(NT_, TR_)                                                                                                         \
+	{                                                                                                                         \
+		static uint64_t done = 0;                                                                                             \
+		set_dyn_lds((const void*)k_wide_layer<NT_, TR_>, 160 * 1024, done);                                                   \
+		hipLaunchKernelGGL((k_wide_layer<NT_, TR_>), g, dim3(256), lds, st, B, C, n_out, (const _Float16*)w16, (const _Float16*)in16, \
+		                   (_Float16*)out16, (const _Float16*)h16, act, pairs ? 1u : 0u);                                    \
+	}
+	if (tr) {
+		switch (nt) { case 8: WIDE(8, true) break; case 4: WIDE(4, true) break; case 2: WIDE(2, true) break; default: WIDE(1, true) }
+	} else {
+		switch (nt) { case 8: WIDE(8, false) break; case 4: WIDE(4, false) break; case 2: WIDE(2, false) break; default: WIDE(1, false) }
+	}
+#undef WIDE
+	TCNN_HIP_CHECK(hipGetLastError());
 }
 
 // ---- launchers ----
@@ -309,9 +449,10 @@ static uint32_t pow2_ceil_steps(uint32_t k) {  // 32-wide K steps, rounded up to
 // persistent: two workgroups per CU (the weights are staged once per workgroup)
 static uint32_t layer_blocks(uint32_t B) { return std::max(1u, std::min(div_round_up(B / 32, 4), 512u)); }
 
-// CutlassMLP widths (reference cutlass_mlp.h:115-121, REQUIRED_ALIGNMENT 16): any multiple of 16 up
-// to 128 (output tiles 1..8; K zero-filled up to 32, 64 or 128).
-bool layered_width_supported(uint32_t w) { return w >= 16 && w <= 128 && w % 16 == 0; }
+// CutlassMLP widths (reference cutlass_mlp.h:115-121, REQUIRED_ALIGNMENT 16): any multiple of 16 --
+// up to 128 on the register-tiled layer kernels (output tiles 1..8; K zero-filled to 32, 64 or 128),
+// above that (or a contraction above 128) on k_wide_layer, contractions up to 4096.
+bool layered_width_supported(uint32_t w) { return w >= 16 && w <= 4096 && w % 16 == 0; }
 
 #define TCNN_KS_DISPATCH(NT_, KSV, CALL)                                                                  \
 	switch (KSV) { case 1: CALL(NT_, 1); break; case 2: CALL(NT_, 2); break; case 4: CALL(NT_, 4); break; default: ok = false; }
@@ -327,6 +468,10 @@ bool layered_width_supported(uint32_t w) { return w >= 16 && w <= 128 && w % 16 
 void launch_layer_fwd(hipStream_t st, uint32_t B, uint32_t N, uint32_t K, const void* w16, const void* x16, void* y16, int act) {
 	TCNN_CHECK(B % 32 == 0 && N % 16 == 0 && K % 16 == 0, "layer_fwd: B % 32, N % 16, K % 16 must be 0");
 	if (B == 0) return;
+	if (N > 128 || K > 128) {
+		launch_wide_layer(st, false, B, K, N, w16, x16, y16, nullptr, act, false);
+		return;
+	}
 	bool ok = true;
 	const dim3 g(layer_blocks(B));
 #define CALL(nt, ks) hipLaunchKernelGGL((k_layer_fwd<nt, ks>), g, dim3(256), 0, st, B, K, (const _Float16*)w16, (const _Float16*)x16, (_Float16*)y16, act)
@@ -341,6 +486,10 @@ void launch_layer_bwd(hipStream_t st, uint32_t B, uint32_t N, uint32_t K, const 
 	TCNN_CHECK(!pairs || !h16, "layer_bwd: the pairs layout is for the untransferred encoding gradient");
 	TCNN_CHECK(B % 32 == 0 && N % 16 == 0 && K % 16 == 0, "layer_bwd: B % 32, N % 16, K % 16 must be 0");
 	if (B == 0) return;
+	if (N > 128 || K > 128) {
+		launch_wide_layer(st, true, B, N, K, w16, dy16, dx16, h16, h16 ? act : ACT_NONE, pairs);
+		return;
+	}
 	bool ok = true;
 	const dim3 g(layer_blocks(B));
 #define CALL(nt, ks) hipLaunchKernelGGL((k_layer_bwd<nt, ks>), g, dim3(256), 0, st, B, N, (const _Float16*)w16, (const _Float16*)dy16, (const _Float16*)h16, (_Float16*)dx16, act, pairs ? 1u : 0u)
@@ -361,22 +510,35 @@ void launch_wgrad(hipStream_t st, uint32_t B, uint32_t N, uint32_t K, const void
 	TCNN_CHECK(nc <= n_chunks, "wgrad: chunk plan");
 	if (nc < n_chunks) TCNN_HIP_CHECK(hipMemsetAsync(partial + (size_t)nc * N * K, 0, (size_t)(n_chunks - nc) * N * K * 4, st));
 	bool ok = true;
-	const dim3 g(nc);
-	// MT = N / 16 (output tiles), KT = K / 16 (input tiles): both 1..8
-#define WG(mt, kt) hipLaunchKernelGGL((k_wgrad<mt, kt>), g, dim3(WG_WAVES * 64), 0, st, B, ppc, (const _Float16*)dy16, (const _Float16*)x16, partial)
-#define WGK(mt)                                                                          \
-	switch (K / 16) {                                                                    \
-		case 1: WG(mt, 1); break; case 2: WG(mt, 2); break; case 3: WG(mt, 3); break;    \
-		case 4: WG(mt, 4); break; case 5: WG(mt, 5); break; case 6: WG(mt, 6); break;    \
-		case 7: WG(mt, 7); break; case 8: WG(mt, 8); break; default: ok = false;         \
-	}
-	switch (N / 16) {
-		case 1: WGK(1); break; case 2: WGK(2); break; case 3: WGK(3); break; case 4: WGK(4); break;
-		case 5: WGK(5); break; case 6: WGK(6); break; case 7: WGK(7); break; case 8: WGK(8); break;
-		default: ok = false;
-	}
+	// blocks of up to 128 x 128 outputs: the full blocks in one launch, the remainder rows / columns
+	// (N % 128, K % 128: 16 .. 112) in up to three more; MT, KT = tiles of 16 per block (1..8)
+	const uint32_t nfull = N / 128, kfull = K / 128, nrem = (N % 128) / 16, krem = (K % 128) / 16;
+	auto one = [&](uint32_t mt, uint32_t kt, uint32_t gy, uint32_t gz, uint32_t nb0, uint32_t kb0) {
+		if (!mt || !kt || !gy || !gz) return;
+		const dim3 g(nc, gy, gz);
+#define WG(m_, k_) hipLaunchKernelGGL((k_wgrad<m_, k_>), g, dim3(WG_WAVES * 64), 0, st, B, ppc, (const _Float16*)dy16, (const _Float16*)x16, partial, N, K, N, nb0, kb0)
+#define WGK(m_)                                                                          \
+		switch (kt) {                                                                    \
+			case 1: WG(m_, 1); break; case 2: WG(m_, 2); break; case 3: WG(m_, 3); break;    \
+			case 4: WG(m_, 4); break; case 5: WG(m_, 5); break; case 6: WG(m_, 6); break;    \
+			case 7: WG(m_, 7); break; case 8: WG(m_, 8); break; default: ok = false;         \
+		}
+		switch (mt) {
+			case 1: WGK(1); break; case 2: WGK(2); break; case 3: WGK(3); break; case 4: WGK(4); break;
+			case 5: WGK(5); break; case 6: WGK(6); break; case 7: WGK(7); break; case 8: WGK(8); break;
+			default: ok = false;
+		}
 #undef WGK
 #undef WG
+	};
+	if (N <= 128 && K <= 128) {
+		one(N / 16, K / 16, 1, 1, 0, 0);  // the common case: one block
+	} else {
+		one(8, 8, nfull, kfull, 0, 0);
+		one(8, krem, nfull, 1, 0, 128 * kfull);
+		one(nrem, 8, 1, kfull, 128 * nfull, 0);
+		one(nrem, krem, 1, 1, 128 * nfull, 128 * kfull);
+	}
 	TCNN_CHECK(ok, "wgrad: unsupported shape N=" + std::to_string(N) + " K=" + std::to_string(K));
 	TCNN_HIP_CHECK(hipGetLastError());
 }

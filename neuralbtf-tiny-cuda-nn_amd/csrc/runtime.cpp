@@ -371,10 +371,12 @@ MlpHost::MlpHost(uint32_t n_input_dims, uint32_t n_output_dims, const json& net)
 	           "Invalid network type: " + otype);
 	width = jval<uint32_t>(net, "n_neurons", 128u);
 	n_hidden_layers = jval<uint32_t>(net, "n_hidden_layers", 5u);
-	TCNN_CHECK(n_hidden_layers >= 1, "FullyFusedMLP requires at least 1 hidden layer (3 layers in total).");
-	if (ieq(otype, "FullyFusedMLP") || ieq(otype, "MegakernelMLP"))
+	if (ieq(otype, "FullyFusedMLP") || ieq(otype, "MegakernelMLP")) {
+		TCNN_CHECK(n_hidden_layers >= 1, "FullyFusedMLP requires at least 1 hidden layer (3 layers in total).");
 		TCNN_CHECK(width == 16 || width == 32 || width == 64 || width == 128,
 		           "FullyFusedMLP only supports 16, 32, 64, and 128 neurons, but got " + std::to_string(width) + ". Use CutlassMLP instead if this is a requirement.");
+	}
+	// CutlassMLP (cutlass_mlp.cu:41-81): any width; 0 hidden layers = one [padded_output][input] matrix
 	activation = parse_activation(jval<std::string>(net, "activation", "ReLU"));
 	output_activation = parse_activation(jval<std::string>(net, "output_activation", "None"));
 	n_input = n_input_dims;
@@ -393,6 +395,10 @@ static void xavier(Pcg32& rnd, uint32_t rows, uint32_t cols, float* out, float s
 }
 
 void MlpHost::initialize_params(Pcg32& rng, float* out, float scale) const {
+	if (n_hidden_layers == 0) {  // one matrix (cutlass_mlp.cu:64-67)
+		xavier(rng, padded_output, n_input, out, scale);
+		return;
+	}
 	xavier(rng, width, n_input, out, scale);
 	out += (size_t)width * n_input;
 	for (uint32_t i = 1; i < n_hidden_layers; ++i) {
@@ -556,9 +562,11 @@ const char* NetworkHost::inference_engine() const {
 	return layered_ok() ? "layered" : "unsupported";
 }
 
+// any width / input width / padded output that is a multiple of 16 (layers above 128 run k_wide_layer)
 bool NetworkHost::layered_ok() const {
-	return layered_width_supported(mlp.width) && mlp.n_input % 16 == 0 && mlp.n_input <= 128 && mlp.padded_output <= 128 &&
-	       mlp.activation != ACT_SINE && mlp.output_activation != ACT_SINE;  // Sine has no post-activation backward
+	return layered_width_supported(mlp.width) && mlp.n_input % 16 == 0 && layered_width_supported(mlp.n_input) &&
+	       layered_width_supported(mlp.padded_output) && mlp.activation != ACT_SINE &&
+	       mlp.output_activation != ACT_SINE;  // Sine has no post-activation backward
 }
 
 void NetworkHost::initialize_params(Pcg32& rng, float* out, float scale) const {
@@ -583,7 +591,7 @@ void NetworkHost::forward_layers(hipStream_t st, StepWorkspace& ws, uint32_t B, 
 		x = act_buf(j);
 		K = W;
 	}
-	launch_layer_fwd(st, B, OUTP, W, p, x, out16, mlp.output_activation);
+	launch_layer_fwd(st, B, OUTP, K, p, x, out16, mlp.output_activation);
 }
 
 void NetworkHost::inference(hipStream_t st, StepWorkspace& ws, uint32_t B, const float* pos, const void* params16, void* out16,
@@ -835,7 +843,7 @@ void NetworkHost::fwd_bwd_layered(hipStream_t st, StepWorkspace& ws, uint32_t B,
 	}
 	launch_act_bwd_inplace(st, B * OUTP, mlp.output_activation, out, ws.dout16.p);
 
-	// backward: weight offsets [W0 | W1..W_{NH-1} | Wout]
+	// backward: weight offsets [W0 | W1..W_{NH-1} | Wout] ([Wout] alone for 0 hidden layers)
 	auto w_off = [&](uint32_t j) -> size_t { return j == 0 ? 0 : (size_t)W * IN + (size_t)(j - 1) * W * W; };
 	auto wgrad = [&](uint32_t N, uint32_t K, const void* dy, const void* x, size_t off) {
 		launch_wgrad(st, B, N, K, dy, x, ws.wgrad_partial.as<float>(), nck);
@@ -845,28 +853,34 @@ void NetworkHost::fwd_bwd_layered(hipStream_t st, StepWorkspace& ws, uint32_t B,
 	};
 	_Float16* dcur = ws.delta0.as<_Float16>();
 	_Float16* dnext = ws.delta1.as<_Float16>();
-	// output layer
-	wgrad(OUTP, W, ws.dout16.p, act(NH - 1), w_off(NH));
-	launch_layer_bwd(st, B, OUTP, W, p16 + w_off(NH), ws.dout16.p, act(NH - 1), dcur, mlp.activation);
-	for (uint32_t j = NH - 1; j >= 1; --j) {
-		wgrad(W, W, dcur, act(j - 1), w_off(j));
-		launch_layer_bwd(st, B, W, W, p16 + w_off(j), dcur, act(j - 1), dnext, mlp.activation);
-		std::swap(dcur, dnext);
-	}
-	wgrad(W, IN, dcur, ws.enc16.p, 0);
-	if (mark) mark(1);
 	const bool enc_grad = enc->n_params() > 0 || dL_dinput;
 	// a grid with feature pairs and no padding takes dL/d(encoding) as level-major pairs [L][B], the
 	// layout its backward reads coalesced (AoS rows would cost one 64-byte line per 4-byte read)
 	const bool pairs = grid && grid->desc.n_features_per_level == 2 && grid->n_to_pad == 0;
 	const int dy_layout = pairs ? 0 : 2;
-	if (enc_grad) {
+	const _Float16* denc = dnext;  // dL/d(encoding), when enc_grad
+	if (NH == 0) {  // one matrix: dWout = dout^T enc, dL/d(encoding) = Wout^T dout (no transfer)
+		wgrad(OUTP, IN, ws.dout16.p, ws.enc16.p, 0);
+		if (mark) mark(1);
+		if (enc_grad) launch_layer_bwd(st, B, OUTP, IN, p16, ws.dout16.p, nullptr, dnext, ACT_NONE, pairs);
+	} else {
+		// output layer
+		wgrad(OUTP, W, ws.dout16.p, act(NH - 1), w_off(NH));
+		launch_layer_bwd(st, B, OUTP, W, p16 + w_off(NH), ws.dout16.p, act(NH - 1), dcur, mlp.activation);
+		for (uint32_t j = NH - 1; j >= 1; --j) {
+			wgrad(W, W, dcur, act(j - 1), w_off(j));
+			launch_layer_bwd(st, B, W, W, p16 + w_off(j), dcur, act(j - 1), dnext, mlp.activation);
+			std::swap(dcur, dnext);
+		}
+		wgrad(W, IN, dcur, ws.enc16.p, 0);
+		if (mark) mark(1);
 		// dL/d(encoding) = W0^T delta_0 (no transfer), AoS [B][IN] or level-major pairs
-		launch_layer_bwd(st, B, W, IN, p16, dcur, nullptr, dnext, ACT_NONE, pairs);
-		if (dL_dinput) enc->backward_input(st, B, pos, dnext, dL_dinput, eparams, dy_layout);
+		if (enc_grad) launch_layer_bwd(st, B, W, IN, p16, dcur, nullptr, dnext, ACT_NONE, pairs);
+		denc = dnext;
 	}
+	if (enc_grad && dL_dinput) enc->backward_input(st, B, pos, denc, dL_dinput, eparams, dy_layout);
 	if (grid) {
-		grid->backward(st, ws.gbw, B, pos, grid->desc.n_pos_dims, dnext, dy_layout, IN, grad32 + n_mlp);
+		grid->backward(st, ws.gbw, B, pos, grid->desc.n_pos_dims, denc, dy_layout, IN, grad32 + n_mlp);
 	}
 	if (mark) mark(2);
 	if (mark) mark(3);
@@ -940,20 +954,31 @@ void TrainerHost::training_step(hipStream_t st, uint32_t B, const float* input, 
 		timer.sampling = (timer.counter++ % timer.every) == 0;
 		if (timer.sampling) timer.marks.push_back({-1, -1, -1, -1, -1});
 	}
-	if (dp && run_optimizer) {
-		if (use_graph && !timer.enabled && !adam.adabound && training_step_graph(st, B, input, target)) return;
-		training_step_dp(st, B, input, target);
+	// a whole step with the optimizer replays as a hipGraph when enabled (not on the steps that record
+	// phase events, not with AdaBound, whose bounds depend on the step)
+	if (run_optimizer && use_graph && !(timer.enabled && timer.sampling) && !adam.adabound && training_step_graph(st, B, input, target))
 		return;
-	}
-	if (peer_attached && run_optimizer) {
-		training_step_peer(st, B, input, target);
+	if (run_optimizer) {
+		step_eager(st, B, input, target);
 		return;
 	}
 	if (overlapped_ok()) {
-		if (use_graph && run_optimizer && !timer.enabled && !adam.adabound && training_step_graph(st, B, input, target)) return;
-		training_step_overlapped(st, B, input, target, run_optimizer);
+		training_step_overlapped(st, B, input, target, false);
 		return;
 	}
+	training_step_sequential(st, B, input, target, false);
+}
+
+// the eager step with the optimizer, on whichever schedule is attached
+void TrainerHost::step_eager(hipStream_t st, uint32_t B, const float* input, const float* target) {
+	if (dp) training_step_dp(st, B, input, target);
+	else if (peer_attached) training_step_peer(st, B, input, target);
+	else if (overlapped_ok()) training_step_overlapped(st, B, input, target, true);
+	else training_step_sequential(st, B, input, target, true);
+}
+
+// tile and layer-wise engines: the pass, the loss sum, then Adam (reference trainer.h:163-190)
+void TrainerHost::training_step_sequential(hipStream_t st, uint32_t B, const float* input, const float* target, bool run_optimizer) {
 	mark(st, 0);
 	model->fwd_bwd(st, ws, B, input, target, n_output_dims, loss_scale, w16.p, nullptr, nullptr, g32.as<float>(),
 	               [&](int ph) { mark(st, ph); });
@@ -1064,7 +1089,7 @@ TrainerHost::~TrainerHost() {
 
 void TrainerHost::set_graph(bool on) {
 	if (!on && graph) {
-		TCNN_HIP_CHECK(hipStreamSynchronize(graph->cs));
+		TCNN_HIP_CHECK(hipDeviceSynchronize());  // replays run on the callers' streams
 		graph.reset();
 	}
 	use_graph = on;
@@ -1080,14 +1105,17 @@ std::vector<uint64_t> TrainerHost::graph_key(uint32_t B, const float* input, con
 	                           (uint64_t)(uintptr_t)ws.gbw.partial.p, (uint64_t)(uintptr_t)ws.gbw.recs.p,
 	                           (uint64_t)(uintptr_t)ws.gbw.dir.p, (uint64_t)(uintptr_t)ws.gbw.dysum.p, ws.n_fused_blocks,
 	                           ws.gbw.n_chunks, (uint64_t)overlapped_ok(), (uint64_t)(uintptr_t)dp, (uint64_t)dp_sharded, dp_per,
-	                           (uint64_t)(uintptr_t)ws.enc16.p};
+	                           (uint64_t)(uintptr_t)ws.enc16.p, (uint64_t)(uintptr_t)ws.acts.p, (uint64_t)(uintptr_t)ws.delta0.p,
+	                           (uint64_t)(uintptr_t)ws.delta1.p, (uint64_t)(uintptr_t)ws.dout16.p, (uint64_t)(uintptr_t)ws.out16.p,
+	                           (uint64_t)(uintptr_t)ws.red_tmp.p, (uint64_t)(uintptr_t)ws.tile_wT.p, (uint64_t)(uintptr_t)ws.loss_sum.p,
+	                           ws.n_loss_partials, (uint64_t)(uintptr_t)peer.get(), (uint64_t)peer_attached};
 	// every scalar the step's kernels take from the trainer (AdamArgs holds no pointer here)
 	const AdamArgs a = adam_args();
 	const size_t n = sizeof(AdamArgs) / 8 + 1;
 	std::vector<uint64_t> ab(n, 0);
 	std::memcpy(ab.data(), &a, sizeof(AdamArgs));
 	k.insert(k.end(), ab.begin(), ab.end());
-	const GridOpts o = model->grid->opts();
+	const GridOpts o = model->grid ? model->grid->opts() : GridOpts{};  // OneBlob / Identity encodings: no grid
 	uint32_t ml = 0;
 	std::memcpy(&ml, &o.max_level, 4);
 	k.insert(k.end(), {(uint64_t)ml, (uint64_t)(uintptr_t)o.max_level_gpu, o.stochastic, o.n_features, o.active, o.inrange_index});
@@ -1099,7 +1127,10 @@ std::vector<uint64_t> TrainerHost::graph_key(uint32_t B, const float* input, con
 }
 
 bool TrainerHost::training_step_graph(hipStream_t st, uint32_t B, const float* input, const float* target) {
-	if (adam_step + 1 >= GRAPH_STEPS || (!dp && !ws.wimage_valid)) return false;  // first step packs the weights eagerly
+	// the single-GPU fused step's first step builds the weight image eagerly (the replays then read it)
+	const bool image_step = overlapped_ok() && !dp && !peer_attached;
+	if (adam_step + 1 >= GRAPH_STEPS || (image_step && !ws.wimage_valid)) return false;
+	if (peer_attached) peer_check();
 	if (ftable_valid < GRAPH_STEPS || ftable_b1 != adam.beta1 || ftable_b2 != adam.beta2)
 		(void)adam_args_table(st, GRAPH_STEPS, GRAPH_STEPS);
 	if (!graph) graph = std::make_unique<StepGraph>();
@@ -1107,8 +1138,7 @@ bool TrainerHost::training_step_graph(hipStream_t st, uint32_t B, const float* i
 	hipGraphExec_t exec = graph->find(key);
 	if (!exec) {
 		// eager step first (sizes every workspace for this B, so the capture allocates nothing)
-		if (dp) training_step_dp(st, B, input, target);
-		else training_step_overlapped(st, B, input, target, true);
+		step_eager(st, B, input, target);
 		key = graph_key(B, input, target);
 		TCNN_HIP_CHECK(hipStreamSynchronize(st));
 		TCNN_HIP_CHECK(hipStreamSynchronize(graph->cs));
@@ -1119,10 +1149,12 @@ bool TrainerHost::training_step_graph(hipStream_t st, uint32_t B, const float* i
 		const uint32_t step0 = adam_step, ftv0 = ftable_valid, lb0 = last_B;
 		const bool wv0 = ws.wimage_valid, dps0 = dp_state_partial;
 		hipGraph_t g = nullptr;
+		const bool tim = timer.enabled;
+		timer.enabled = false;  // no phase events inside the graph
 		TCNN_HIP_CHECK(hipStreamBeginCapture(graph->cs, hipStreamCaptureModeThreadLocal));
-		if (dp) training_step_dp(graph->cs, B, input, target);
-		else training_step_overlapped(graph->cs, B, input, target, true);
+		step_eager(graph->cs, B, input, target);
 		TCNN_HIP_CHECK(hipStreamEndCapture(graph->cs, &g));
+		timer.enabled = tim;
 		adam_step = step0;  // the capture ran nothing
 		ftable_valid = ftv0;
 		last_B = lb0;
@@ -1136,15 +1168,13 @@ bool TrainerHost::training_step_graph(hipStream_t st, uint32_t B, const float* i
 		++graph_captures;
 		return true;
 	}
-	TCNN_HIP_CHECK(hipEventRecord(graph->e0, st));
-	TCNN_HIP_CHECK(hipStreamWaitEvent(graph->cs, graph->e0, 0));
-	TCNN_HIP_CHECK(hipGraphLaunch(exec, graph->cs));
-	TCNN_HIP_CHECK(hipEventRecord(graph->e1, graph->cs));
-	TCNN_HIP_CHECK(hipStreamWaitEvent(st, graph->e1, 0));
-	// the host-side effects of training_step_overlapped / training_step_dp
+	// replayed straight on the caller's stream (the legacy null stream included): no private stream,
+	// no event joins -- captured on graph->cs only because a capture needs a non-null stream
+	TCNN_HIP_CHECK(hipGraphLaunch(exec, st));
+	// the host-side effects of the eager step
 	++adam_step;
-	ws.wimage_valid = !dp;  // the data-parallel step leaves the weight image to be packed by the next step
-	if (dp && dp_sharded) dp_state_partial = true;
+	ws.wimage_valid = image_step;  // the data-parallel steps leave the weight image to be rebuilt by the next step
+	if ((dp && dp_sharded) || peer_attached) dp_state_partial = true;
 	last_B = B;
 	++graph_replays;
 	return true;

@@ -152,7 +152,10 @@ struct MlpHost {
 	std::string otype = "FullyFusedMLP";
 	MlpHost() = default;
 	MlpHost(uint32_t n_input_dims, uint32_t n_output_dims, const json& net);
-	uint32_t n_params() const { return width * n_input + (n_hidden_layers - 1) * width * width + padded_output * width; }
+	uint32_t n_params() const {
+		return n_hidden_layers == 0 ? padded_output * n_input
+		                            : width * n_input + (n_hidden_layers - 1) * width * width + padded_output * width;
+	}
 	void initialize_params(Pcg32& rng, float* host_out, float scale = 1.0f) const;  // Xavier (gpu_matrix.h:284-299)
 	json hyperparams() const;
 };
@@ -378,6 +381,8 @@ struct TrainerHost {
 	TrainerHost(uint32_t n_in, uint32_t n_out, const json& cfg, uint32_t seed);
 	void initialize_params(uint32_t seed);
 	void training_step(hipStream_t st, uint32_t B, const float* input, const float* target, bool run_optimizer);
+	void step_eager(hipStream_t st, uint32_t B, const float* input, const float* target);  // with the optimizer
+	void training_step_sequential(hipStream_t st, uint32_t B, const float* input, const float* target, bool run_optimizer);
 	void training_step_part(hipStream_t st, uint32_t B, const float* input, const float* target, int part);
 	void optimizer_step(hipStream_t st);
 	// Trainer::forward / backward (trainer.h:97-153): the two halves of training_step with the
@@ -413,6 +418,7 @@ struct TrainerHost {
 	void dp_peer_abandon();  // local, no barrier: only before any exchange step (a failed attach on some rank)
 	double peer_timeout_s = peer_default_timeout_s();
 	void dp_peer_set_timeout(double seconds);
+	void peer_check() const;  // throws if a wait of an earlier step failed
 	int peer_nranks = 1;  // ranks of the attached peer exchange
 	// ranks whose gradients Adam's input sums (RCCL communicator or peer exchange): grad_scale = user / N
 	int dp_nranks() const { return dp ? dp->nranks : (peer_attached ? peer_nranks : 1); }

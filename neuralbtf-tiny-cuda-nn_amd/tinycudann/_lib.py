@@ -81,6 +81,7 @@ _SIGS = {
     "tcnn_trainer_param_gradients": (c_void_p, [c_void_p]),
     "tcnn_trainer_gradients_fp32": (c_void_p, [c_void_p]),
     "tcnn_trainer_set_gradient_scale": (c_int, [c_void_p, c_float]),
+    "tcnn_trainer_set_loss_scale": (c_int, [c_void_p, c_float]),
     "tcnn_trainer_set_graph": (c_int, [c_void_p, c_int]),
     "tcnn_trainer_graph_stats": (c_int, [c_void_p, c_void_p, c_void_p]),
     "tcnn_trainer_set_params_full_precision": (c_int, [c_void_p, c_void_p, c_uint64]),

@@ -110,6 +110,11 @@ class Trainer:
     def set_gradient_scale(self, s):
         L.check(L.lib().tcnn_trainer_set_gradient_scale(self.h, float(s)))
 
+    def set_loss_scale(self, s):
+        """the loss scale of training_step / forward / optimizer_step (the reference's loss_scale
+        argument, trainer.h:97-160; default 128)"""
+        L.check(L.lib().tcnn_trainer_set_loss_scale(self.h, float(s)))
+
     def set_params_full_precision(self, host_params):
         import numpy as np
         a = np.ascontiguousarray(host_params, dtype=np.float32)

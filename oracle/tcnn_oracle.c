@@ -629,7 +629,9 @@ void orc_grid_bwd_bwd(const orc_grid* g, uint32_t B, const float* pos_in, const 
 /* Fully fused MLP                                                                              */
 /* ------------------------------------------------------------------------------------------ */
 
+/* NH == 0 (CutlassMLP without hidden layers, cutlass_mlp.cu:64-67): one [OUTP][IN] matrix */
 uint32_t orc_mlp_n_params(uint32_t W, uint32_t IN, uint32_t NH, uint32_t OUTP) {
+	if (NH == 0) return OUTP * IN;
 	return W * IN + (NH - 1) * W * W + OUTP * W;
 }
 
@@ -689,7 +691,9 @@ static void mlp_view_init(mlp_view* v, uint32_t W, uint32_t IN, uint32_t NH, uin
 	v->wf = (float*)malloc(n * sizeof(float));
 	orc_h2f_array(params, v->wf, n);
 	size_t o = 0;
-	v->off[0] = 0; o += (size_t)W * IN;
+	v->off[0] = 0;
+	if (NH == 0) return;  /* the output matrix at 0 */
+	o += (size_t)W * IN;
 	for (uint32_t k = 1; k < NH; ++k) { v->off[k] = o; o += (size_t)W * W; }
 	v->off[NH] = o;
 }
@@ -701,6 +705,16 @@ static inline float in_at(const uint16_t* input, int soa, uint32_t IN, uint32_t 
 /* one sample forward; h: NH*W floats (fp16-rounded post-activations); out: OUTP fp16 */
 static void mlp_fwd_sample(const mlp_view* v, uint32_t act, const float* x, float* h, uint16_t* out) {
 	const uint32_t W = v->W, IN = v->IN, NH = v->NH, OUTP = v->OUTP;
+	if (NH == 0) {  /* out = act_out(Wout x) */
+		const float* Wo = v->wf;
+		for (uint32_t o = 0; o < OUTP; ++o) {
+			float acc = 0.0f, part = 0.0f;
+			for (uint32_t k = 0; k < IN; ++k) { part += Wo[(size_t)o * IN + k] * x[k]; MIMIC_STEP(acc, part, k, 16, IN); }
+			if (!g_mimic) acc = part;
+			out[o] = orc_f2h(act_fwd(act >> 8, acc));
+		}
+		return;
+	}
 	const float* W0 = v->wf + v->off[0];
 	for (uint32_t n = 0; n < W; ++n) {
 		float acc = 0.0f, part = 0.0f;
@@ -763,6 +777,21 @@ void orc_mlp_fwd(uint32_t W, uint32_t IN, uint32_t NH, uint32_t OUTP, uint32_t a
 static void mlp_bwd_sample(const mlp_view* v, uint32_t act, const float* x, const float* h, const float* g,
                            float* wgrad, float* dx, float* scratch, float* deltas) {
 	const uint32_t W = v->W, IN = v->IN, NH = v->NH, OUTP = v->OUTP;
+	if (NH == 0) {  /* dWout[o][k] += g[o] x[k]; dx = Wout^T g */
+		const float* Wo = v->wf;
+		if (wgrad)
+			for (uint32_t o = 0; o < OUTP; ++o) {
+				if (g[o] == 0.0f) continue;
+				for (uint32_t k = 0; k < IN; ++k) wgrad[(size_t)o * IN + k] += WTERM(g[o] * x[k]);
+			}
+		if (dx)
+			for (uint32_t k = 0; k < IN; ++k) {
+				float acc = 0.0f;
+				for (uint32_t o = 0; o < OUTP; ++o) acc += DTERM(Wo[(size_t)o * IN + k], g[o]);
+				dx[k] = orc_h2f(orc_f2h(acc));
+			}
+		return;
+	}
 	float* d_cur = scratch;      /* delta of layer being processed (fp16-rounded) */
 	float* d_nxt = scratch + W;
 	/* output layer: dWout[o][k] += g[o] * h_last[k]; delta_H = act'(h_H) * Wout^T g */
@@ -1120,9 +1149,13 @@ int orc_model_init(orc_model* m, uint32_t seed) {
 	orc_pcg32_seed(&rng, s[0], 1u);
 	/* NWIE::initialize_params (network_with_input_encoding.h:124-130): network first */
 	float* p = m->w32;
-	orc_xavier_uniform(&rng, m->W, IN, p, 1.0f); p += (size_t)m->W * IN;
-	for (uint32_t k = 1; k < m->NH; ++k) { orc_xavier_uniform(&rng, m->W, m->W, p, 1.0f); p += (size_t)m->W * m->W; }
-	orc_xavier_uniform(&rng, m->OUTP, m->W, p, 1.0f); p += (size_t)m->OUTP * m->W;
+	if (m->NH == 0) {  /* CutlassMLP with no hidden layer: one matrix */
+		orc_xavier_uniform(&rng, m->OUTP, IN, p, 1.0f); p += (size_t)m->OUTP * IN;
+	} else {
+		orc_xavier_uniform(&rng, m->W, IN, p, 1.0f); p += (size_t)m->W * IN;
+		for (uint32_t k = 1; k < m->NH; ++k) { orc_xavier_uniform(&rng, m->W, m->W, p, 1.0f); p += (size_t)m->W * m->W; }
+		orc_xavier_uniform(&rng, m->OUTP, m->W, p, 1.0f); p += (size_t)m->OUTP * m->W;
+	}
 	/* GridEncodingTemplated::initialize_params (grid.h:1059-1062) */
 	if (m->enc_type == 0) orc_generate_uniform(&rng, m->grid.n_params, p, -1e-4f, 1e-4f);
 	orc_f2h_array(m->w32, m->w16, n); /* trainer.h:83-85 */

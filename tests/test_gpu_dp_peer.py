@@ -56,13 +56,18 @@ def _worker(rank, world, port, B, q, cfg_name="hash"):
     lo, hi = shard_bounds(B, rank, world)
     cfg = _cfg(cfg_name)
 
-    def run(**kw):
+    def run(graph=False, **kw):
         tr = Trainer(2, 3, cfg, seed=1337)
         dp = DataParallelTrainer(tr, **kw)
+        tr.set_graph(graph)
         losses = []
+        pos_d = torch.empty(hi - lo, 2, device="cuda")  # fixed buffers refilled in place (graphs key on pointers)
+        tgt_d = torch.empty(hi - lo, 3, device="cuda")
         for s in range(4):
             pos_s, tgt_s = make_batch(B, step=s)
-            dp.training_step(torch.from_numpy(pos_s[lo:hi]).cuda(), torch.from_numpy(tgt_s[lo:hi]).cuda())
+            pos_d.copy_(torch.from_numpy(pos_s[lo:hi]))
+            tgt_d.copy_(torch.from_numpy(tgt_s[lo:hi]))
+            dp.training_step(pos_d, tgt_d)
             losses.append(tr.loss())
         dp.gather_state()
         torch.cuda.synchronize()
@@ -70,7 +75,15 @@ def _worker(rank, world, port, B, q, cfg_name="hash"):
         return tr, dp, a["w32"], a["w16"], bytes(tr.serialize(optimizer=True)), losses
 
     _, _, w_ref, h_ref, snap_ref, l_ref = run(exchange="torch")  # replicated all-reduce (gloo), overlapped
+    graph_same = True
+    if world == 2 and cfg_name == "hash":  # the peer step replayed as a hipGraph: bit-identical to eager
+        trg, dpg, w_g, h_g, snap_g, l_g = run(graph=True, exchange="peer", peer_fallback=False, peer_timeout_s=60)
+        assert trg.graph_stats()[1] >= 2, trg.graph_stats()
+        dpg.close()
+        del trg, dpg
     tr, dp, w_peer, h_peer, snap_peer, l_peer = run(exchange="peer", peer_fallback=False, peer_timeout_s=60)
+    if world == 2 and cfg_name == "hash":
+        graph_same = bool(np.array_equal(w_g, w_peer) and np.array_equal(h_g, h_peer) and snap_g == snap_peer and l_g == l_peer)
     assert tr.engine == ("fused" if cfg_name != "oneblob_cutlass" else "layered")
     # detach (collective), then this rank trains on alone from the gathered state
     dp.close()
@@ -78,7 +91,7 @@ def _worker(rank, world, port, B, q, cfg_name="hash"):
     tr.training_step(torch.from_numpy(pos_s[lo:hi]).cuda(), torch.from_numpy(tgt_s[lo:hi]).cuda())
     torch.cuda.synchronize()
     after = trainer_arrays(tr)["w32"]
-    q.put((rank, w_ref, h_ref, snap_ref, l_ref, w_peer, h_peer, snap_peer, l_peer, bool(np.isfinite(after).all())))
+    q.put((rank, w_ref, h_ref, snap_ref, l_ref, w_peer, h_peer, snap_peer, l_peer, bool(np.isfinite(after).all()), graph_same))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -103,8 +116,8 @@ def test_peer_exchange_equals_allreduce(world, cfg_name):
         p.join(timeout=60)
         assert p.exitcode == 0
     for r in res:
-        _, w_ref, h_ref, snap_ref, l_ref, w_peer, h_peer, snap_peer, l_peer, finite = r
-        assert finite
+        _, w_ref, h_ref, snap_ref, l_ref, w_peer, h_peer, snap_peer, l_peer, finite, graph_same = r
+        assert finite and graph_same
         if world == 2:
             np.testing.assert_array_equal(w_peer, w_ref)
             np.testing.assert_array_equal(h_peer, h_ref)
@@ -152,6 +165,9 @@ def _worker8(rank, world, port, B, q):
     dp.close()
     if rank == 0:  # the single-process step on the whole 2^18 batch (same seed, same batch)
         ref = Trainer(2, 3, CONFIG_HASH, seed=1337)
+        # loss scale 8 x 128: the per-sample fp16 dL/dy (loss_scale * 2 (p - t) / (p^2 + 0.01) / (B dims)) is
+        # then the shards' bit for bit, so every fp16 intermediate of every sample matches too
+        ref.set_loss_scale(128.0 * world)
         pos_s, tgt_s = make_batch(B, step=0)
         p, t = torch.from_numpy(pos_s).cuda(), torch.from_numpy(tgt_s).cuda()
         ref.training_step(p, t, run_optimizer=False)
@@ -170,15 +186,17 @@ def test_peer_exchange_8_ranks_equals_single_gpu_step():
     summed gradient of the first step equals the single-process 2^18 step's (N GPUs x B/N
     = 1 GPU x B within summation-order tolerance).
 
-    Tolerance, per element: each rank's loss normalises by its own B/8 * dims, so the shards' fp16
-    loss-scaled dL/dy are exactly 8x the single step's (a power of two; neither side is subnormal at the
-    initial outputs ~1e-5 against targets ~0.5) and every per-sample term of the network gradient is the
-    same up to that factor: what differs is the fp32 summation order (8 shard sums of 2^15 terms + one
-    8-term sum vs 2^18 terms) -- bounded by 2^-20 * sum|terms| (relative 1e-6 of the gradient scale here)
-    -- and, in the grid, the per-chunk int32 fixed-point steps (2^-31 of the chunk's sum |dL/dy| per
-    update, 8x finer chunks on the shards). Checked as |g_peer / 8 - g_single| <= 1e-5 |g_single| +
-    1e-6 max|g| per part (network, grid), and Adam's first update agrees wherever the gradients round to
-    the same fp16 value (elsewhere step 1 of Adam moves by +-lr sign(g) and may legitimately differ)."""
+    Each rank's loss normalises by its own B/8 * dims, so the shards' loss-scaled dL/dy are 8x those of
+    a single 2^18 step at the same loss scale -- and 8x smaller values meet fp16's subnormal range
+    sooner (measured: 8.5e-4 relative on a grid entry). The single step therefore runs at loss scale
+    8 x 128: its per-sample fp16 dL/dy are then the shards' bit for bit, and so is every fp16
+    intermediate downstream (hidden deltas, dL/d(encoding)). What is left is the order of the fp32
+    sums (8 shard sums + one 8-term sum vs one 2^18-point sum) and, in the grid, the per-chunk int32
+    fixed-point steps (2^-31 of a chunk's sum |dL/dy| per update). Bound per element: the oracle's
+    per-element trainer bound at this batch (helpers.trainer_grad_bounds: 8 fp16 ulps of the
+    abs-backprop magnitude of every term + the grid's fixed-point bound), scaled by the loss scale --
+    far above both effects, and far below a missing or doubled shard. Adam's first update (which
+    divides by the loss scale) must agree wherever the two fp16 gradients it reads are equal."""
     import torch.multiprocessing as mp
     world, B = 8, 1 << 18
     ctx = mp.get_context("spawn")
@@ -194,24 +212,30 @@ def test_peer_exchange_8_ranks_equals_single_gpu_step():
     for r in range(1, world):  # replicas bit-identical after 1 and 3 steps
         np.testing.assert_array_equal(res[0]["w16_1"], res[r]["w16_1"])
         np.testing.assert_array_equal(res[0]["w16_3"], res[r]["w16_3"])
-    ref = res[0]["ref_g32"].astype(np.float64)
+    ref = res[0]["ref_g32"].astype(np.float64)  # at loss scale 8 x 128
     n = ref.size
-    g = np.zeros(n)
+    g = np.zeros(n)  # the ranks' summed gradient (each shard's loss scale 128 over B/8 points)
     covered = np.zeros(n, bool)
     for r in range(world):
         plo, phi, gs = res[r]["g_shard"]
-        g[plo:phi] = gs.astype(np.float64) / world
+        g[plo:phi] = gs.astype(np.float64)
         covered[plo:phi] = True
     assert covered.all()
-    from helpers import CONFIG_HASH, O
-    W, NH = CONFIG_HASH["network"]["n_neurons"], CONFIG_HASH["network"]["n_hidden_layers"]
-    nm = O.mlp_n_params(W, 32, NH, 16)
-    for part in (slice(0, nm), slice(nm, n)):
-        d = np.abs(g[part] - ref[part])
-        bound = 1e-5 * np.abs(ref[part]) + 1e-6 * np.abs(ref[part]).max()
-        k = int(np.argmax(d / bound))
-        assert d[k] <= bound[k], (part, k, g[part][k], ref[part][k])
-    # Adam's first step: equal wherever the two gradients round to the same fp16 (the g16 Adam reads)
-    same16 = g.astype(np.float32).astype(np.float16) == ref.astype(np.float32).astype(np.float16)
-    assert same16.mean() > 0.99, same16.mean()
+    from helpers import CONFIG_HASH, O, make_batch, trainer_grad_bounds
+    nm = O.mlp_n_params(CONFIG_HASH["network"]["n_neurons"], 32, CONFIG_HASH["network"]["n_hidden_layers"], 16)
+    pos, tgt = make_batch(B, step=0)
+    mag, grid_bound = trainer_grad_bounds(CONFIG_HASH, res[0]["ref_w16_0"], pos, tgt, n_threads=16)
+    bound = np.concatenate([8 * 2.0 ** -10 * np.asarray(mag, np.float64) + 1e-6 * np.abs(ref[:nm]).max(),
+                            np.asarray(grid_bound, np.float64)]) * world
+    d = np.abs(g - ref)
+    r_el = np.where(d == 0, 0.0, d / np.maximum(bound, 1e-300))  # untouched grid entries: 0 on both sides
+    k = int(np.argmax(r_el))
+    assert r_el[k] <= 1.0, (k, g[k], ref[k], bound[k])
+    # Adam's first step: equal wherever the fp16 gradients it reads, divided by the loss scale, are equal
+    g16_peer = (g / world).astype(np.float32).astype(np.float16).astype(np.float64) / 128.0
+    g16_ref = ref.astype(np.float32).astype(np.float16).astype(np.float64) / (128.0 * world)
+    same16 = g16_peer == g16_ref
+    # they differ only where fp16(g / 8) is subnormal (the peer path's gradient scale 1/N applies before
+    # the reference's fp16 gradient rounding): 2.8 % of config_hash's grid entries at step 1
+    assert same16.mean() > 0.95, same16.mean()
     np.testing.assert_array_equal(res[0]["w16_1"][same16], res[0]["ref_w16_1"][same16])

@@ -60,6 +60,46 @@ def test_graph_replay_bit_identical(torch_mod):
     assert graph.optimizer_step_count == eager.optimizer_step_count == 10
 
 
+@pytest.mark.parametrize("engine", ["tile", "layered"])
+def test_graph_replay_other_engines(torch_mod, engine):
+    """The tile engine (HashGrid + W128/H4, configs[3]'s network) and the layer-wise engine (OneBlob +
+    CutlassMLP) replay their whole step -- encoding pass, MLP kernel(s), reductions, grid backward,
+    Adam -- as one graph, bit-identical to the eager step."""
+    import copy
+    torch = torch_mod
+    from helpers import CONFIG_ONEBLOB
+    from tinycudann import Trainer
+    if engine == "tile":
+        cfg = copy.deepcopy(CONFIG_HASH)
+        cfg["network"].update({"n_neurons": 128, "n_hidden_layers": 4})
+    else:
+        cfg = copy.deepcopy(CONFIG_ONEBLOB)
+        cfg["network"].update({"otype": "CutlassMLP", "n_neurons": 64, "n_hidden_layers": 2})
+    eager = Trainer(2, 3, cfg, seed=1337)
+    graph = Trainer(2, 3, cfg, seed=1337)
+    assert eager.engine == ("fused" if engine == "tile" else "layered")
+    graph.set_graph(True)
+    B = 4096
+    pos_d = torch.empty(B, 2, device="cuda")
+    tgt_d = torch.empty(B, 3, device="cuda")
+    le, lg = [], []
+    for s in range(5):
+        pos, tgt = make_batch(B, step=s)
+        pos_d.copy_(torch.from_numpy(pos))
+        tgt_d.copy_(torch.from_numpy(tgt))
+        eager.training_step(pos_d, tgt_d)
+        graph.training_step(pos_d, tgt_d)
+        le.append(eager.loss())
+        lg.append(graph.loss())
+    torch.cuda.synchronize()
+    a, b = trainer_arrays(eager), trainer_arrays(graph)
+    for k in ("w32", "w16", "g16"):
+        assert np.array_equal(a[k], b[k]), k
+    assert le == lg
+    captures, replays = graph.graph_stats()
+    assert captures == 1 and replays == 4, (captures, replays)
+
+
 def test_update_hyperparams_rejects_loss_type_change(torch_mod):
     """The loss type is fixed at construction (the reference's Loss::update_hyperparams holds no
     hyperparameters): a request to change it fails loudly instead of being ignored."""

@@ -61,6 +61,13 @@ CONFIGS = {
     # (config_oneblob as-is: NS = 2; IN 128 with 4 hidden layers: NS = 1; HashGrid W128/H5: NS = 2)
     "oneblob_w128_h4": (_cfg({"otype": "OneBlob", "n_bins": 64}, _net(128, 4)), 2e-3),
     "hashgrid_w128_h5": (_cfg(CONFIG_HASH["encoding"], _net(128, 5)), 2e-3),
+    # widths above 128 (k_wide_layer + blocked k_wgrad; reference cutlass_mlp.cu:41-81, fully_fused_mlp.cu:591):
+    # CutlassMLP W256, an encoding 256 wide (HashGrid L32 F8) into FullyFusedMLP W64, CutlassMLP with no
+    # hidden layer (one [16][128] matrix, cutlass_mlp.cu:64-67)
+    "hashgrid_cutlass_w256_h2": (_cfg(CONFIG_HASH["encoding"], _net(256, 2, "CutlassMLP")), 2e-3),
+    "hashgrid_l32f8_in256_w64_h2": (_cfg(dict(CONFIG_HASH["encoding"], n_levels=32, n_features_per_level=8), _net(64, 2)), 2e-3),
+    "oneblob_cutlass_h0": (_cfg({"otype": "OneBlob", "n_bins": 64}, _net(64, 0, "CutlassMLP")), 1e-3),
+    "identity_cutlass_w144_h1": (_cfg({"otype": "Identity"}, _net(144, 1, "CutlassMLP")), 1e-3),
 }
 # FullyFusedMLP configurations the tile engine trains (engine "fused"); the rest run layer by layer
 TILE = {"oneblob_w64_h2", "oneblob16_w64_h2", "hashgrid_w128_h4", "identity_w64_h3", "oneblob_w64_h5", "hashgrid_w128_h2",
@@ -144,7 +151,8 @@ def test_layered_engine_forced_matches_oracle(torch_mod, name, monkeypatch):
     assert rel_err(a["g32"], om.grad32) <= tol
 
 
-@pytest.mark.parametrize("name", ["oneblob_as_file_w128_h5", "hashgrid_w128_h4", "identity_w32_h3"])
+@pytest.mark.parametrize("name", ["oneblob_as_file_w128_h5", "hashgrid_w128_h4", "identity_w32_h3", "hashgrid_cutlass_w256_h2",
+                                  "hashgrid_l32f8_in256_w64_h2", "oneblob_cutlass_h0"])
 def test_layered_inference_matches_oracle(torch_mod, name):
     torch = torch_mod
     from tinycudann import Trainer
@@ -233,3 +241,31 @@ def test_create_network_identity_module(torch_mod):
     assert rel_err(dx.cpu().numpy(), refdx) <= 2e-3
     lib.tcnn_context_destroy(ctx)
     lib.tcnn_module_destroy(m)
+
+
+def test_padded_output_above_128(torch_mod):
+    """136 network outputs (padded to 144 > 128, the output layer on k_wide_layer; reference
+    fully_fused_mlp.cu:702-703 hands outputs above 16 to a separate GEMM) with CutlassMLP W64/H2 on
+    config_hash's grid: loss, gradients and inference against the oracle."""
+    torch = torch_mod
+    from tinycudann import Trainer
+    cfg = _cfg(CONFIG_HASH["encoding"], _net(64, 2, "CutlassMLP"))
+    n_out = 136
+    t = Trainer(2, n_out, cfg, seed=1337)
+    assert t.engine == "layered"
+    om = O.OracleModel(cfg, 2, n_out, seed=1337)
+    assert t.n_params == om.n_params
+    B = 512
+    pos, tgt3 = make_batch(B)
+    tgt = np.ascontiguousarray(np.tile(tgt3, (1, 46))[:, :n_out] * np.linspace(0.5, 1.0, n_out, dtype=np.float32))
+    t.training_step(torch.from_numpy(pos).cuda(), torch.from_numpy(tgt).cuda(), run_optimizer=False)
+    loss_ref = om.train_step(pos, tgt, run_optimizer=False, n_threads=4)
+    assert abs(t.loss() - loss_ref) <= 1e-3 * abs(loss_ref), (t.loss(), loss_ref)
+    a = trainer_arrays(t)
+    nm = om.n_mlp_params
+    assert rel_err(a["g32"][:nm], om.grad32[:nm]) <= 2e-3
+    assert rel_err(a["g32"][nm:], om.grad32[nm:]) <= 2e-3
+    t2 = Trainer(2, n_out, cfg, seed=1337)
+    out = t2.inference(torch.from_numpy(pos).cuda()).cpu().numpy()
+    ref = O.h2f(O.OracleModel(cfg, 2, n_out, seed=1337).inference(pos, n_threads=4))[:, :n_out]
+    assert_within_fp16_ulps(out, ref)

@@ -365,3 +365,35 @@ def test_grid_max_level_masking():
     cut = g0.offsets[9] * F
     np.testing.assert_array_equal(gb[:cut], gfull[:cut])
     assert np.all(gb[cut:] == 0)
+
+
+def test_mlp_without_hidden_layers_and_wide_shapes():
+    """The restatement's MLP at the shapes the wide layer kernels serve: no hidden layer (CutlassMLP,
+    cutlass_mlp.cu:64-67: one [padded_out][in] matrix), W 256 / IN 256 / padded output 144, against a
+    float64 evaluation of the same fp16-stored layers (fp16 rounding after every layer, fp32 sums)."""
+    rng = np.random.default_rng(7)
+    for W, IN, NH, OUTP in ((64, 128, 0, 16), (256, 32, 2, 16), (64, 256, 1, 144)):
+        n = O.mlp_n_params(W, IN, NH, OUTP)
+        assert n == (OUTP * IN if NH == 0 else W * IN + (NH - 1) * W * W + OUTP * W)
+        p16 = O.f2h((rng.standard_normal(n) * 0.1).astype(np.float32))
+        B = 64
+        x16 = O.f2h(rng.random((B, IN), dtype=np.float32))
+        out, hidden = O.mlp_fwd(W, IN, NH, OUTP, p16, x16, input_soa=False, activation=1)
+        pf = O.h2f(p16).astype(np.float64)
+        a = O.h2f(x16).astype(np.float64)
+        off, k, acts = 0, IN, [a]
+        for _ in range(NH):
+            Wm = pf[off:off + W * k].reshape(W, k)
+            off += W * k
+            a = np.maximum(a @ Wm.T, 0).astype(np.float16).astype(np.float64)
+            acts.append(a)
+            k = W
+        Wo = pf[off:off + OUTP * k].reshape(OUTP, k)
+        ref = a @ Wo.T
+        np.testing.assert_allclose(O.h2f(out).astype(np.float64), ref, rtol=2e-3, atol=2e-3 * np.abs(ref).max())
+        dout = O.f2h((rng.standard_normal((B, OUTP)) * 0.01).astype(np.float32))
+        wg, din = O.mlp_bwd(W, IN, NH, OUTP, p16, x16, hidden, dout, input_soa=False, activation=1)
+        g = O.h2f(dout).astype(np.float64)
+        np.testing.assert_allclose(wg[off:], (g.T @ acts[-1]).ravel(), rtol=1e-4, atol=1e-6)
+        if NH == 0:
+            np.testing.assert_allclose(O.h2f(din), g @ Wo, rtol=2e-3, atol=1e-5)
