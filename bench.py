@@ -34,8 +34,13 @@ MLP_TRAIN_FLOP_PER_SAMPLE = 43008
 GRID_BWD_BYTES_PER_SAMPLE = 584
 PHASES = ["fused_grid_mlp_fwd_loss_bwd", "grid_bwd_with_network_adam_tail", "adam_grid_slab_sums", "loss_sum"]
 ADAM_BYTES_PER_PARAM = 36  # Adam's fp32 master/m/v/step + fp16 grad/weight traffic
-PROFILE_EVERY = 25  # phase events on every 25th timed step (each event record idles the GPU ~6 us, ~4 records per
-# sampled step: every 10th step cost the measured step ~2.4 us; every 25th ~1 us)
+# Per-kernel phase times come from hipEvents the trainer records on its stream (tcnn_trainer_profile_*)
+# during a profiled pass of PHASE_STEPS steps run right after the timed region, events on every
+# PHASE_EVERY-th step: each event record idles the GPU ~6 us (~5 records per sampled step), so events
+# inside the timed region would bias `value` (r04: every 25th timed step, i.e. ONE sampled step in the
+# driver's 20-step run -- VERDICT r04 weak item 8)
+PHASE_STEPS = 100
+PHASE_EVERY = 2
 
 
 def rgb_field_torch(pos):
@@ -271,8 +276,6 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    if not args.no_profile:
-        L.check(L.lib().tcnn_trainer_profile_begin_sampled(trainer.h, PROFILE_EVERY))
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -289,11 +292,20 @@ def main():
 
     phase_ms = None
     if not args.no_profile:
+        # the profiled pass: the same step on the same batches, events on every PHASE_EVERY-th step
+        L.check(L.lib().tcnn_trainer_profile_begin_sampled(trainer.h, PHASE_EVERY))
+        for i in range(PHASE_STEPS):
+            step(i)
+        torch.cuda.synchronize()
         ms = (ctypes.c_double * len(PHASES))()
         nst = ctypes.c_uint32(0)
         L.check(L.lib().tcnn_trainer_profile_end(trainer.h, ms, len(PHASES), ctypes.byref(nst)))
         phase_ms = {PHASES[k]: ms[k] for k in range(len(PHASES))}
         phase_ms["sampled_steps"] = nst.value
+        phase_ms["source"] = (f"hipEvents on the trainer's stream, every {PHASE_EVERY}th step of a {PHASE_STEPS}-step "
+                              "pass right after the timed region (events inside it would bias value)")
+        if world > 1:
+            dist.barrier()
 
     loss = trainer.loss()
     if rank != 0:

@@ -270,6 +270,10 @@ const char* tcnn_trainer_hyperparams(tcnn_trainer* t);
 /* Trainer::initialize_params (trainer.h:68-87): re-seed pcg32{seed_seq{seed}[0]}, re-initialise every
  * parameter, zero the optimizer state and its step counter. */
 int tcnn_trainer_initialize_params(tcnn_trainer* t, uint32_t seed);
+/* Trainer::initialize_params from the caller's pcg32 {state, inc} (the reference's m_rng, trainer.h:67-85,
+ * which keeps advancing across re-initialisations): draws the n_params initial values from it and
+ * returns the advanced state (by n_params) in *state. */
+int tcnn_trainer_initialize_params_rng(tcnn_trainer* t, uint64_t* state, uint64_t inc);
 /* Engine diagnostics: name of the path the trainer runs ("fused" / "layered" / "unsupported"), for
  * training and for network->inference ("fused": the whole MLP in one launch). */
 const char* tcnn_trainer_engine(const tcnn_trainer* t);

@@ -119,12 +119,15 @@ public:
 		ctx->owner = this;
 		ctx->step = ++m_n_steps;
 		const float* in = detail::engine_input(stream, input, ctx->input_f32);
-		if (m_perturbation_sigma > 0 && !external_dL_dy) {
-			// trainer.h:114-123: logistic noise (m_rng) added to the output; the loss and dL/dy see the
-			// perturbed output, the context's output stays unperturbed
+		if (m_perturbation_sigma > 0) {
+			// trainer.h:114-123: logistic noise (m_rng) drawn on every forward -- with an external dL/dy too,
+			// so the generator advances as the reference's -- and added to the output; the loss and dL/dy see
+			// the perturbed output, the context's output stays unperturbed
 			const size_t n_el = (size_t)padded_output_width() * n;
 			m_perturbation.enlarge(n_el);
 			generate_random_logistic(stream, m_rng, n_el, m_perturbation.data(), 0.0f, m_perturbation_sigma);
+		}
+		if (m_perturbation_sigma > 0 && !external_dL_dy) {
 			ctx->h = tcnn_trainer_forward_perturbed(m_h, stream, n, in, target.data(), data_pdf ? data_pdf->data() : nullptr,
 			                                        m_perturbation.data(), prepare_input_gradients ? 1 : 0);
 		} else {
@@ -173,8 +176,11 @@ public:
 
 	// trainer.h:68-87
 	void initialize_params() {
-		detail::check_rc(tcnn_trainer_initialize_params(m_h, m_seed));
-		reset_rng();
+		// from m_rng, which keeps advancing (the reference re-initialises from its live generator, not
+		// from the seed): a second call draws new values, as the reference's does
+		uint64_t state = m_rng.state;
+		detail::check_rc(tcnn_trainer_initialize_params_rng(m_h, &state, m_rng.inc));
+		m_rng.advance((int64_t)n_params());
 		++m_n_steps;  // contexts of earlier steps no longer describe the parameters
 	}
 

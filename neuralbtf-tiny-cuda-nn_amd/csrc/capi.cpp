@@ -703,6 +703,16 @@ const char* tcnn_trainer_hyperparams(tcnn_trainer* t) {
 		return nullptr;
 	return g_str.c_str();
 }
+int tcnn_trainer_initialize_params_rng(tcnn_trainer* t, uint64_t* state, uint64_t inc) {
+	return guard([&] {
+		TCNN_CHECK(state != nullptr, "initialize_params_rng: null state");
+		Pcg32 rng;
+		rng.state = *state;
+		rng.inc = inc;
+		t->t->initialize_params_rng(rng);
+		*state = rng.state;
+	});
+}
 int tcnn_trainer_initialize_params(tcnn_trainer* t, uint32_t seed) {
 	return guard([&] { t->t->initialize_params(seed); });
 }

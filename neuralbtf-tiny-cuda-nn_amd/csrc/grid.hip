@@ -621,7 +621,7 @@ void launch_grid_bwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_
 	gl.dbg_times = nullptr;
 	gl.opts = go;
 	dim3 g(n_slices * n_chunks + n_tail);
-	if (dbg_grid_times()) gl.dbg_times = (unsigned long long*)g_dbg_times.get((size_t)g.x * 48);
+	if (dbg_grid_times()) gl.dbg_times = (unsigned long long*)g_dbg_times.get((size_t)g.x * 64);
 	const size_t lds = GRID_BWD_LDS_BYTES;
 	const _Float16* dy = (const _Float16*)dLdy16;
 	switch (D) {
@@ -632,26 +632,27 @@ void launch_grid_bwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_
 	}
 	TCNN_HIP_CHECK(hipGetLastError());
 	if (gl.dbg_times) {
-		std::vector<unsigned long long> t((size_t)g.x * 6);
+		std::vector<unsigned long long> t((size_t)g.x * 8);
 		TCNN_HIP_CHECK(hipStreamSynchronize(st));
 		TCNN_HIP_CHECK(hipMemcpy(t.data(), gl.dbg_times, t.size() * 8, hipMemcpyDeviceToHost));
 		unsigned long long t0 = ~0ull, t1 = 0;
-		for (uint32_t b = 0; b < g.x; ++b) { t0 = std::min(t0, t[6 * b]); t1 = std::max(t1, t[6 * b + 4]); }
+		for (uint32_t b = 0; b < g.x; ++b) { t0 = std::min(t0, t[8 * b]); t1 = std::max(t1, t[8 * b + 4]); }
 		fprintf(stderr, "grid_bwd: %u items x %u chunks + %u tail, span %.1f us\n", n_slices, n_chunks, n_tail, (t1 - t0) / 100.0);
 		for (uint32_t it = 0; it < n_slices; ++it) {
-			double sum = 0, mx = 0, st0 = 1e30, ph[4] = {0, 0, 0, 0}, ld = 0;
+			double sum = 0, mx = 0, st0 = 1e30, ph[4] = {0, 0, 0, 0}, ld = 0, zr = 0;
 			for (uint32_t c = 0; c < n_chunks; ++c) {
 				const uint32_t b = it * n_chunks + c;
-				const double d = (t[6 * b + 4] - t[6 * b]) / 100.0;
-				sum += d; mx = std::max(mx, d); st0 = std::min(st0, (t[6 * b] - t0) / 100.0);
-				for (int k = 0; k < 4; ++k) ph[k] += (t[6 * b + k + 1] - t[6 * b + k]) / 100.0 / n_chunks;
-					ld += ((double)t[6 * b + 5] - (double)t[6 * b]) / 100.0 / n_chunks;
+				const double d = (t[8 * b + 4] - t[8 * b]) / 100.0;
+				sum += d; mx = std::max(mx, d); st0 = std::min(st0, (t[8 * b] - t0) / 100.0);
+				for (int k = 0; k < 4; ++k) ph[k] += (t[8 * b + k + 1] - t[8 * b + k]) / 100.0 / n_chunks;
+					ld += ((double)t[8 * b + 5] - (double)t[8 * b]) / 100.0 / n_chunks;
+					zr += ((double)t[8 * b + 6] - (double)t[8 * b]) / 100.0 / n_chunks;
 			}
-			fprintf(stderr, "  item %2u: mean %.1f max %.1f us, first start +%.1f | prepass %.1f (zero+loads %.1f) accumulate %.1f merge %.1f write %.1f\n", it,
-			        sum / n_chunks, mx, st0, ph[0], ld, ph[1], ph[2], ph[3]);
+			fprintf(stderr, "  item %2u: mean %.1f max %.1f us, first start +%.1f | prepass %.1f (zero %.1f, +loads %.1f) accumulate %.1f merge %.1f write %.1f\n", it,
+			        sum / n_chunks, mx, st0, ph[0], zr, ld, ph[1], ph[2], ph[3]);
 		}
 		for (uint32_t b = n_slices * n_chunks; b < g.x; ++b)
-			fprintf(stderr, "  tail wg %u: %.1f us start +%.1f\n", b - n_slices * n_chunks, (t[6 * b + 4] - t[6 * b]) / 100.0, (t[6 * b] - t0) / 100.0);
+			fprintf(stderr, "  tail wg %u: %.1f us start +%.1f\n", b - n_slices * n_chunks, (t[8 * b + 4] - t[8 * b]) / 100.0, (t[8 * b] - t0) / 100.0);
 	}
 }
 

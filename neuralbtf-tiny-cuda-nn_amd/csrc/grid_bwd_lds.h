@@ -390,8 +390,8 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 	if (blockIdx.x >= n_items * n_chunks) {
 		grid_bwd_mlp_tail(ep, blockIdx.x - n_items * n_chunks, (float*)acc);
 		if (dbg_times && threadIdx.x == 0) {
-			dbg_times[6 * blockIdx.x] = t_start;
-			for (int k = 1; k < 5; ++k) dbg_times[6 * blockIdx.x + k] = wall_clock64();
+			dbg_times[8 * blockIdx.x] = t_start;
+			for (int k = 1; k < 5; ++k) dbg_times[8 * blockIdx.x + k] = wall_clock64();
 		}
 		return;
 	}
@@ -400,18 +400,9 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 	// config_hash) stay in that XCD's L2
 	const uint32_t item = blockIdx.x / n_chunks, chunk = blockIdx.x % n_chunks;
 	const GridSlice it = items[item];
-	const LevelInfo li = levels[it.level];
 	const uint32_t len = it.end - it.begin;
 	const uint32_t nf = it.nf, f0 = it.f0;
 	const Interp interp = (Interp)interp_u;
-	// Replicas: a small level's accumulators fit the LDS several times; wave w adds into replica
-	// w % R, which divides the same-address atomic serialisation on the coarse dense levels
-	// (level 0: 256 entries hit by every point) by up to R. Integer sums: the replica merge below is
-	// exact and order-independent.
-	const uint32_t slots = len * nf;  // int32 slots of one replica (F = 2 packed pairs: 2 per entry)
-	const uint32_t R = max(1u, min(16u, GRID_BWD_SLOTS / max(slots, 1u)));
-	for (uint32_t j = threadIdx.x; j < R * slots; j += blockDim.x) acc[j] = 0;
-	int* acc_w = acc + ((threadIdx.x >> 6) % R) * slots;
 	const uint32_t i0 = chunk * pts_per_chunk;
 	const uint32_t i1 = min(B, i0 + pts_per_chunk);
 
@@ -424,7 +415,9 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 	// D == 2, F <= 2 without grid options, and a chunk of at most GRID_BWD_PR points per thread (the
 	// config_hash step: 32768-point chunks): the chunk's dL/dy bits are loaded once, all of them in
 	// flight together, kept in registers for the accumulation, and the pre-pass is one load latency
-	// instead of one per 8 points.
+	// instead of one per 8 points. The loads are issued first -- they need only the item -- so the
+	// level table's load and the accumulators' zeroing run in their shadow (r05: at 2^15 points the
+	// item load -> level load -> zeroing -> dL/dy load chain was ~5 us of a 13 us item)
 	constexpr bool REGS_OK = D == 2 && F <= 2 && !OPTS;
 	const uint32_t n_pts = i1 > i0 ? i1 - i0 : 0u;
 	const bool use_regs = REGS_OK && n_pts <= GRID_BWD_THREADS * GRID_BWD_PR;
@@ -438,6 +431,22 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 				dyb[p] = i < i1 ? load_dy_bits<F>(layout, dLdy, dy_stride, it.level, B, i) : 0u;
 			}
 			load_pos_batch<D>(pos, pstride, i0, i1, 0, xs0);
+		}
+	}
+	const LevelInfo li = levels[it.level];
+	// Replicas: a small level's accumulators fit the LDS several times; wave w adds into replica
+	// w % R, which divides the same-address atomic serialisation on the coarse dense levels
+	// (level 0: 256 entries hit by every point) by up to R. Integer sums: the replica merge below is
+	// exact and order-independent.
+	const uint32_t slots = len * nf;  // int32 slots of one replica (F = 2 packed pairs: 2 per entry)
+	const uint32_t R = max(1u, min(16u, GRID_BWD_SLOTS / max(slots, 1u)));
+	const uint32_t nz = R * slots;
+	for (uint32_t j = 4 * threadIdx.x; j + 4 <= nz; j += 4 * blockDim.x) *(int4*)(acc + j) = int4{0, 0, 0, 0};  // ds_write_b128
+	for (uint32_t j = nz / 4 * 4 + threadIdx.x; j < nz; j += blockDim.x) acc[j] = 0;
+	if (dbg_times && threadIdx.x == 0) dbg_times[8 * blockIdx.x + 6] = wall_clock64();  // zeroing issued
+	int* acc_w = acc + ((threadIdx.x >> 6) % R) * slots;
+	if constexpr (REGS_OK) {
+		if (use_regs) {
 #pragma unroll
 			for (uint32_t p = 0; p < GRID_BWD_PR; ++p) {
 				float s = 0.0f;
@@ -472,7 +481,7 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 			}
 		}
 	}
-	if (dbg_times && threadIdx.x == 0) dbg_times[6 * blockIdx.x + 5] = wall_clock64() + (m != m ? 1 : 0);  // dL/dy loads done
+	if (dbg_times && threadIdx.x == 0) dbg_times[8 * blockIdx.x + 5] = wall_clock64() + (m != m ? 1 : 0);  // dL/dy loads done
 #pragma unroll
 	for (int o = 32; o > 0; o >>= 1) m += __shfl_xor(m, o);
 	if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
@@ -489,7 +498,7 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 		e = max(-126, min(e, 100));
 	}
 	const float scale = ldexpf(1.0f, e);
-	if (dbg_times && threadIdx.x == 0) dbg_times[6 * blockIdx.x + 1] = wall_clock64();  // zeroing + pre-pass done
+	if (dbg_times && threadIdx.x == 0) dbg_times[8 * blockIdx.x + 1] = wall_clock64();  // zeroing + pre-pass done
 
 	// uniform per item: index kind and accumulation mode
 	uint64_t full = 1;
@@ -518,7 +527,7 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 		grid_bwd_mode<D, F, H, IDX_GENERIC, OPTS>(mode, layout, B, pos, pstride, dLdy, dy_stride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, nf, i0, i1, scale, acc_w, o);
 	}
 	__syncthreads();
-	if (dbg_times && threadIdx.x == 0) dbg_times[6 * blockIdx.x + 2] = wall_clock64();  // accumulation done
+	if (dbg_times && threadIdx.x == 0) dbg_times[8 * blockIdx.x + 2] = wall_clock64();  // accumulation done
 	if (R > 1) {  // merge the replicas into replica 0
 		if (mode == 0) {
 			long long* a64 = (long long*)acc;
@@ -536,7 +545,7 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 		}
 		__syncthreads();
 	}
-	if (dbg_times && threadIdx.x == 0) dbg_times[6 * blockIdx.x + 3] = wall_clock64();  // replica merge done
+	if (dbg_times && threadIdx.x == 0) dbg_times[8 * blockIdx.x + 3] = wall_clock64();  // replica merge done
 	// write the chunk slab (GridSlabMap layout: this item's accumulators are one contiguous range)
 	const float inv = finite ? ldexpf(1.0f, -e) : __builtin_nanf("");
 	float* dst = partial + (size_t)chunk * partial_stride + (size_t)li.offset * F + (size_t)f0 * li.size + (size_t)it.begin * nf;
@@ -571,8 +580,8 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 		}
 	}
 	if (dbg_times && threadIdx.x == 0) {
-		dbg_times[6 * blockIdx.x] = t_start;
-		dbg_times[6 * blockIdx.x + 4] = wall_clock64();
+		dbg_times[8 * blockIdx.x] = t_start;
+		dbg_times[8 * blockIdx.x + 4] = wall_clock64();
 	}
 }
 

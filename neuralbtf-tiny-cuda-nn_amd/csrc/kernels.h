@@ -215,7 +215,9 @@ void fused_image_layout(uint32_t W, uint32_t IN, uint32_t NH, uint32_t* RSI, uin
 // out[c] = sum_j in[j*N + c] in block_column_sums order (G = 16 column blocks of 1024 threads):
 // the network-gradient reduction of the sequential path, identical to the grid-backward tail's
 void launch_column_sums(hipStream_t st, const float* in, uint32_t n_parts, uint32_t N, float* out);
-constexpr uint32_t MLP_TAIL_GROUPS = 16;
+// workgroups of the grid backward's network-gradient tail = column blocks of launch_column_sums (the
+// same G in both keeps the two reductions' summation order identical); TCNN_MLP_TAIL_GROUPS overrides
+uint32_t mlp_tail_groups();
 // out[p] = sum_j in[j*stride + grid_slab_index(map, p)] (the grid backward's slabs, fixed order)
 void launch_grid_slab_reduce(hipStream_t st, const float* in, uint32_t n_parts, uint32_t stride, uint32_t n, float* out,
                              const GridSlabMap* map, GradFinalize fin = {});

@@ -6,6 +6,8 @@
 //   k_relative_l2       standalone RelativeL2 (reference losses/relative_l2.h:40-76)
 #include "kernels.h"
 
+#include <cstdlib>
+
 #include "adam_device.h"
 #include "grid_device.h"
 #include "mlp_fused.h"
@@ -65,10 +67,19 @@ __global__ __launch_bounds__(1024) void k_column_sums(const float* __restrict__ 
 	for (uint32_t t = threadIdx.x; t < ncol; t += blockDim.x) out[c0 + t] = lds_cs[t];
 }
 
+uint32_t mlp_tail_groups() {
+	static const uint32_t g = [] {
+		const char* e = std::getenv("TCNN_MLP_TAIL_GROUPS");
+		const int v = e ? std::atoi(e) : 0;
+		return v > 0 && v <= 64 ? (uint32_t)v : 16u;
+	}();
+	return g;
+}
+
 void launch_column_sums(hipStream_t st, const float* in, uint32_t n_parts, uint32_t N, float* out) {
 	TCNN_CHECK(N % 4 == 0, "column sums: N must be a multiple of 4");
 	if (!N) return;
-	const uint32_t G = MLP_TAIL_GROUPS, cb = column_block(N, G);
+	const uint32_t G = mlp_tail_groups(), cb = column_block(N, G);
 	const uint32_t S = std::max(1u, 1024u / (cb / 4));
 	const size_t lds = (size_t)(cb + S * cb) * 4;
 	TCNN_CHECK(lds <= 64 * 1024, "column sums: column block too large");

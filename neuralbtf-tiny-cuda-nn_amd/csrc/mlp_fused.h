@@ -588,45 +588,58 @@ __device__ __forceinline__ void fused_slice(const FusedTrainArgs& a, uint32_t ba
 // Workgroup reduction of the per-wave dW / loss registers into this block's fp32 partial slab.
 // Deterministic pairwise tree over the waves through two LDS slabs (plain loads/stores: gfx950 LDS
 // float atomics are ~24x slower than integer ones and would make the order data-dependent).
+// The LDS slabs hold the accumulators in register order -- f4 j of lane l at floats 256 j + 4 l --
+// so every pass is one conflict-free ds_write_b128 / ds_read_b128 per f4 (r04 used the parameter
+// layout: scattered 4-byte accesses, 4-way bank conflicts, ~30 % of the kernel at 2^15 points,
+// profiles/r05_fused_phases.txt); the parameter order is applied once, by the global slab store.
+template <int W, int IN, int NH>
+__device__ __forceinline__ uint32_t wgrad_frag_to_param(uint32_t f) {
+	using L = FusedLayout<W, IN, NH>;
+	constexpr uint32_t NT = L::NT, NTI = L::NTI, NHM = L::NHM;
+	constexpr uint32_t oH = W * IN, oO = W * IN + NHM * W * W;
+	const uint32_t j = f / 256, rem = f % 256, lane = rem / 4, r = rem % 4, q = lane >> 4, c = lane & 15;
+	if (j < NT * NTI) {
+		const uint32_t mt = j / NTI, u = j % NTI, n = 16 * mt + 4 * q + r;
+		return n * IN + 16 * u + c;
+	}
+	if (j < NT * NTI + NHM * NT * NT) {
+		const uint32_t k = j - NT * NTI, jj = k / (NT * NT), mt = (k / NT) % NT, nt = k % NT, n = 16 * mt + 4 * q + r;
+		return oH + jj * W * W + n * W + 16 * nt + c;
+	}
+	const uint32_t nt = j - NT * NTI - NHM * NT * NT;
+	return oO + (4 * r + q) * W + 16 * nt + c;  // accumulator row 4q + r = output 4r + q
+}
+
 template <int W, int IN, int NH, int WAVES>
 __device__ __forceinline__ void block_reduce_wgrad(WgradAcc<W, IN, NH>& acc, float* slab, const FusedTrainArgs& a,
                                                    int tid, int wave, int lane) {
 	using L = FusedLayout<W, IN, NH>;
 	constexpr int NT = L::NT, NTI = L::NTI, NHM = L::NHM, N = L::N_MLP;
-	constexpr int oH = W * IN, oO = W * IN + NHM * W * W;
-	const int c = lane & 15, q = lane >> 4;
+	static_assert(N % 256 == 0, "whole f4 per lane");
 #pragma unroll
 	for (int off = 32; off > 0; off >>= 1) acc.loss += __shfl_xor(acc.loss, off);
 	float* lsum = slab + 2 * N;  // [WAVES] per-wave loss
 	if (lane == 0) lsum[wave] = acc.loss;
-	// slab element of this lane's accumulator register (mt/nt tile, r row) -- same map for write/add
+	// f4 j of this lane at S + 256 j + 4 lane -- the same map for write and add
 	auto visit = [&](float* S, bool add) {
+		int j = 0;
+		auto io = [&](f4& v) {
+			f4* p = (f4*)(S + 256 * j + 4 * lane);
+			if (add) v += *p; else *p = v;
+			++j;
+		};
 #pragma unroll
-		for (int mt = 0; mt < NT; ++mt) {
+		for (int mt = 0; mt < NT; ++mt)
 #pragma unroll
-			for (int r = 0; r < 4; ++r) {
-				const int n = 16 * mt + 4 * q + r;
+			for (int u = 0; u < NTI; ++u) io(acc.W0[mt][u]);
 #pragma unroll
-				for (int u = 0; u < NTI; ++u) {
-					float* p = &S[n * IN + 16 * u + c];
-					if (add) acc.W0[mt][u][r] += *p; else *p = acc.W0[mt][u][r];
-				}
+		for (int jj = 0; jj < NHM; ++jj)
 #pragma unroll
-				for (int j = 0; j < NHM; ++j)
+			for (int mt = 0; mt < NT; ++mt)
 #pragma unroll
-					for (int nt = 0; nt < NT; ++nt) {
-						float* p = &S[oH + j * W * W + n * W + 16 * nt + c];
-						if (add) acc.H[j][mt][nt][r] += *p; else *p = acc.H[j][mt][nt][r];
-					}
-			}
-		}
+				for (int nt = 0; nt < NT; ++nt) io(acc.H[jj][mt][nt]);
 #pragma unroll
-		for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-			for (int r = 0; r < 4; ++r) {
-				float* p = &S[oO + (4 * r + q) * W + 16 * nt + c];  // accumulator row 4q + r = output 4r + q
-				if (add) acc.Wo[nt][r] += *p; else *p = acc.Wo[nt][r];
-			}
+		for (int nt = 0; nt < NT; ++nt) io(acc.Wo[nt]);
 	};
 	for (int r = WAVES / 2; r >= 1; r >>= 1) {
 		for (int h = 0; h < r; h += 2) {
@@ -640,7 +653,7 @@ __device__ __forceinline__ void block_reduce_wgrad(WgradAcc<W, IN, NH>& acc, flo
 	if (wave == 0) visit(slab, false);
 	__syncthreads();
 	float* dst = a.wgrad_partial + (size_t)blockIdx.x * N;
-	for (int p = tid; p < N; p += WAVES * 64) dst[p] = slab[p];
+	for (int f = tid; f < N; f += WAVES * 64) dst[wgrad_frag_to_param<W, IN, NH>((uint32_t)f)] = slab[f];
 	if (tid == 0) {
 		float l = 0.0f;
 		for (int w = 0; w < WAVES; ++w) l += lsum[w];
@@ -664,6 +677,8 @@ __global__ __launch_bounds__(64 * FUSED_WAVES, 8 / FUSED_WAVES) void k_fused_tra
 	const int c = lane & 15, q = lane >> 4;
 
 	constexpr int NTHR = 64 * FUSED_WAVES;
+	unsigned long long tk0 = 0;
+	if constexpr (PROF) tk0 = stamp();
 	if (a.wimage) copy_image_to_lds(smem, a.wimage, L::oStage, tid, NTHR);
 	else load_weights_lds_v<W, IN, NH>(smem, a.params, tid, NTHR);
 	LevelInfo* sLvl = (LevelInfo*)((char*)smem + RL::LVL_BYTES);
@@ -680,7 +695,10 @@ __global__ __launch_bounds__(64 * FUSED_WAVES, 8 / FUSED_WAVES) void k_fused_tra
 
 	unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 	unsigned long long t0 = 0, t1 = 0;
-	if constexpr (PROF) t0 = stamp();
+	if constexpr (PROF) {
+		t0 = stamp();
+		ph[6] = t0 - tk0;  // prologue: weight image + level table into LDS
+	}
 	for (uint32_t chunk = blockIdx.x * FUSED_WAVES + wave; chunk < n_chunks; chunk += gridDim.x * FUSED_WAVES) {
 		const uint32_t base = chunk * 32;
 		h4 xt[2][NTI];
@@ -788,11 +806,16 @@ __global__ __launch_bounds__(64 * FUSED_WAVES, 8 / FUSED_WAVES) void k_fused_tra
 	if constexpr (PROF) {
 		if (lane == 0) {
 			unsigned long long* o = a.prof + (size_t)(blockIdx.x * FUSED_WAVES + wave) * 8;
-			for (int k = 0; k < 6; ++k) o[k] = ph[k];
+			for (int k = 0; k < 7; ++k) o[k] = ph[k];
 		}
+		t0 = stamp();
 	}
 	__syncthreads();
 	block_reduce_wgrad<W, IN, NH, FUSED_WAVES>(acc, (float*)smem, a, tid, wave, lane);
+	if constexpr (PROF) {
+		t1 = stamp();
+		if (lane == 0) a.prof[(size_t)(blockIdx.x * FUSED_WAVES + wave) * 8 + 7] = t1 - t0;  // epilogue: block reduce + slab
+	}
 }
 
 

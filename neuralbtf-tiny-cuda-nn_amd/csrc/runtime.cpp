@@ -640,6 +640,14 @@ void NetworkHost::fused_forward(hipStream_t st, StepWorkspace& ws, uint32_t B, c
 		launch_mlp_infer(st, mlp.width, IN, mlp.n_hidden_layers, mlp.activation, true, B, ws.wimage.p, enc, out16);
 		return;
 	}
+	if (!use_image && ((uintptr_t)params16 & 15)) {
+		// the kernel builds its LDS image with 16-byte loads from aligned parameters; a parameter view
+		// with an odd offset (e.g. a slice of a flat torch buffer) gets the packed image instead
+		ws.wimage.reserve(fused_weight_image_bytes(mlp.width, IN, mlp.n_hidden_layers));
+		launch_pack_weights(st, mlp.width, IN, mlp.n_hidden_layers, params16, ws.wimage.p);
+		ws.wimage_valid = false;  // packed from these parameters, which need not be the trainer's
+		use_image = true;
+	}
 	launch_fused_fwd(st, mlp.width, IN, mlp.n_hidden_layers, grid->desc.n_pos_dims, grid->desc.hash_type, mlp.activation, B,
 	                 use_image ? ws.wimage.p : nullptr, params16, eparams, pos, grid->dev_levels(), grid->hash_grid(), grid->desc.interp,
 	                 grid->inrange_index_ok && grid->desc.interp == Interp::Linear && !sw.no_inrange_index, enc_soa, out16);
@@ -705,7 +713,12 @@ void NetworkHost::fused_kernel(hipStream_t st, StepWorkspace& ws, uint32_t B, co
 	// parameters (load_weights_lds_v) -- no k_pack_weights launch; the Adam tail of the grid backward
 	// still writes the next step's image into ws.wimage
 	ws.wimage.reserve(fused_weight_image_bytes(mlp.width, mlp.n_input, mlp.n_hidden_layers));
-	const bool use_image = !pack && ws.wimage_valid;
+	bool use_image = !pack && ws.wimage_valid;
+	if (!use_image && ((uintptr_t)params16 & 15)) {  // unaligned parameter view: pack the image (see fused_forward)
+		launch_pack_weights(st, mlp.width, mlp.n_input, mlp.n_hidden_layers, params16, ws.wimage.p);
+		ws.wimage_valid = false;
+		use_image = true;
+	}
 	const uint8_t* table = (const uint8_t*)params16 + (size_t)n_mlp * 2;
 	launch_fused_train(st, mlp.width, mlp.n_input, mlp.n_hidden_layers, grid->desc.n_pos_dims, grid->desc.hash_type,
 	                   mlp.activation, B, dims, loss_scale, params16, table, pos, target, out16, ws.dLdenc.p,
@@ -743,7 +756,7 @@ void NetworkHost::fwd_bwd_fused(hipStream_t st, StepWorkspace& ws, uint32_t B, c
 	ep.enabled = 1;
 	ep.apply_adam = 0;
 	ep.buf.g32 = grad32;
-	ep.n_mlp_groups = MLP_TAIL_GROUPS;
+	ep.n_mlp_groups = mlp_tail_groups();
 	ep.n_mlp = n_mlp;
 	ws.loss_sum.reserve(16);
 	ep.d_loss = ws.loss_sum.as<float>();
@@ -909,13 +922,17 @@ TrainerHost::TrainerHost(uint32_t n_in, uint32_t n_out, const json& cfg, uint32_
 }
 
 void TrainerHost::initialize_params(uint32_t seed) {
-	log_debug("Trainer: initializing " + std::to_string(n_params) + " params and resetting training.");  // trainer.h:70
-	TCNN_HIP_CHECK(hipDeviceSynchronize());  // queued steps on the caller's stream must not race the reset
 	// trainer.h:52-55: pcg32{seed_seq{seed}.generate()[0]}
 	std::seed_seq seq{seed};
 	std::vector<uint32_t> seeds(2);
 	seq.generate(seeds.begin(), seeds.end());
 	Pcg32 rng{seeds.front()};
+	initialize_params_rng(rng);
+}
+
+void TrainerHost::initialize_params_rng(Pcg32& rng) {
+	log_debug("Trainer: initializing " + std::to_string(n_params) + " params and resetting training.");  // trainer.h:70
+	TCNN_HIP_CHECK(hipDeviceSynchronize());  // queued steps on the caller's stream must not race the reset
 	std::vector<float> host(n_params);
 	model->initialize_params(rng, host.data());
 	w32.reserve(n_params * 4);
@@ -1020,7 +1037,7 @@ void TrainerHost::training_step_overlapped(hipStream_t st, uint32_t B, const flo
 	ep.adam_mlp.n = (uint32_t)n_mlp;
 	ep.buf = AdamBuffers{w32.as<float>(), w16.as<_Float16>(), gsum, g16.as<_Float16>(), m1.as<float>(), m2.as<float>(),
 	                     steps.as<uint32_t>()};
-	ep.n_mlp_groups = MLP_TAIL_GROUPS;
+	ep.n_mlp_groups = mlp_tail_groups();
 	ep.n_mlp = (uint32_t)n_mlp;
 	ep.d_loss = d_loss.as<float>();
 	TCNN_CHECK(n_mlp % 4 == 0, "network parameter count must be a multiple of 4");

@@ -380,6 +380,7 @@ struct TrainerHost {
 
 	TrainerHost(uint32_t n_in, uint32_t n_out, const json& cfg, uint32_t seed);
 	void initialize_params(uint32_t seed);
+	void initialize_params_rng(Pcg32& rng);  // from the caller's generator (advanced by n_params draws)
 	void training_step(hipStream_t st, uint32_t B, const float* input, const float* target, bool run_optimizer);
 	void step_eager(hipStream_t st, uint32_t B, const float* input, const float* target);  // with the optimizer
 	void training_step_sequential(hipStream_t st, uint32_t B, const float* input, const float* target, bool run_optimizer);

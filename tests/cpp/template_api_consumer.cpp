@@ -388,6 +388,30 @@ int main(int argc, char** argv) {
 			for (uint32_t i = 0; i < 4096; ++i)
 				for (uint32_t k = 0; k < 3; ++k) diff += (float)o16[(size_t)i * 16 + k] != hi[(size_t)i * 3 + k];
 			EXPECT(diff == 0);
+
+			// initialize_params re-initialises from the trainer's live generator (trainer.h:67-85: m_rng
+			// keeps advancing), so a second initialisation draws new values -- the first n_params draws
+			// after the construction-time ones: the network's first weight equals the Xavier transform of
+			// the generator advanced by n_params
+			std::shared_ptr<NetworkWithInputEncoding<network_precision_t>> rnet{
+			    new NetworkWithInputEncoding<network_precision_t>(2, 3, config["encoding"], config["network"])};
+			Trainer<float, network_precision_t, network_precision_t> rt(rnet, po, pl, 1337);
+			const uint64_t np = tcnn_trainer_n_params(rt.handle());
+			std::vector<float> w0(np), w1(np);
+			HIP_CHECK_THROW(hipMemcpy(w0.data(), tcnn_trainer_params_fp32(rt.handle()), np * 4, hipMemcpyDeviceToHost));
+			rt.initialize_params();
+			HIP_CHECK_THROW(hipMemcpy(w1.data(), tcnn_trainer_params_fp32(rt.handle()), np * 4, hipMemcpyDeviceToHost));
+			std::seed_seq seq{1337u};
+			std::vector<uint32_t> sd(2);
+			seq.generate(sd.begin(), sd.end());
+			default_rng_t g{sd.front()};
+			g.advance((int64_t)np);
+			const float scale = std::sqrt(6.0f / (float)(64 + 32));  // W0 of config_hash: 64 x 32
+			volatile float t0 = g.next_float() * 2.0f;  // the engine's xavier: t = u * 2; t = t * scale; t - scale
+			volatile float t1 = t0 * scale;
+			const float x0 = t1 - scale;
+			EXPECT(w1[0] == x0);
+			EXPECT(w0[0] != w1[0]);
 		}
 
 		// Trainer over any DifferentiableObject (trainer.h:50): a Network alone from create_network

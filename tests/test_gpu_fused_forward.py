@@ -71,3 +71,43 @@ def test_trainer_inference_matches_two_pass_forward():
     ya, yb = ta.inference(x), tb.inference(x)
     assert float(ya.abs().max()) > 0
     np.testing.assert_array_equal(ya.cpu().numpy(), yb.cpu().numpy())
+
+
+def test_unaligned_parameter_view():
+    """A parameter tensor that is a view at an 8-byte offset into a flat fp16 buffer (not 16-byte aligned:
+    the in-kernel LDS image build uses 16-byte loads) runs through the packed weight image instead of
+    failing: inference and the kept-context backward bit-identical to the aligned tensor."""
+    import ctypes
+    import torch
+    from tinycudann import _lib as L
+    lib = L.lib()
+    import json
+    m = L.check_ptr(lib.tcnn_create_network_with_input_encoding(2, 3, json.dumps(CONFIG_HASH["encoding"]).encode(),
+                                                                 json.dumps(CONFIG_HASH["network"]).encode()))
+    n = lib.tcnn_module_n_params(m)
+    p32 = torch.zeros(n, dtype=torch.float32, device="cuda")
+    L.check(lib.tcnn_module_initialize_params(m, 1337, ctypes.c_void_p(p32.data_ptr()), 1.0))
+    aligned = p32.half().contiguous()
+    flat = torch.zeros(n + 8, dtype=torch.float16, device="cuda")
+    view = flat[4:4 + n]
+    view.copy_(aligned)
+    assert view.data_ptr() % 16 == 8
+    B = 4096
+    x = torch.rand(B, 2, device="cuda")
+    outs = []
+    for p in (aligned, view):
+        out = torch.empty(B, 16, dtype=torch.float16, device="cuda")
+        L.check(lib.tcnn_module_inference(m, None, B, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                          ctypes.c_void_p(p.data_ptr())))
+        ctx = L.check_ptr(lib.tcnn_module_forward(m, None, B, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                                  ctypes.c_void_p(p.data_ptr()), 0))
+        dout = torch.full((B, 16), 0.01, dtype=torch.float16, device="cuda")
+        grad = torch.empty(n, dtype=torch.float16, device="cuda")
+        L.check(lib.tcnn_module_backward(m, None, ctx, B, None, ctypes.c_void_p(dout.data_ptr()), ctypes.c_void_p(grad.data_ptr()),
+                                         ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(p.data_ptr())))
+        torch.cuda.synchronize()
+        lib.tcnn_context_destroy(ctx)
+        outs.append((out.cpu().numpy(), grad.cpu().numpy()))
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+    lib.tcnn_module_destroy(m)
