@@ -299,7 +299,7 @@ int tcnn_debug_probe(void* stream, float* mfma_out /* device [64*4] */, int16_t*
 /* Diagnostic build of the config_hash fused kernel with s_memtime stamps: per-phase wave-cycle sums
  * (0 grid encode, 1 hidden layers fwd, 2 output+loss, 3 bwd through hidden layers + their dW,
  * 4 first-layer dW, 5 dL/dx + store, 6 prologue, 7 epilogue reduction), summed over all waves, written to
- * host_cycles8[8]. */
+ * host_cycles8[16] (slots 8.. used by newer builds). */
 int tcnn_debug_fused_phase_cycles(tcnn_trainer* t, void* stream, uint32_t n, const float* input, const float* target,
                                   uint64_t* host_cycles8);
 /* out[i] = fma(a[i], b[i], c[i]) with the packed-fp16 FMA the grid forward uses (n_pairs half2 values) */

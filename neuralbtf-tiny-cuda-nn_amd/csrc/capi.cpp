@@ -753,17 +753,17 @@ int tcnn_debug_fused_phase_cycles(tcnn_trainer* t, void* stream, uint32_t n, con
 		const uint32_t nb = fused_train_n_blocks(64, 32, 2, 2, tr.n_output_dims, false, n);
 		const size_t WV = fused_train_waves();  // waves per workgroup of the fused kernel
 		DevBuf prof;
-		prof.reserve((size_t)nb * WV * 8 * 8);
-		TCNN_HIP_CHECK(hipMemsetAsync(prof.p, 0, (size_t)nb * WV * 8 * 8, st));
+		prof.reserve((size_t)nb * WV * 16 * 8);
+		TCNN_HIP_CHECK(hipMemsetAsync(prof.p, 0, (size_t)nb * WV * 16 * 8, st));
 		launch_fused_train_profile(st, n, tr.n_output_dims, tr.w16.p, (const uint8_t*)tr.w16.p + tr.n_mlp * 2, input, target,
 		                           tr.ws.dLdenc.p, tr.ws.wgrad_partial.as<float>(), tr.ws.loss_partial.as<float>(),
 		                           m.grid->dev_levels(), nb, tr.ws.wimage.p, prof.as<unsigned long long>());
-		std::vector<unsigned long long> h((size_t)nb * WV * 8);
+		std::vector<unsigned long long> h((size_t)nb * WV * 16);
 		TCNN_HIP_CHECK(hipMemcpyAsync(h.data(), prof.p, h.size() * 8, hipMemcpyDeviceToHost, st));
 		TCNN_HIP_CHECK(hipStreamSynchronize(st));
-		for (int k = 0; k < 8; ++k) {
+		for (int k = 0; k < 16; ++k) {
 			unsigned long long sum = 0;
-			for (size_t w = 0; w < (size_t)nb * WV; ++w) sum += h[w * 8 + k];
+			for (size_t w = 0; w < (size_t)nb * WV; ++w) sum += h[w * 16 + k];
 			host_cycles8[k] = sum;
 		}
 	});

@@ -610,9 +610,17 @@ __device__ __forceinline__ uint32_t wgrad_frag_to_param(uint32_t f) {
 	return oO + (4 * r + q) * W + 16 * nt + c;  // accumulator row 4q + r = output 4r + q
 }
 
-template <int W, int IN, int NH, int WAVES>
+template <int W, int IN, int NH, int WAVES, bool PROF = false>
 __device__ __forceinline__ void block_reduce_wgrad(WgradAcc<W, IN, NH>& acc, float* slab, const FusedTrainArgs& a,
-                                                   int tid, int wave, int lane) {
+                                                   int tid, int wave, int lane, unsigned long long* pst = nullptr) {
+	int np = 0;
+	auto pstamp = [&] {
+		if constexpr (PROF) {
+			const unsigned long long t = stamp();
+			if (lane == 0 && np < 6) pst[np] = t;
+			++np;
+		}
+	};
 	using L = FusedLayout<W, IN, NH>;
 	constexpr int NT = L::NT, NTI = L::NTI, NHM = L::NHM, N = L::N_MLP;
 	static_assert(N % 256 == 0, "whole f4 per lane");
@@ -641,19 +649,49 @@ __device__ __forceinline__ void block_reduce_wgrad(WgradAcc<W, IN, NH>& acc, flo
 #pragma unroll
 		for (int nt = 0; nt < NT; ++nt) io(acc.Wo[nt]);
 	};
-	for (int r = WAVES / 2; r >= 1; r >>= 1) {
-		for (int h = 0; h < r; h += 2) {
-			// writers r+h, r+h+1 -> slabs 0, 1 ; readers h, h+1 add them
-			if (wave >= r + h && wave < r + h + 2 && wave < 2 * r) visit(slab + (wave - r - h) * N, false);
-			__syncthreads();
-			if (wave >= h && wave < h + 2 && wave < r) visit(slab + (wave - h) * N, true);
-			__syncthreads();
-		}
-	}
-	if (wave == 0) visit(slab, false);
-	__syncthreads();
 	float* dst = a.wgrad_partial + (size_t)blockIdx.x * N;
-	for (int f = tid; f < N; f += WAVES * 64) dst[wgrad_frag_to_param<W, IN, NH>((uint32_t)f)] = slab[f];
+	if constexpr (WAVES == 4) {
+		// (w0 + w2) + (w1 + w3): waves 2, 3 write, waves 0, 1 add and write their sums back in place
+		// (each lane rewrites only the f4s it read), then all four waves add the two sums and store the
+		// slab in parameter order -- 3 LDS passes instead of the tree's 5, the last one spread over
+		// every wave, its reads all in flight (unrolled)
+		if (wave >= 2) visit(slab + (wave - 2) * N, false);
+		__syncthreads();
+		pstamp();
+		if (wave < 2) {
+			visit(slab + wave * N, true);
+			visit(slab + wave * N, false);
+		}
+		__syncthreads();
+		pstamp();
+		constexpr int PER = (N / 4 + WAVES * 64 - 1) / (WAVES * 64);  // f4s per thread
+#pragma unroll
+		for (int k = 0; k < PER; ++k) {
+			const int g = tid + k * WAVES * 64;
+			if ((N / 4) % (WAVES * 64) != 0 && g >= N / 4) break;
+			const f4 v = ((const f4*)slab)[g] + ((const f4*)(slab + N))[g];
+#pragma unroll
+			for (int r = 0; r < 4; ++r) dst[wgrad_frag_to_param<W, IN, NH>((uint32_t)(4 * g + r))] = v[r];
+		}
+		pstamp();
+	} else {
+		for (int r = WAVES / 2; r >= 1; r >>= 1) {
+			for (int h = 0; h < r; h += 2) {
+				// writers r+h, r+h+1 -> slabs 0, 1 ; readers h, h+1 add them
+				if (wave >= r + h && wave < r + h + 2 && wave < 2 * r) visit(slab + (wave - r - h) * N, false);
+				__syncthreads();
+				pstamp();
+				if (wave >= h && wave < h + 2 && wave < r) visit(slab + (wave - h) * N, true);
+				__syncthreads();
+				pstamp();
+			}
+		}
+		if (wave == 0) visit(slab, false);
+		__syncthreads();
+		pstamp();
+		for (int f = tid; f < N; f += WAVES * 64) dst[wgrad_frag_to_param<W, IN, NH>((uint32_t)f)] = slab[f];
+		pstamp();
+	}
 	if (tid == 0) {
 		float l = 0.0f;
 		for (int w = 0; w < WAVES; ++w) l += lsum[w];
@@ -805,16 +843,29 @@ __global__ __launch_bounds__(64 * FUSED_WAVES, 8 / FUSED_WAVES) void k_fused_tra
 	}
 	if constexpr (PROF) {
 		if (lane == 0) {
-			unsigned long long* o = a.prof + (size_t)(blockIdx.x * FUSED_WAVES + wave) * 8;
+			unsigned long long* o = a.prof + (size_t)(blockIdx.x * FUSED_WAVES + wave) * 16;
 			for (int k = 0; k < 7; ++k) o[k] = ph[k];
 		}
 		t0 = stamp();
 	}
 	__syncthreads();
-	block_reduce_wgrad<W, IN, NH, FUSED_WAVES>(acc, (float*)smem, a, tid, wave, lane);
+	unsigned long long ts = 0;
+	unsigned long long pst[6] = {0, 0, 0, 0, 0, 0};
+	if constexpr (PROF) ts = stamp();
+	block_reduce_wgrad<W, IN, NH, FUSED_WAVES, PROF>(acc, (float*)smem, a, tid, wave, lane, pst);
 	if constexpr (PROF) {
 		t1 = stamp();
-		if (lane == 0) a.prof[(size_t)(blockIdx.x * FUSED_WAVES + wave) * 8 + 7] = t1 - t0;  // epilogue: block reduce + slab
+		if (lane == 0) {
+			unsigned long long* o = a.prof + (size_t)(blockIdx.x * FUSED_WAVES + wave) * 16;
+			o[7] = t1 - ts;  // epilogue: block reduce + slab
+			o[8] = ts - t0;  // waiting for the workgroup's other waves
+			unsigned long long prev = ts;
+			for (int k = 0; k < 6; ++k) {  // the reduction's passes (tree rounds, final write, slab store)
+				if (pst[k] == 0) break;
+				o[9 + k] = pst[k] - prev;
+				prev = pst[k];
+			}
+		}
 	}
 }
 
