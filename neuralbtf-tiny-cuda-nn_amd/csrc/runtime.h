@@ -123,7 +123,10 @@ struct GridEncodingHost {
 		// profiles/r04_grid_bwd_chunks.txt); config_hash at 2^18 keeps its 8
 		c = std::max(c, (B + GRID_BWD_REG_POINTS - 1) / GRID_BWD_REG_POINTS);
 		if (sw.grid_bwd_chunks) c = sw.grid_bwd_chunks;  // tuning override
-		return std::max(1u, std::min(std::min(c, 32u), B / 4096));
+		// >= 8192 points per chunk: below that the per-chunk slab (written here, read by Adam or the
+		// slab reduction) costs more than the parallelism gains (2^15 points, one rank of N = 8:
+		// 4 chunks 46.6 us per step vs 8 chunks 48.0, profiles/r05_chunk_sweep.txt)
+		return std::max(1u, std::min(std::min(c, 32u), B / 8192));
 	}
 	// bin-pass geometry for B points (reserves the record / directory buffers in w)
 	GridBinArgs bin_args(GridBwdBufs& w, uint32_t B) const;
