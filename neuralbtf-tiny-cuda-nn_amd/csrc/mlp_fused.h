@@ -717,11 +717,28 @@ __global__ __launch_bounds__(64 * FUSED_WAVES, 8 / FUSED_WAVES) void k_fused_tra
 	constexpr int NTHR = 64 * FUSED_WAVES;
 	unsigned long long tk0 = 0;
 	if constexpr (PROF) tk0 = stamp();
-	if (a.wimage) copy_image_to_lds(smem, a.wimage, L::oStage, tid, NTHR);
-	else load_weights_lds_v<W, IN, NH>(smem, a.params, tid, NTHR);
+	// The packed weight image is copied with global_load_lds_dwordx4 (LDS-DMA, no VGPRs) issued AFTER
+	// the level table's barrier, so its latency runs under the first slice's position loads and
+	// gathers; every wave waits for its own copies and meets the others at one barrier after its
+	// first slice's encode, before the first MFMA reads the image (each wave has >= 1 slice: the launch
+	// has at most B / 32 waves; one without meets it after its empty loop). Without an image the workgroup
+	// builds it from the parameters first.
+	const bool async_image = a.wimage != nullptr;
+	if (!async_image) load_weights_lds_v<W, IN, NH>(smem, a.params, tid, NTHR);
 	LevelInfo* sLvl = (LevelInfo*)((char*)smem + RL::LVL_BYTES);
 	for (int l = tid; l < NLVL; l += NTHR) sLvl[l] = a.levels[l];
 	__syncthreads();
+	if (async_image) {
+		constexpr int n16 = L::oStage / 8;  // 16-byte units of the image
+#pragma unroll
+		for (int k0 = 0; k0 < n16; k0 += NTHR) {
+			const int u = k0 + wave * 64;  // this wave's 1 KB piece (lane-linear in LDS)
+			if (u + lane < n16)
+				__builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(a.wimage + 8 * (u + lane)),
+				                                 (__attribute__((address_space(3))) void*)(smem + 8 * u), 16, 0, 0);
+		}
+	}
+	bool image_pending = async_image;
 
 	_Float16* bufA = smem + L::oStage + wave * 2 * L::STAGE;
 	_Float16* bufD = bufA + L::STAGE;
@@ -835,12 +852,17 @@ __global__ __launch_bounds__(64 * FUSED_WAVES, 8 / FUSED_WAVES) void k_fused_tra
 						xt[tau][2 * s + (pp >> 1)][2 * (pp & 1) + 1] = e[1];
 					}
 		}
+		if (image_pending) {  // uniform: every wave passes here exactly once, on its first slice
+			__syncthreads();  // vmcnt(0): this wave's image copies landed; the barrier: everyone's did
+			image_pending = false;
+		}
 		if constexpr (PROF) { t1 = stamp(); ph[0] += t1 - t0; t0 = t1; }
 		auto target = [&](int tau, uint32_t o) { return tg[tau][o >> 2]; };
 		auto after_loss = [] {};
 		fused_slice<W, IN, NH, ACT, EXT_DOUT, PROF>(a, base, c, q, xt, target, after_loss, Gext, smem + L::oW0,
 		                                            smem + L::oWh, smem + L::oWo, bufA, bufD, acc, ph, t0);
 	}
+	if (image_pending) __syncthreads();  // a wave without a slice (B % 128 != 0) still meets that barrier
 	if constexpr (PROF) {
 		if (lane == 0) {
 			unsigned long long* o = a.prof + (size_t)(blockIdx.x * FUSED_WAVES + wave) * 16;

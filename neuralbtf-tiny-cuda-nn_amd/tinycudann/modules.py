@@ -57,12 +57,20 @@ def _torch_precision(p):
     return torch.half if p == PRECISION_FP16 else torch.float
 
 
-def _stream():
-    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
+def _stream(t=None):
+    """the current stream of t's device (default: the current device) as a raw handle -- the binding's
+    hot path makes a few of these calls per step, and torch.cuda.current_stream() builds a Stream object
+    each time (the torch step is host-bound at 2^16 points, tools/torch_host_breakdown.py)"""
+    if _raw_stream is not None:
+        return _raw_stream(t.device.index if t is not None else torch.cuda.current_device())
+    return torch.cuda.current_stream().cuda_stream
 
 
 def _ptr(t):
-    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+    return t.data_ptr() if t is not None else None  # ctypes converts the int for a c_void_p argument
 
 
 _GRANULARITY = None
@@ -141,9 +149,9 @@ class _NativeModule:
         B = input.shape[0]
         out = torch.empty(B, self._n_out, dtype=self._out_dtype, device=input.device)
         if not (input.requires_grad or params.requires_grad):
-            L.check(L.lib().tcnn_module_inference(self.h, _stream(), B, _ptr(input), _ptr(out), _ptr(params)))
+            L.check(L.lib().tcnn_module_inference(self.h, _stream(input), B, _ptr(input), _ptr(out), _ptr(params)))
             return None, out
-        ctx = L.check_ptr(L.lib().tcnn_module_forward(self.h, _stream(), B, _ptr(input), _ptr(out), _ptr(params),
+        ctx = L.check_ptr(L.lib().tcnn_module_forward(self.h, _stream(input), B, _ptr(input), _ptr(out), _ptr(params),
                                                        int(input.requires_grad)))
         return _NativeContext(ctx), out
 
@@ -158,7 +166,7 @@ class _NativeModule:
             doutput = doutput.to(self._out_dtype)
         if not doutput.is_contiguous():
             doutput = doutput.contiguous()
-        L.check(L.lib().tcnn_module_backward_scaled(self.h, _stream(), ctx.h, B, _ptr(dL_dinput), _ptr(doutput),
+        L.check(L.lib().tcnn_module_backward_scaled(self.h, _stream(input), ctx.h, B, _ptr(dL_dinput), _ptr(doutput),
                                                     _ptr(dL_dparams), _ptr(input), _ptr(output), _ptr(params),
                                                     float(loss_scale), 0))
         return dL_dinput, dL_dparams
