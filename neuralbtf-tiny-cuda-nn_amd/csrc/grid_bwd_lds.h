@@ -220,15 +220,30 @@ __device__ __forceinline__ void grid_bwd_points_regs(const uint32_t (&dyb)[GRID_
 				for (uint32_t d = 0; d < D; ++d) inr = inr && xs[k & 1][u][d] >= 0.0f && xs[k & 1][u][d] <= 1.0f;
 			fast_b = fast_b && __builtin_amdgcn_ballot_w64(!inr) == 0;
 		}
-		if (fast_b && i0 + threadIdx.x + (k * U + U - 1) * blockDim.x < i1) {  // the whole batch is inside the chunk
+		if (fast_b) {
 			if constexpr (FAST_KIND) {
+				if (i0 + threadIdx.x + (k * U + U - 1) * blockDim.x < i1) {  // the whole batch is inside the chunk
 #pragma unroll
-				for (uint32_t u = 0; u < U; ++u) {
-					const uint32_t p = k * U + u;
-					float dy[F];
+					for (uint32_t u = 0; u < U; ++u) {
+						const uint32_t p = k * U + u;
+						float dy[F];
 #pragma unroll
-					for (uint32_t f = 0; f < F; ++f) dy[f] = dy_bits_feature(dyb[p], f) * scale;
-					accum_point_2d_fast<F, H, KIND, MODE>(*(const float(*)[2]) & xs[k & 1][u][0], dy, li, f0, nf, acc);
+						for (uint32_t f = 0; f < F; ++f) dy[f] = dy_bits_feature(dyb[p], f) * scale;
+						accum_point_2d_fast<F, H, KIND, MODE>(*(const float(*)[2]) & xs[k & 1][u][0], dy, li, f0, nf, acc);
+					}
+				} else {
+					// the chunk's last, partial batch (e.g. 4 points per thread at 4096-point chunks: the
+					// 2^15-point shard of N = 8): the same branch-free path per point that exists (r04 sent
+					// these through the generic per-corner path, 3.5 us of accumulation for 4 points)
+#pragma unroll
+					for (uint32_t u = 0; u < U; ++u) {
+						const uint32_t p = k * U + u;
+						if (i0 + threadIdx.x + p * blockDim.x >= i1) break;
+						float dy[F];
+#pragma unroll
+						for (uint32_t f = 0; f < F; ++f) dy[f] = dy_bits_feature(dyb[p], f) * scale;
+						accum_point_2d_fast<F, H, KIND, MODE>(*(const float(*)[2]) & xs[k & 1][u][0], dy, li, f0, nf, acc);
+					}
 				}
 			}
 			continue;

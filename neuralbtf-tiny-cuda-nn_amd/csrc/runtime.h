@@ -122,7 +122,7 @@ struct GridEncodingHost {
 		// (configs[3], 2^20 points: 8 -> 32 chunks, grid backward 170 -> 99 us, step -4 %,
 		// profiles/r04_grid_bwd_chunks.txt); config_hash at 2^18 keeps its 8
 		c = std::max(c, (B + GRID_BWD_REG_POINTS - 1) / GRID_BWD_REG_POINTS);
-		if (sw.grid_bwd_chunks) c = sw.grid_bwd_chunks;  // tuning override
+		if (sw.grid_bwd_chunks) return std::max(1u, std::min(std::min(sw.grid_bwd_chunks, 32u), B / 1024));  // tuning override
 		// >= 8192 points per chunk: below that the per-chunk slab (written here, read by Adam or the
 		// slab reduction) costs more than the parallelism gains (2^15 points, one rank of N = 8:
 		// 4 chunks 46.6 us per step vs 8 chunks 48.0, profiles/r05_chunk_sweep.txt)
