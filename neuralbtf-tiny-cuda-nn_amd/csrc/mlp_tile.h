@@ -41,10 +41,11 @@ constexpr int tile_imin(int a, int b) { return a < b ? a : b; }
 // ---------------------------------------------------------------------------------------------
 // training
 // ---------------------------------------------------------------------------------------------
-// LDS halves of a tile workgroup with the first NS hidden matrices streamed from L2 instead of staged
-constexpr int tile_halves(int W, int IN, int NH, int NS) {
+// LDS halves of a tile workgroup of TS-sample tiles with the first NS hidden matrices streamed from L2
+// instead of staged
+constexpr int tile_halves(int W, int IN, int NH, int NS, int TS = 32) {
 	const int KP0 = (IN + 31) / 32 * 32, RS0 = KP0 + 8, RSW = W + 8, RSG = 24;
-	return W * RS0 + (NH - 1 - NS) * W * RSW + 16 * RSW + 32 * RS0 + NH * 32 * RSW + 32 * RSG;
+	return W * RS0 + (NH - 1 - NS) * W * RSW + 16 * RSW + TS * RS0 + NH * TS * RSW + TS * RSG;
 }
 // waves per workgroup: W128 runs 8 (2 per SIMD, one 16-row tile of every matrix each) up to 4 hidden
 // layers; with 5 its weight-gradient accumulators (>= 164 registers) spill at 256 registers per wave,
@@ -67,21 +68,30 @@ constexpr int tile_waves(int W, int NH, bool RA = false) { return W == 128 && NH
 constexpr int tile_lds_limit() { return 160 * 1024; }
 // fewest streamed hidden matrices that let the rest of the network + the tile's activations fit
 // (RA: all of them, from registers)
-constexpr int tile_n_streamed(int W, int IN, int NH, bool RA = false) {
+constexpr int tile_n_streamed(int W, int IN, int NH, bool RA = false, int TS = 32) {
 	if (RA) return NH - 1;
 	int ns = 0;
-	while (ns < NH - 1 && tile_halves(W, IN, NH, ns) * 2 + tile_waves(W, NH) * 4 > tile_lds_limit()) ++ns;
+	while (ns < NH - 1 && tile_halves(W, IN, NH, ns, TS) * 2 + tile_waves(W, NH) * 4 > tile_lds_limit()) ++ns;
 	return ns;
+}
+// 64-sample tiles (TS = 64): half the workgroup barriers per sample (each layer's barrier now covers
+// four 16-sample MFMA columns per row tile, the weight-gradient MFMAs contract over two 32-sample
+// halves). For the 8-wave W128 kernel (enough waves for the output layer's four 16-sample columns),
+// where at most one hidden matrix has to move from LDS to L2 to make room for the larger tile
+// (configs[3] HashGrid + W128/H4: 119 KB of staged weights + 38 KB of tile -> one hidden matrix read
+// from L2, 158 KB).
+constexpr bool tile_ts64_ok(int W, int IN, int NH, bool RA) {
+	return !RA && W == 128 && tile_waves(W, NH) == 8 && tile_n_streamed(W, IN, NH, false, 64) <= 1;
 }
 // workgroups per CU the launch aims for: two waves per SIMD where the LDS (and, for W128 RA, the
 // registers) allow
-constexpr int tile_train_wg_per_cu(int W, int IN, int NH, bool RA = false) {
+constexpr int tile_train_wg_per_cu(int W, int IN, int NH, bool RA = false, int TS = 32) {
 	return W == 128 && RA ? 1
 	                      : tile_imax(1, tile_imin(8 / tile_waves(W, NH, RA),
-	                                               tile_lds_limit() / (tile_halves(W, IN, NH, tile_n_streamed(W, IN, NH, RA)) * 2 + tile_waves(W, NH, RA) * 4)));
+	                                               tile_lds_limit() / (tile_halves(W, IN, NH, tile_n_streamed(W, IN, NH, RA, TS), TS) * 2 + tile_waves(W, NH, RA) * 4)));
 }
 
-template <int WR, int IN, int NH, bool RA = false>
+template <int WR, int IN, int NH, bool RA = false, int TS = 32>
 struct TileLayout {
 	static constexpr int W = tile_kw(WR);
 	static_assert(W == 32 || W == 64 || W == 128, "tile engine: W in {16, 32, 64, 128}");
@@ -95,19 +105,22 @@ struct TileLayout {
 	// hidden matrices 1..NS are not staged: their forward A fragments come from the fp16 parameters
 	// (L2-resident, every workgroup reads the same 32 KB), their backward ones from a transposed copy
 	// (RA: loaded once into registers)
-	static constexpr int NS = tile_n_streamed(W, IN, NH, RA);
+	static constexpr int NS = tile_n_streamed(W, IN, NH, RA, TS);
+	static constexpr int NTAU = TS / 16, KH = TS / 32;  // 16-sample MFMA columns / 32-sample K halves per tile
+	static_assert(TS == 32 || (TS == 64 && tile_ts64_ok(W, IN, NH, RA)), "tile samples: 32, or 64 where tile_ts64_ok");
+	static_assert(NTAU <= WAVES, "one wave per 16-sample column of the output layer");
 	static_assert(NS == 0 || W == WR, "streamed matrices only for unpadded widths");
 	static constexpr int oW0 = 0, oWh = oW0 + W * RS0, oWo = oWh + (NH - 1 - NS) * W * RSW;
-	static constexpr int oX = oWo + 16 * RSW;                 // slot 0: the tile's input [32][RS0]
-	static constexpr int oA = oX + 32 * RS0;                  // slots 1..NH: [32][RSW]
-	static constexpr int oG = oA + NH * 32 * RSW;             // dL/dy of the tile [32][RSG]
-	static constexpr int HALVES = oG + 32 * RSG;
+	static constexpr int oX = oWo + 16 * RSW;                 // slot 0: the tile's input [TS][RS0]
+	static constexpr int oA = oX + TS * RS0;                  // slots 1..NH: [TS][RSW]
+	static constexpr int oG = oA + NH * TS * RSW;             // dL/dy of the tile [TS][RSG]
+	static constexpr int HALVES = oG + TS * RSG;
 	static constexpr int BYTES = HALVES * 2 + WAVES * 4;       // + per-wave loss
 	static constexpr int N_MLP = WR * IN + (NH - 1) * WR * WR + 16 * WR;  // parameters (unpadded)
-	static constexpr int WG_PER_CU = tile_train_wg_per_cu(W, IN, NH, RA);
+	static constexpr int WG_PER_CU = tile_train_wg_per_cu(W, IN, NH, RA, TS);
 	// waves per SIMD the launch runs (amdgpu_waves_per_eu: caps the registers so they fit)
 	static constexpr int WAVES_PER_EU = tile_imax(1, WG_PER_CU * WAVES / 4);
-	static_assert(HALVES == tile_halves(W, IN, NH, NS), "layout");
+	static_assert(HALVES == tile_halves(W, IN, NH, NS, TS), "layout");
 	static_assert(oWh % 8 == 0 && oWo % 8 == 0 && oX % 8 == 0 && oA % 8 == 0 && oG % 8 == 0, "16-byte alignment");
 	static_assert(BYTES <= tile_lds_limit(), "tile exceeds the LDS");
 };
@@ -146,14 +159,14 @@ __device__ __forceinline__ h4 out_act_fwd(int a, f4 y) {
 
 // launch bounds as plain function calls (a template-id's commas would split the macro arguments)
 constexpr int tile_train_nthr(int WR, int NH, bool RA) { return tile_waves(tile_kw(WR), NH, RA) * 64; }
-constexpr int tile_train_weu(int WR, int IN, int NH, bool RA) {
-	return tile_imax(1, tile_train_wg_per_cu(tile_kw(WR), IN, NH, RA) * tile_waves(tile_kw(WR), NH, RA) / 4);
+constexpr int tile_train_weu(int WR, int IN, int NH, bool RA, int TS) {
+	return tile_imax(1, tile_train_wg_per_cu(tile_kw(WR), IN, NH, RA, TS) * tile_waves(tile_kw(WR), NH, RA) / 4);
 }
 
-template <int WR, int IN, int NH, Act ACT, bool RA>
-__global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN, NH, RA)) void k_mlp_tile_train(const TileTrainArgs a) {
-	using L = TileLayout<WR, IN, NH, RA>;
-	constexpr int W = L::W;
+template <int WR, int IN, int NH, Act ACT, bool RA, int TS>
+__global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN, NH, RA, TS)) void k_mlp_tile_train(const TileTrainArgs a) {
+	using L = TileLayout<WR, IN, NH, RA, TS>;
+	constexpr int W = L::W, NTAU = L::NTAU, KH = L::KH;
 	constexpr int MTW = L::MTW, KT0 = L::KT0, RS0 = L::RS0, RSW = L::RSW, RSG = L::RSG;
 	constexpr int WAVES = L::WAVES, NTHR = L::NTHR;
 	constexpr int NTW = L::MT / WAVES;  // Wout column tiles per wave (= MTW)
@@ -190,13 +203,13 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 		}
 		// zero the padded input columns of slot 0 once (the input loads never write them)
 		if (L::KP0 > IN)
-			for (int idx = tid; idx < 32 * (L::KP0 - IN); idx += NTHR)
+			for (int idx = tid; idx < TS * (L::KP0 - IN); idx += NTHR)
 				smem[L::oX + (idx / (L::KP0 - IN)) * RS0 + IN + idx % (L::KP0 - IN)] = (_Float16)0.0f;
 	}
 	// staged matrices (m == 0 or m > NS); streamed ones (1 <= m <= NS) are read from global memory
 	auto Wm = [&](int m) -> const _Float16* { return m == 0 ? smem + L::oW0 : smem + L::oWh + (m - 1 - L::NS) * W * RSW; };
 	auto streamed = [](int m) { return m >= 1 && m <= L::NS; };
-	auto slot = [&](int m) -> _Float16* { return m == 0 ? smem + L::oX : smem + L::oA + (m - 1) * 32 * RSW; };
+	auto slot = [&](int m) -> _Float16* { return m == 0 ? smem + L::oX : smem + L::oA + (m - 1) * TS * RSW; };
 	_Float16* sG = smem + L::oG;
 
 	// ---- register accumulators of this wave's weight-gradient rows ----
@@ -233,22 +246,22 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 	float loss = 0.0f;
 
 	// input rows of a tile: IN/8 16-byte vectors per sample
-	constexpr int XV = 32 * IN / 8, XPT = (XV + NTHR - 1) / NTHR;
-	const uint32_t n_tiles = a.B / 32;
+	constexpr int XV = TS * IN / 8, XPT = (XV + NTHR - 1) / NTHR;
+	const uint32_t n_tiles = a.B / TS;
 	uint32_t tile = blockIdx.x;
 	h8 xr[XPT];
 	auto load_x = [&](uint32_t t) {
 #pragma unroll
 		for (int j = 0; j < XPT; ++j) {
 			const int idx = tid + NTHR * j;
-			if (idx < XV) xr[j] = *(const h8*)(a.enc + ((size_t)t * 32 + idx / (IN / 8)) * IN + 8 * (idx % (IN / 8)));
+			if (idx < XV) xr[j] = *(const h8*)(a.enc + ((size_t)t * TS + idx / (IN / 8)) * IN + 8 * (idx % (IN / 8)));
 		}
 	};
 	if (tile < n_tiles) load_x(tile);
 	__syncthreads();
 
 	for (; tile < n_tiles; tile += gridDim.x) {
-		const uint32_t base = tile * 32;
+		const uint32_t base = tile * TS;
 		// ---- input tile -> slot 0; prefetch the next tile's rows ----
 #pragma unroll
 		for (int j = 0; j < XPT; ++j) {
@@ -256,10 +269,10 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 			if (idx < XV) *(h8*)(slot(0) + (idx / (IN / 8)) * RS0 + 8 * (idx % (IN / 8))) = xr[j];
 		}
 		if (tile + gridDim.x < n_tiles) load_x(tile + gridDim.x);
-		// targets / external dL/dy of this wave's output lanes (waves 0, 1: sample tile tau = wave)
+		// targets / external dL/dy of this wave's output lanes (waves 0 .. NTAU-1: 16-sample column tau = wave)
 		float tg[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 		h4 gext = zero4();
-		if (wave < 2) {
+		if (wave < NTAU) {
 			const uint32_t i = base + 16 * wave + c;
 			if (ext) {
 				if constexpr (OP) {
@@ -285,9 +298,11 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 			const int rsi = m == 0 ? RS0 : RSW;
 			const _Float16* Wt = streamed(m) ? nullptr : Wm(m);
 			const _Float16* in = slot(m);
-			f4 acc[MTW][2];
+			f4 acc[MTW][NTAU];
 #pragma unroll
-			for (int i = 0; i < MTW; ++i) acc[i][0] = acc[i][1] = fz;
+			for (int i = 0; i < MTW; ++i)
+#pragma unroll
+				for (int tau = 0; tau < NTAU; ++tau) acc[i][tau] = fz;
 			h8 ag[MTW][W / 32];  // a streamed layer's A fragments, all loads issued before the first MFMA
 			if (RA && streamed(m)) {
 #pragma unroll
@@ -303,26 +318,27 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 			}
 #pragma unroll
 			for (int s = 0; s < KS; ++s) {
-				const h8 b0 = *(const h8*)(in + c * rsi + 32 * s + 8 * q);
-				const h8 b1 = *(const h8*)(in + (16 + c) * rsi + 32 * s + 8 * q);
+				h8 b[NTAU];
+#pragma unroll
+				for (int tau = 0; tau < NTAU; ++tau) b[tau] = *(const h8*)(in + (16 * tau + c) * rsi + 32 * s + 8 * q);
 #pragma unroll
 				for (int i = 0; i < MTW; ++i) {
 					const h8 af = streamed(m) ? ag[i][s] : *(const h8*)(Wt + (16 * (wave * MTW + i) + c) * rsi + 32 * s + 8 * q);
-					acc[i][0] = mfma16(af, b0, acc[i][0]);
-					acc[i][1] = mfma16(af, b1, acc[i][1]);
+#pragma unroll
+					for (int tau = 0; tau < NTAU; ++tau) acc[i][tau] = mfma16(af, b[tau], acc[i][tau]);
 				}
 			}
 			_Float16* outs = slot(m + 1);
 #pragma unroll
 			for (int i = 0; i < MTW; ++i)
 #pragma unroll
-				for (int tau = 0; tau < 2; ++tau)
+				for (int tau = 0; tau < NTAU; ++tau)
 					*(h4*)(outs + (16 * tau + c) * RSW + 16 * (wave * MTW + i) + 4 * q) = tile_act<ACT>(acc[i][tau]);
 			__syncthreads();
 		}
 
-		// ---- output layer (+ output activation) + loss + output transfer (waves 0, 1: tau = wave) ----
-		if (wave < 2) {
+		// ---- output layer (+ output activation) + loss + output transfer (waves 0 .. NTAU-1: tau = wave) ----
+		if (wave < NTAU) {
 			const int tau = wave;
 			const _Float16* aN = slot(NH);
 			f4 y = fz;
@@ -367,15 +383,18 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 		__syncthreads();
 
 		// ---- dWout += G^T a_NH ; delta_NH = act'(a_NH) * (Wout^T G) ----
-		h4 dl[MTW][2];
+		h4 dl[MTW][NTAU];
 		{
 			const _Float16* aN = slot(NH);
-			const h8 ga = lds_trfrag(sG, RSG, q, c, 0);  // A[out c][sample 8q+e]
 #pragma unroll
-			for (int i = 0; i < NTW; ++i) dWo[i] = mfma16(ga, lds_trfrag(aN, RSW, q, c, wave * NTW + i), dWo[i]);
-			h8 gb[2];
+			for (int kh = 0; kh < KH; ++kh) {
+				const h8 ga = lds_trfrag(sG + 32 * kh * RSG, RSG, q, c, 0);  // A[out c][sample 32kh+8q+e]
 #pragma unroll
-			for (int tau = 0; tau < 2; ++tau) gb[tau] = q < 2 ? *(const h8*)(sG + (16 * tau + c) * RSG + 8 * q) : zero8();
+				for (int i = 0; i < NTW; ++i) dWo[i] = mfma16(ga, lds_trfrag(aN + 32 * kh * RSW, RSW, q, c, wave * NTW + i), dWo[i]);
+			}
+			h8 gb[NTAU];
+#pragma unroll
+			for (int tau = 0; tau < NTAU; ++tau) gb[tau] = q < 2 ? *(const h8*)(sG + (16 * tau + c) * RSG + 8 * q) : zero8();
 #pragma unroll
 			for (int i = 0; i < MTW; ++i) {
 				const int mt = wave * MTW + i;
@@ -384,7 +403,7 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 				// ds_read_b64_tr_b16 exchange under a partial EXEC mask returned garbage (NaN deltas).
 				const h8 af = lds_trfrag(smem + L::oWo, RSW, q & 1, c, mt);
 #pragma unroll
-				for (int tau = 0; tau < 2; ++tau) {
+				for (int tau = 0; tau < NTAU; ++tau) {
 					const f4 v = mfma16(af, gb[tau], fz);
 					dl[i][tau] = act_bwd<ACT>(*(const h4*)(aN + (16 * tau + c) * RSW + 16 * mt + 4 * q), v);
 				}
@@ -396,7 +415,7 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 #pragma unroll
 			for (int i = 0; i < MTW; ++i)
 #pragma unroll
-				for (int tau = 0; tau < 2; ++tau) *(h4*)(aN + (16 * tau + c) * RSW + 16 * (wave * MTW + i) + 4 * q) = dl[i][tau];
+				for (int tau = 0; tau < NTAU; ++tau) *(h4*)(aN + (16 * tau + c) * RSW + 16 * (wave * MTW + i) + 4 * q) = dl[i][tau];
 		}
 		__syncthreads();
 
@@ -421,52 +440,59 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 #pragma unroll
 					for (int s = 0; s < W / 32; ++s) agT[i][s] = *(const h8*)(WgT + (size_t)(16 * (wave * MTW + i) + c) * W + 32 * s + 8 * q);
 			}
-			// dW_m += delta_{m+1} a_m^T (contraction over the tile's 32 samples)
+			// dW_m += delta_{m+1} a_m^T (contraction over the tile's samples, 32 per MFMA)
 #pragma unroll
-			for (int i = 0; i < MTW; ++i) {
-				const h8 ad = lds_trfrag(dsl, RSW, q, c, wave * MTW + i);  // A[neuron][sample]
-				if (m == 0) {
+			for (int i = 0; i < MTW; ++i)
 #pragma unroll
-					for (int k = 0; k < KT0; ++k) dW0[i][k] = mfma16(ad, lds_trfrag(am, rsm, q, c, k), dW0[i][k]);
-				} else {
+				for (int kh = 0; kh < KH; ++kh) {
+					const h8 ad = lds_trfrag(dsl + 32 * kh * RSW, RSW, q, c, wave * MTW + i);  // A[neuron][sample]
+					const _Float16* amk = am + 32 * kh * rsm;
+					if (m == 0) {
 #pragma unroll
-					for (int k = 0; k < L::MT; ++k) dWh[m > 0 ? m - 1 : 0][i][k] = mfma16(ad, lds_trfrag(am, rsm, q, c, k), dWh[m > 0 ? m - 1 : 0][i][k]);
+						for (int k = 0; k < KT0; ++k) dW0[i][k] = mfma16(ad, lds_trfrag(amk, rsm, q, c, k), dW0[i][k]);
+					} else {
+#pragma unroll
+						for (int k = 0; k < L::MT; ++k) dWh[m > 0 ? m - 1 : 0][i][k] = mfma16(ad, lds_trfrag(amk, rsm, q, c, k), dWh[m > 0 ? m - 1 : 0][i][k]);
+					}
 				}
-			}
 			// delta_m = act'(a_m) * (M_m^T delta_{m+1})  (m == 0: dL/d(encoding), no transfer)
 			const _Float16* Mt = streamed(m) ? nullptr : Wm(m);
 			if (m > 0) {
 #pragma unroll
 				for (int i = 0; i < MTW; ++i) {
 					const int t = wave * MTW + i;
-					f4 v0 = fz, v1 = fz;
+					f4 v[NTAU];
+#pragma unroll
+					for (int tau = 0; tau < NTAU; ++tau) v[tau] = fz;
 #pragma unroll
 					for (int s = 0; s < W / 32; ++s) {
 						const h8 af = streamed(m) ? agT[i][s] : lds_trfrag(Mt + 32 * s * rsm, rsm, q, c, t);  // A[feature][neuron 32s+8q+e]
-						v0 = mfma16(af, *(const h8*)(dsl + c * RSW + 32 * s + 8 * q), v0);
-						v1 = mfma16(af, *(const h8*)(dsl + (16 + c) * RSW + 32 * s + 8 * q), v1);
+#pragma unroll
+						for (int tau = 0; tau < NTAU; ++tau) v[tau] = mfma16(af, *(const h8*)(dsl + (16 * tau + c) * RSW + 32 * s + 8 * q), v[tau]);
 					}
-					dl[i][0] = act_bwd<ACT>(*(const h4*)(am + c * rsm + 16 * t + 4 * q), v0);
-					dl[i][1] = act_bwd<ACT>(*(const h4*)(am + (16 + c) * rsm + 16 * t + 4 * q), v1);
+#pragma unroll
+					for (int tau = 0; tau < NTAU; ++tau) dl[i][tau] = act_bwd<ACT>(*(const h4*)(am + (16 * tau + c) * rsm + 16 * t + 4 * q), v[tau]);
 				}
 				__syncthreads();
 				_Float16* dst = slot(m);  // a_m is dead: delta_m takes its slot
 #pragma unroll
 				for (int i = 0; i < MTW; ++i)
 #pragma unroll
-					for (int tau = 0; tau < 2; ++tau) *(h4*)(dst + (16 * tau + c) * RSW + 16 * (wave * MTW + i) + 4 * q) = dl[i][tau];
+					for (int tau = 0; tau < NTAU; ++tau) *(h4*)(dst + (16 * tau + c) * RSW + 16 * (wave * MTW + i) + 4 * q) = dl[i][tau];
 				__syncthreads();
 			} else if (a.dldenc) {
 				for (int t = wave; t < KT0; t += WAVES) {
-					f4 v[2] = {fz, fz};
+					f4 v[NTAU];
+#pragma unroll
+					for (int tau = 0; tau < NTAU; ++tau) v[tau] = fz;
 #pragma unroll
 					for (int s = 0; s < W / 32; ++s) {
 						const h8 af = lds_trfrag(Mt + 32 * s * RS0, RS0, q, c, t);
 #pragma unroll
-						for (int tau = 0; tau < 2; ++tau) v[tau] = mfma16(af, *(const h8*)(dsl + (16 * tau + c) * RSW + 32 * s + 8 * q), v[tau]);
+						for (int tau = 0; tau < NTAU; ++tau) v[tau] = mfma16(af, *(const h8*)(dsl + (16 * tau + c) * RSW + 32 * s + 8 * q), v[tau]);
 					}
 #pragma unroll
-					for (int tau = 0; tau < 2; ++tau) {
+					for (int tau = 0; tau < NTAU; ++tau) {
 						const h4 d = __builtin_convertvector(v[tau], h4);
 						const uint32_t i = base + 16 * tau + c;
 						if (a.dldenc_pairs) {  // features 16t + 4q + r -> levels 8t + 2q (r = 0, 1), + 1 (r = 2, 3)
@@ -703,11 +729,14 @@ struct TileShapeInfo {
 	uint32_t lds_bytes, n_streamed, wg_per_cu, waves;  // training (the variant tile_ra_selected picks)
 	uint32_t infer_lds_bytes, infer_wg_per_cu, infer_tile;
 	uint32_t reg_a;                                    // 1: the register-resident training variant
+	uint32_t ts64;                                     // 1: 64-sample tiles (batches that are a multiple of 64)
 };
 
 // whether the training launch of a shape with tile_ra_ok takes the register-resident variant (its
 // default policy, TCNN_TILE_REG_A=0/1 overrides; read once per process)
 bool tile_ra_selected(uint32_t W, uint32_t IN, uint32_t NH);
+// whether shapes with tile_ts64_ok run 64-sample tiles (default; TCNN_TILE_SAMPLES=32 selects 32)
+bool tile_ts64_selected();
 
 // per-width entry points (one translation unit per width); false if (IN, NH) is not instantiated
 bool tile_shape_w16(uint32_t IN, uint32_t NH, TileShapeInfo* info);
@@ -728,30 +757,46 @@ inline void tile_info_fill(TileShapeInfo* info) {
 	using L = TileLayout<WR, IN, NH>;
 	using LI = TileInferLayout<WR, IN, NH>;
 	*info = TileShapeInfo{(uint32_t)L::BYTES, (uint32_t)L::NS, (uint32_t)L::WG_PER_CU, (uint32_t)L::WAVES,
-	                      (uint32_t)LI::BYTES, (uint32_t)LI::WG_PER_CU, (uint32_t)LI::T, 0u};
+	                      (uint32_t)LI::BYTES, (uint32_t)LI::WG_PER_CU, (uint32_t)LI::T, 0u, 0u};
 	if constexpr (tile_ra_ok(tile_kw(WR), IN, NH)) {
 		if (tile_ra_selected(WR, IN, NH)) {
 			using LR = TileLayout<WR, IN, NH, true>;
 			info->lds_bytes = LR::BYTES, info->n_streamed = LR::NS, info->wg_per_cu = LR::WG_PER_CU, info->waves = LR::WAVES;
 			info->reg_a = 1u;
+			return;
+		}
+	}
+	if constexpr (tile_ts64_ok(tile_kw(WR), IN, NH, false)) {
+		if (tile_ts64_selected()) {
+			// the 64-sample variant's layout; a batch that is not a multiple of 64 runs the 32-sample kernel,
+			// which streams no more matrices (the transposed copy is sized for the larger count)
+			using L6 = TileLayout<WR, IN, NH, false, 64>;
+			info->lds_bytes = tile_imax(L::BYTES, L6::BYTES), info->n_streamed = L6::NS, info->wg_per_cu = tile_imin(L::WG_PER_CU, L6::WG_PER_CU);
+			info->ts64 = 1u;
 		}
 	}
 }
 
 // the definitions of one width's entry points (used once per mlp_tile_w*.hip)
 #define TCNN_TILE_WIDTH_TU(w)                                                                                                    \
-	template <int IN, int NH, Act A, bool RA>                                                                                    \
+	template <int IN, int NH, Act A, bool RA, int TS = 32>                                                                       \
 	static void tile_train_launch_v_##w(hipStream_t st, uint32_t blocks, const TileTrainArgs& a) {                               \
-		using L = TileLayout<w, IN, NH, RA>;                                                                                     \
+		using L = TileLayout<w, IN, NH, RA, TS>;                                                                                 \
 		static uint64_t done = 0;                                                                                                \
-		set_dyn_lds((const void*)k_mlp_tile_train<w, IN, NH, A, RA>, L::BYTES, done);                                            \
-		hipLaunchKernelGGL((k_mlp_tile_train<w, IN, NH, A, RA>), dim3(blocks), dim3(L::NTHR), L::BYTES, st, a);                 \
+		set_dyn_lds((const void*)k_mlp_tile_train<w, IN, NH, A, RA, TS>, L::BYTES, done);                                        \
+		hipLaunchKernelGGL((k_mlp_tile_train<w, IN, NH, A, RA, TS>), dim3(blocks), dim3(L::NTHR), L::BYTES, st, a);             \
 	}                                                                                                                            \
 	template <int IN, int NH, Act A>                                                                                             \
 	static void tile_train_launch_##w(hipStream_t st, uint32_t blocks, const TileTrainArgs& a) {                                 \
 		if constexpr (tile_ra_ok(tile_kw(w), IN, NH)) {                                                                          \
 			if (tile_ra_selected(w, IN, NH)) {                                                                                   \
 				tile_train_launch_v_##w<IN, NH, A, true>(st, blocks, a);                                                         \
+				return;                                                                                                          \
+			}                                                                                                                    \
+		}                                                                                                                        \
+		if constexpr (tile_ts64_ok(tile_kw(w), IN, NH, false)) {                                                                 \
+			if (tile_ts64_selected() && a.B % 64 == 0) {                                                                         \
+				tile_train_launch_v_##w<IN, NH, A, false, 64>(st, blocks, a);                                                    \
 				return;                                                                                                          \
 			}                                                                                                                    \
 		}                                                                                                                        \

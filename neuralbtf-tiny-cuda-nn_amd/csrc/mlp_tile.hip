@@ -17,6 +17,14 @@ bool tile_ra_selected(uint32_t W, uint32_t IN, uint32_t NH) {
 	return env != 0;
 }
 
+bool tile_ts64_selected() {
+	static const bool on = [] {
+		const char* e = std::getenv("TCNN_TILE_SAMPLES");
+		return !(e && std::atoi(e) == 32);
+	}();
+	return on;
+}
+
 static bool tile_shape(uint32_t W, uint32_t IN, uint32_t NH, TileShapeInfo* info) {
 	switch (W) {
 		case 16: return tile_shape_w16(IN, NH, info);
@@ -77,7 +85,8 @@ uint32_t tile_train_blocks(uint32_t B, uint32_t W, uint32_t IN, uint32_t NH) {
 		return e ? std::atoi(e) : 0;
 	}();
 	if (env > 0) per_cu = std::min(std::max(1u, (uint32_t)env), std::max(1u, (160u * 1024u) / i.lds_bytes));
-	return std::max(1u, std::min(cu_count() * per_cu, B / 32));
+	const uint32_t ts = i.ts64 && B % 64 == 0 ? 64u : 32u;
+	return std::max(1u, std::min(cu_count() * per_cu, B / ts));
 }
 
 void launch_mlp_tile_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, int act, int out_act, uint32_t B, uint32_t dims,

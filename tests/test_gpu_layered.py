@@ -61,6 +61,10 @@ CONFIGS = {
     # (config_oneblob as-is: NS = 2; IN 128 with 4 hidden layers: NS = 1; HashGrid W128/H5: NS = 2)
     "oneblob_w128_h4": (_cfg({"otype": "OneBlob", "n_bins": 64}, _net(128, 4)), 2e-3),
     "hashgrid_w128_h5": (_cfg(CONFIG_HASH["encoding"], _net(128, 5)), 2e-3),
+    # 64-sample tiles of the 8-wave W128 kernel (mlp_tile.h tile_ts64_ok; hashgrid_w128_h4 above too): IN 128
+    # with 3 hidden layers (one hidden matrix moves to L2 to make room for the tile), 1 hidden layer
+    "oneblob_w128_h3": (_cfg({"otype": "OneBlob", "n_bins": 64}, _net(128, 3)), 2e-3),
+    "identity_w128_h1": (_cfg({"otype": "Identity"}, _net(128, 1)), 1e-3),
     # widths above 128 (k_wide_layer + blocked k_wgrad; reference cutlass_mlp.cu:41-81, fully_fused_mlp.cu:591):
     # CutlassMLP W256, an encoding 256 wide (HashGrid L32 F8) into FullyFusedMLP W64, CutlassMLP with no
     # hidden layer (one [16][128] matrix, cutlass_mlp.cu:64-67)
@@ -71,7 +75,8 @@ CONFIGS = {
 }
 # FullyFusedMLP configurations the tile engine trains (engine "fused"); the rest run layer by layer
 TILE = {"oneblob_w64_h2", "oneblob16_w64_h2", "hashgrid_w128_h4", "identity_w64_h3", "oneblob_w64_h5", "hashgrid_w128_h2",
-        "oneblob_as_file_w128_h5", "oneblob_w128_h4", "hashgrid_w128_h5", "identity_w32_h3"}
+        "oneblob_as_file_w128_h5", "oneblob_w128_h4", "hashgrid_w128_h5", "identity_w32_h3", "oneblob_w128_h3",
+        "identity_w128_h1"}
 # the same shapes with the tile engine switched off run on the layer-wise engine
 LAYERED_AB = ["oneblob_as_file_w128_h5", "hashgrid_w128_h4"]
 
