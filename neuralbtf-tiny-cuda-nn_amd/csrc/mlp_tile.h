@@ -43,8 +43,9 @@ constexpr int tile_imin(int a, int b) { return a < b ? a : b; }
 // ---------------------------------------------------------------------------------------------
 // LDS halves of a tile workgroup of TS-sample tiles with the first NS hidden matrices streamed from L2
 // instead of staged
+constexpr int tile_rsw(int W) { return W + 8; }  // row stride of the W-wide LDS buffers (halves)
 constexpr int tile_halves(int W, int IN, int NH, int NS, int TS = 32) {
-	const int KP0 = (IN + 31) / 32 * 32, RS0 = KP0 + 8, RSW = W + 8, RSG = 24;
+	const int KP0 = (IN + 31) / 32 * 32, RS0 = KP0 + 8, RSW = tile_rsw(W), RSG = 24;
 	return W * RS0 + (NH - 1 - NS) * W * RSW + 16 * RSW + TS * RS0 + NH * TS * RSW + TS * RSG;
 }
 // waves per workgroup: W128 runs 8 (2 per SIMD, one 16-row tile of every matrix each) up to 4 hidden
@@ -98,7 +99,10 @@ struct TileLayout {
 	static_assert(IN % 16 == 0 && IN <= 128, "tile engine: IN a multiple of 16, <= 128");
 	static_assert(!RA || tile_ra_ok(W, IN, NH), "register-resident variant: shape out of its register budget");
 	static constexpr int KP0 = (IN + 31) / 32 * 32;  // K of the first layer, padded to the MFMA depth
-	static constexpr int RS0 = KP0 + 8, RSW = W + 8, RSG = 24;
+	// W-wide buffers (hidden matrices, Wout, activation slots): rows padded by 16 B; W128 rows also swap
+	// the 16-byte chunks of each pair in rows 4..11 of every 16 (tile_ix)
+	static constexpr bool SWZ = W == 128;
+	static constexpr int RS0 = KP0 + 8, RSW = tile_rsw(W), RSG = 24;
 	static constexpr int WAVES = tile_waves(W, NH, RA), NTHR = WAVES * 64;
 	static constexpr int MT = W / 16, MTW = MT / WAVES;  // output-row tiles per matrix / per wave
 	static constexpr int KT0 = IN / 16;              // feature tiles of the input
@@ -124,6 +128,45 @@ struct TileLayout {
 	static_assert(oWh % 8 == 0 && oWo % 8 == 0 && oX % 8 == 0 && oA % 8 == 0 && oG % 8 == 0, "16-byte alignment");
 	static_assert(BYTES <= tile_lds_limit(), "tile exceeds the LDS");
 };
+
+// W128 LDS swizzle: in rows r with r % 16 in 4..11 the two 16-byte chunks of every 32-byte pair trade
+// places (chunk c -> c ^ 1). Chunk bit 0 comes from the lane in every access of the kernel (row-fragment
+// ds_read_b128: q & 1; ds_read_b64_tr_b16: (c >> 1) & 1; h4 loads / stores: q >> 1), so the swap stays a
+// per-lane constant and every compile-time offset remains an immediate. Searched over all per-row
+// bit-0 swaps against the kernel's access patterns (64-wide banking of ds_read_b128 in its 4 x 16 lane
+// groups and of ds_read_b64[_tr_b16] in 2 x 32, 32-wide of ds_write_b64 in 4 x 16) at the 272-byte row
+// stride: the row-fragment reads become conflict-free (2-way before: lanes c = 11, q = 1 and c = 12,
+// q = 0 met on one slot), transpose reads and stores stay 2-way, h4 loads go 1 -> 2-way; weighted by
+// the configs[3] kernel's instruction mix, 23 % fewer LDS cycles. (A full chunk XOR makes the
+// transpose reads conflict-free too, but its per-access offsets are lane-dependent XORs the compiler
+// keeps in registers: 50-140 spills at 256 VGPRs.)
+__device__ __forceinline__ int tile_swz(int r) { return (((r & 15) + 4) >> 3) & 1; }
+template <bool SWZ, int RS>
+__device__ __forceinline__ int tile_ix(int row, int col) {
+	if constexpr (SWZ) return row * RS + (col ^ (tile_swz(row) << 3));
+	else return row * RS + col;
+}
+// the same with the column split into a part that is a multiple of 16 (compile-time / wave-uniform) and
+// the lane's part (< 16, holding bit 3): the swap touches only the lane's part, so the compiler keeps one
+// per-lane base and folds the rest into immediate offsets
+template <bool SWZ, int RS>
+__device__ __forceinline__ int tile_ix(int row, int col16, int col_lane) {
+	if constexpr (SWZ) return row * RS + col16 + (col_lane ^ (tile_swz(row) << 3));
+	else return row * RS + col16 + col_lane;
+}
+// lds_trfrag on a (possibly swizzled) buffer: lane (c, q) receives S[8q + e][16 tile + c], e = 0..7
+template <bool SWZ, int RS>
+__device__ __forceinline__ h8 tile_trfrag(const _Float16* S, int q, int c, int tile) {
+	if constexpr (!SWZ) {
+		return lds_trfrag(S, RS, q, c, tile);
+	} else {
+		typedef __attribute__((address_space(3))) s4 lds_s4;
+		const int row = 8 * q + (c >> 2);
+		const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(S + tile_ix<true, RS>(row, 16 * tile, 4 * (c & 3))));
+		const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(S + tile_ix<true, RS>(row + 4, 16 * tile, 4 * (c & 3))));
+		return cat8(__builtin_bit_cast(h4, lo), __builtin_bit_cast(h4, hi));
+	}
+}
 
 struct TileTrainArgs {
 	uint32_t B, dims, loss_l2;
@@ -170,9 +213,30 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 	constexpr int MTW = L::MTW, KT0 = L::KT0, RS0 = L::RS0, RSW = L::RSW, RSG = L::RSG;
 	constexpr int WAVES = L::WAVES, NTHR = L::NTHR;
 	constexpr int NTW = L::MT / WAVES;  // Wout column tiles per wave (= MTW)
+	constexpr bool SWZ = L::SWZ;
 	extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
 	const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 	const int c = lane & 15, q = lane >> 4;
+	// The lane's part of every LDS address, computed once (with the W128 swizzle, tile_ix): the accesses
+	// below add only compile-time / wave-uniform offsets, which the compiler folds into the instructions'
+	// immediate offsets instead of keeping one address register per access.
+	//   row fragment (ds_read_b128): row 16 k + c, columns 32 s + 8 q ..+7    -> lf + 16 k RS + 32 s
+	//   h4 (ds_read_b64 / ds_write_b64): row 16 k + c, columns 16 t + 4 q ..+3 -> l4 + 16 k RS + 16 t
+	//   transpose read (tile_trfrag): rows 8 q + (c >> 2) and + 4, columns 16 t + 4 (c & 3) ..+3
+	const int lf = tile_ix<SWZ, RSW>(c, 0, 8 * q), l4 = tile_ix<SWZ, RSW>(c, 0, 4 * q), lf0 = c * RS0 + 8 * q;
+	const int ltr = tile_ix<SWZ, RSW>(8 * q + (c >> 2), 0, 4 * (c & 3)), ltr4 = tile_ix<SWZ, RSW>(8 * q + (c >> 2) + 4, 0, 4 * (c & 3));
+	const int lto = tile_ix<SWZ, RSW>(8 * (q & 1) + (c >> 2), 0, 4 * (c & 3)), lto4 = tile_ix<SWZ, RSW>(8 * (q & 1) + (c >> 2) + 4, 0, 4 * (c & 3));
+	auto ixf = [&](bool x0, int row16, int col32) { return x0 ? row16 * RS0 + col32 + lf0 : row16 * RSW + col32 + lf; };
+	auto ix4 = [&](int row16, int col16) { return row16 * RSW + col16 + l4; };
+	auto trpair = [](const _Float16* lo, const _Float16* hi) {
+		typedef __attribute__((address_space(3))) s4 lds_s4;
+		const s4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)lo);
+		const s4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)hi);
+		return cat8(__builtin_bit_cast(h4, a), __builtin_bit_cast(h4, b));
+	};
+	// S[8q + e][16 t + c] of a W-wide buffer (Wout: the rows 8 (q & 1) + e of its 16)
+	auto trw = [&](const _Float16* S, int t) { return trpair(S + ltr + 16 * t, S + ltr4 + 16 * t); };
+	auto trwo = [&](const _Float16* S, int t) { return trpair(S + lto + 16 * t, S + lto4 + 16 * t); };
 	const f4 fz = {0.0f, 0.0f, 0.0f, 0.0f};
 	float* wloss = (float*)(smem + L::HALVES);
 	const bool ext = a.dout != nullptr;
@@ -193,13 +257,13 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 		for (int idx = tid; idx < (NH - 1 - L::NS) * W * (W / 8); idx += NTHR) {
 			const int r = idx / (W / 8), c8 = idx % (W / 8);  // r over the staged hidden rows
 			const int j = r / W + L::NS, rr = r % W;
-			*(h8*)(smem + L::oWh + r * RSW + 8 * c8) =
+			*(h8*)(smem + L::oWh + (r / W) * W * RSW + tile_ix<SWZ, RSW>(rr, 8 * c8)) =
 			    (rr < WR && 8 * c8 < WR) ? *(const h8*)(p + ((size_t)j * WR + rr) * WR + 8 * c8) : zero8();
 		}
 		p += (NH - 1) * WR * WR;
 		for (int idx = tid; idx < 16 * (W / 8); idx += NTHR) {
 			const int r = idx / (W / 8), c8 = idx % (W / 8);
-			*(h8*)(smem + L::oWo + (OP ? out_row(r) : r) * RSW + 8 * c8) = 8 * c8 < WR ? *(const h8*)(p + (size_t)r * WR + 8 * c8) : zero8();
+			*(h8*)(smem + L::oWo + tile_ix<SWZ, RSW>(OP ? out_row(r) : r, 8 * c8)) = 8 * c8 < WR ? *(const h8*)(p + (size_t)r * WR + 8 * c8) : zero8();
 		}
 		// zero the padded input columns of slot 0 once (the input loads never write them)
 		if (L::KP0 > IN)
@@ -270,17 +334,21 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 		}
 		if (tile + gridDim.x < n_tiles) load_x(tile + gridDim.x);
 		// targets / external dL/dy of this wave's output lanes (waves 0 .. NTAU-1: 16-sample column tau = wave)
+		// (the external dL/dy's h4 rides in tg[0..1]: the two cases exclude each other, 2 registers saved)
 		float tg[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-		h4 gext = zero4();
+		typedef float tile_f2 __attribute__((ext_vector_type(2)));
 		if (wave < NTAU) {
 			const uint32_t i = base + 16 * wave + c;
 			if (ext) {
+				h4 gext;
 				if constexpr (OP) {
 					const _Float16* dp = a.dout + (size_t)i * 16 + q;
 					gext = h4{dp[0], dp[4], dp[8], dp[12]};
 				} else {
 					gext = *(const h4*)(a.dout + (size_t)i * 16 + 4 * q);
 				}
+				const tile_f2 gb2 = __builtin_bit_cast(tile_f2, gext);
+				tg[0] = gb2[0], tg[1] = gb2[1];
 			} else if constexpr (OP) {  // register 0 only: outputs 4.. of a wider network are read in the loss
 				if (q < (int)a.dims) tg[0] = a.target[(size_t)i * a.dims + q];
 			} else {
@@ -295,7 +363,6 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 #pragma unroll
 		for (int m = 0; m < NH; ++m) {
 			const int KS = (m == 0 ? L::KP0 : W) / 32;
-			const int rsi = m == 0 ? RS0 : RSW;
 			const _Float16* Wt = streamed(m) ? nullptr : Wm(m);
 			const _Float16* in = slot(m);
 			f4 acc[MTW][NTAU];
@@ -320,10 +387,10 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 			for (int s = 0; s < KS; ++s) {
 				h8 b[NTAU];
 #pragma unroll
-				for (int tau = 0; tau < NTAU; ++tau) b[tau] = *(const h8*)(in + (16 * tau + c) * rsi + 32 * s + 8 * q);
+				for (int tau = 0; tau < NTAU; ++tau) b[tau] = *(const h8*)(in + ixf(m == 0, 16 * tau, 32 * s));
 #pragma unroll
 				for (int i = 0; i < MTW; ++i) {
-					const h8 af = streamed(m) ? ag[i][s] : *(const h8*)(Wt + (16 * (wave * MTW + i) + c) * rsi + 32 * s + 8 * q);
+					const h8 af = streamed(m) ? ag[i][s] : *(const h8*)(Wt + ixf(m == 0, 16 * (wave * MTW + i), 32 * s));
 #pragma unroll
 					for (int tau = 0; tau < NTAU; ++tau) acc[i][tau] = mfma16(af, b[tau], acc[i][tau]);
 				}
@@ -333,7 +400,7 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 			for (int i = 0; i < MTW; ++i)
 #pragma unroll
 				for (int tau = 0; tau < NTAU; ++tau)
-					*(h4*)(outs + (16 * tau + c) * RSW + 16 * (wave * MTW + i) + 4 * q) = tile_act<ACT>(acc[i][tau]);
+					*(h4*)(outs + ix4(16 * tau, 16 * (wave * MTW + i))) = tile_act<ACT>(acc[i][tau]);
 			__syncthreads();
 		}
 
@@ -344,7 +411,7 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 			f4 y = fz;
 #pragma unroll
 			for (int s = 0; s < W / 32; ++s)
-				y = mfma16(*(const h8*)(smem + L::oWo + c * RSW + 32 * s + 8 * q), *(const h8*)(aN + (16 * tau + c) * RSW + 32 * s + 8 * q), y);
+				y = mfma16(*(const h8*)(smem + L::oWo + ixf(false, 0, 32 * s)), *(const h8*)(aN + ixf(false, 16 * tau, 32 * s)), y);
 			const uint32_t i = base + 16 * tau + c;
 			const h4 yh = out_act_fwd(a.out_act, y);
 			if (a.out) {
@@ -357,7 +424,7 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 			}
 			h4 g = zero4();
 			if (ext) {
-				g = gext;
+				g = __builtin_bit_cast(h4, tile_f2{tg[0], tg[1]});
 			} else {
 #pragma unroll
 				for (int r = 0; r < 4; ++r) {
@@ -390,7 +457,7 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 			for (int kh = 0; kh < KH; ++kh) {
 				const h8 ga = lds_trfrag(sG + 32 * kh * RSG, RSG, q, c, 0);  // A[out c][sample 32kh+8q+e]
 #pragma unroll
-				for (int i = 0; i < NTW; ++i) dWo[i] = mfma16(ga, lds_trfrag(aN + 32 * kh * RSW, RSW, q, c, wave * NTW + i), dWo[i]);
+				for (int i = 0; i < NTW; ++i) dWo[i] = mfma16(ga, trw(aN + 32 * kh * RSW, wave * NTW + i), dWo[i]);
 			}
 			h8 gb[NTAU];
 #pragma unroll
@@ -401,11 +468,11 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 				// A[neuron][out 8q+e]: K = 16 outputs, the upper half of the MFMA depth is zero through gb.
 				// Every lane takes part in the transpose read (lanes q >= 2 re-read rows 0..15): the
 				// ds_read_b64_tr_b16 exchange under a partial EXEC mask returned garbage (NaN deltas).
-				const h8 af = lds_trfrag(smem + L::oWo, RSW, q & 1, c, mt);
+				const h8 af = trwo(smem + L::oWo, mt);
 #pragma unroll
 				for (int tau = 0; tau < NTAU; ++tau) {
 					const f4 v = mfma16(af, gb[tau], fz);
-					dl[i][tau] = act_bwd<ACT>(*(const h4*)(aN + (16 * tau + c) * RSW + 16 * mt + 4 * q), v);
+					dl[i][tau] = act_bwd<ACT>(*(const h4*)(aN + ix4(16 * tau, 16 * mt)), v);
 				}
 			}
 		}
@@ -415,7 +482,7 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 #pragma unroll
 			for (int i = 0; i < MTW; ++i)
 #pragma unroll
-				for (int tau = 0; tau < NTAU; ++tau) *(h4*)(aN + (16 * tau + c) * RSW + 16 * (wave * MTW + i) + 4 * q) = dl[i][tau];
+				for (int tau = 0; tau < NTAU; ++tau) *(h4*)(aN + ix4(16 * tau, 16 * (wave * MTW + i))) = dl[i][tau];
 		}
 		__syncthreads();
 
@@ -445,14 +512,14 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 			for (int i = 0; i < MTW; ++i)
 #pragma unroll
 				for (int kh = 0; kh < KH; ++kh) {
-					const h8 ad = lds_trfrag(dsl + 32 * kh * RSW, RSW, q, c, wave * MTW + i);  // A[neuron][sample]
+					const h8 ad = trw(dsl + 32 * kh * RSW, wave * MTW + i);  // A[neuron][sample]
 					const _Float16* amk = am + 32 * kh * rsm;
 					if (m == 0) {
 #pragma unroll
-						for (int k = 0; k < KT0; ++k) dW0[i][k] = mfma16(ad, lds_trfrag(amk, rsm, q, c, k), dW0[i][k]);
+						for (int k = 0; k < KT0; ++k) dW0[i][k] = mfma16(ad, lds_trfrag(amk, RS0, q, c, k), dW0[i][k]);
 					} else {
 #pragma unroll
-						for (int k = 0; k < L::MT; ++k) dWh[m > 0 ? m - 1 : 0][i][k] = mfma16(ad, lds_trfrag(amk, rsm, q, c, k), dWh[m > 0 ? m - 1 : 0][i][k]);
+						for (int k = 0; k < L::MT; ++k) dWh[m > 0 ? m - 1 : 0][i][k] = mfma16(ad, trw(amk, k), dWh[m > 0 ? m - 1 : 0][i][k]);
 					}
 				}
 			// delta_m = act'(a_m) * (M_m^T delta_{m+1})  (m == 0: dL/d(encoding), no transfer)
@@ -466,19 +533,19 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 					for (int tau = 0; tau < NTAU; ++tau) v[tau] = fz;
 #pragma unroll
 					for (int s = 0; s < W / 32; ++s) {
-						const h8 af = streamed(m) ? agT[i][s] : lds_trfrag(Mt + 32 * s * rsm, rsm, q, c, t);  // A[feature][neuron 32s+8q+e]
+						const h8 af = streamed(m) ? agT[i][s] : trw(Mt + 32 * s * rsm, t);  // A[feature][neuron 32s+8q+e]
 #pragma unroll
-						for (int tau = 0; tau < NTAU; ++tau) v[tau] = mfma16(af, *(const h8*)(dsl + (16 * tau + c) * RSW + 32 * s + 8 * q), v[tau]);
+						for (int tau = 0; tau < NTAU; ++tau) v[tau] = mfma16(af, *(const h8*)(dsl + ixf(false, 16 * tau, 32 * s)), v[tau]);
 					}
 #pragma unroll
-					for (int tau = 0; tau < NTAU; ++tau) dl[i][tau] = act_bwd<ACT>(*(const h4*)(am + (16 * tau + c) * rsm + 16 * t + 4 * q), v[tau]);
+					for (int tau = 0; tau < NTAU; ++tau) dl[i][tau] = act_bwd<ACT>(*(const h4*)(am + ix4(16 * tau, 16 * t)), v[tau]);
 				}
 				__syncthreads();
 				_Float16* dst = slot(m);  // a_m is dead: delta_m takes its slot
 #pragma unroll
 				for (int i = 0; i < MTW; ++i)
 #pragma unroll
-					for (int tau = 0; tau < NTAU; ++tau) *(h4*)(dst + (16 * tau + c) * RSW + 16 * (wave * MTW + i) + 4 * q) = dl[i][tau];
+					for (int tau = 0; tau < NTAU; ++tau) *(h4*)(dst + ix4(16 * tau, 16 * (wave * MTW + i))) = dl[i][tau];
 				__syncthreads();
 			} else if (a.dldenc) {
 				for (int t = wave; t < KT0; t += WAVES) {
@@ -489,7 +556,7 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 					for (int s = 0; s < W / 32; ++s) {
 						const h8 af = lds_trfrag(Mt + 32 * s * RS0, RS0, q, c, t);
 #pragma unroll
-						for (int tau = 0; tau < NTAU; ++tau) v[tau] = mfma16(af, *(const h8*)(dsl + (16 * tau + c) * RSW + 32 * s + 8 * q), v[tau]);
+						for (int tau = 0; tau < NTAU; ++tau) v[tau] = mfma16(af, *(const h8*)(dsl + ixf(false, 16 * tau, 32 * s)), v[tau]);
 					}
 #pragma unroll
 					for (int tau = 0; tau < NTAU; ++tau) {

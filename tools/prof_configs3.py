@@ -13,7 +13,7 @@ B = 1 << 20
 t = Trainer(2, 3, cfg, seed=1337)
 pos = torch.rand(B, 2, device="cuda")
 tgt = rgb_field_torch(pos)
-for _ in range(25):
+for _ in range(int(os.environ.get("STEPS", "25"))):
     t.training_step(pos, tgt)
 torch.cuda.synchronize()
 print("loss", t.loss(), "engine", t.engine)
