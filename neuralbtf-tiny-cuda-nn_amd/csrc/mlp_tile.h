@@ -99,9 +99,11 @@ struct TileLayout {
 	static_assert(IN % 16 == 0 && IN <= 128, "tile engine: IN a multiple of 16, <= 128");
 	static_assert(!RA || tile_ra_ok(W, IN, NH), "register-resident variant: shape out of its register budget");
 	static constexpr int KP0 = (IN + 31) / 32 * 32;  // K of the first layer, padded to the MFMA depth
-	// W-wide buffers (hidden matrices, Wout, activation slots): rows padded by 16 B; W128 rows also swap
-	// the 16-byte chunks of each pair in rows 4..11 of every 16 (tile_ix)
-	static constexpr bool SWZ = W == 128;
+	// every LDS matrix (W0 and the input slot [.][RS0], the hidden matrices, Wout and the activation slots
+	// [.][RSW]): rows padded by 16 B, and the 16-byte chunks of each pair swapped in rows 4..11 of every 16
+	// (tile_ix) -- except W0 and the input slot of the 4-wave W128 kernel (5 hidden layers), whose
+	// swizzled transposes cost 12 more spilled registers at its 512-register bound
+	static constexpr bool SWZ = true, SWZ0 = !(W == 128 && tile_waves(W, NH, RA) == 4);
 	static constexpr int RS0 = KP0 + 8, RSW = tile_rsw(W), RSG = 24;
 	static constexpr int WAVES = tile_waves(W, NH, RA), NTHR = WAVES * 64;
 	static constexpr int MT = W / 16, MTW = MT / WAVES;  // output-row tiles per matrix / per wave
@@ -129,7 +131,7 @@ struct TileLayout {
 	static_assert(BYTES <= tile_lds_limit(), "tile exceeds the LDS");
 };
 
-// W128 LDS swizzle: in rows r with r % 16 in 4..11 the two 16-byte chunks of every 32-byte pair trade
+// Tile LDS swizzle: in rows r with r % 16 in 4..11 the two 16-byte chunks of every 32-byte pair trade
 // places (chunk c -> c ^ 1). Chunk bit 0 comes from the lane in every access of the kernel (row-fragment
 // ds_read_b128: q & 1; ds_read_b64_tr_b16: (c >> 1) & 1; h4 loads / stores: q >> 1), so the swap stays a
 // per-lane constant and every compile-time offset remains an immediate. Searched over all per-row
@@ -154,20 +156,6 @@ __device__ __forceinline__ int tile_ix(int row, int col16, int col_lane) {
 	if constexpr (SWZ) return row * RS + col16 + (col_lane ^ (tile_swz(row) << 3));
 	else return row * RS + col16 + col_lane;
 }
-// lds_trfrag on a (possibly swizzled) buffer: lane (c, q) receives S[8q + e][16 tile + c], e = 0..7
-template <bool SWZ, int RS>
-__device__ __forceinline__ h8 tile_trfrag(const _Float16* S, int q, int c, int tile) {
-	if constexpr (!SWZ) {
-		return lds_trfrag(S, RS, q, c, tile);
-	} else {
-		typedef __attribute__((address_space(3))) s4 lds_s4;
-		const int row = 8 * q + (c >> 2);
-		const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(S + tile_ix<true, RS>(row, 16 * tile, 4 * (c & 3))));
-		const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(S + tile_ix<true, RS>(row + 4, 16 * tile, 4 * (c & 3))));
-		return cat8(__builtin_bit_cast(h4, lo), __builtin_bit_cast(h4, hi));
-	}
-}
-
 struct TileTrainArgs {
 	uint32_t B, dims, loss_l2;
 	float loss_scale, n_total;
@@ -213,7 +201,7 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 	constexpr int MTW = L::MTW, KT0 = L::KT0, RS0 = L::RS0, RSW = L::RSW, RSG = L::RSG;
 	constexpr int WAVES = L::WAVES, NTHR = L::NTHR;
 	constexpr int NTW = L::MT / WAVES;  // Wout column tiles per wave (= MTW)
-	constexpr bool SWZ = L::SWZ;
+	constexpr bool SWZ = L::SWZ, SWZ0 = L::SWZ0;
 	extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
 	const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 	const int c = lane & 15, q = lane >> 4;
@@ -222,8 +210,9 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 	// immediate offsets instead of keeping one address register per access.
 	//   row fragment (ds_read_b128): row 16 k + c, columns 32 s + 8 q ..+7    -> lf + 16 k RS + 32 s
 	//   h4 (ds_read_b64 / ds_write_b64): row 16 k + c, columns 16 t + 4 q ..+3 -> l4 + 16 k RS + 16 t
-	//   transpose read (tile_trfrag): rows 8 q + (c >> 2) and + 4, columns 16 t + 4 (c & 3) ..+3
-	const int lf = tile_ix<SWZ, RSW>(c, 0, 8 * q), l4 = tile_ix<SWZ, RSW>(c, 0, 4 * q), lf0 = c * RS0 + 8 * q;
+	//   transpose read (trw / trwo / trx): rows 8 q + (c >> 2) and + 4, columns 16 t + 4 (c & 3) ..+3
+	const int lf = tile_ix<SWZ, RSW>(c, 0, 8 * q), l4 = tile_ix<SWZ, RSW>(c, 0, 4 * q), lf0 = tile_ix<SWZ0, RS0>(c, 0, 8 * q);
+	const int ltx = tile_ix<SWZ0, RS0>(8 * q + (c >> 2), 0, 4 * (c & 3)), ltx4 = tile_ix<SWZ0, RS0>(8 * q + (c >> 2) + 4, 0, 4 * (c & 3));
 	const int ltr = tile_ix<SWZ, RSW>(8 * q + (c >> 2), 0, 4 * (c & 3)), ltr4 = tile_ix<SWZ, RSW>(8 * q + (c >> 2) + 4, 0, 4 * (c & 3));
 	const int lto = tile_ix<SWZ, RSW>(8 * (q & 1) + (c >> 2), 0, 4 * (c & 3)), lto4 = tile_ix<SWZ, RSW>(8 * (q & 1) + (c >> 2) + 4, 0, 4 * (c & 3));
 	auto ixf = [&](bool x0, int row16, int col32) { return x0 ? row16 * RS0 + col32 + lf0 : row16 * RSW + col32 + lf; };
@@ -237,6 +226,10 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 	// S[8q + e][16 t + c] of a W-wide buffer (Wout: the rows 8 (q & 1) + e of its 16)
 	auto trw = [&](const _Float16* S, int t) { return trpair(S + ltr + 16 * t, S + ltr4 + 16 * t); };
 	auto trwo = [&](const _Float16* S, int t) { return trpair(S + lto + 16 * t, S + lto4 + 16 * t); };
+	auto trx = [&](const _Float16* S, int t) {  // [.][RS0] buffers
+		if constexpr (SWZ0) return trpair(S + ltx + 16 * t, S + ltx4 + 16 * t);
+		else return lds_trfrag(S, RS0, q, c, t);
+	};
 	const f4 fz = {0.0f, 0.0f, 0.0f, 0.0f};
 	float* wloss = (float*)(smem + L::HALVES);
 	const bool ext = a.dout != nullptr;
@@ -251,7 +244,7 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 		const _Float16* p = a.params;
 		for (int idx = tid; idx < W * (L::KP0 / 8); idx += NTHR) {
 			const int r = idx / (L::KP0 / 8), c8 = idx % (L::KP0 / 8);
-			*(h8*)(smem + L::oW0 + r * RS0 + 8 * c8) = (r < WR && 8 * c8 < IN) ? *(const h8*)(p + (size_t)r * IN + 8 * c8) : zero8();
+			*(h8*)(smem + L::oW0 + tile_ix<SWZ0, RS0>(r, 8 * c8)) = (r < WR && 8 * c8 < IN) ? *(const h8*)(p + (size_t)r * IN + 8 * c8) : zero8();
 		}
 		p += WR * IN;
 		for (int idx = tid; idx < (NH - 1 - L::NS) * W * (W / 8); idx += NTHR) {
@@ -268,7 +261,7 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 		// zero the padded input columns of slot 0 once (the input loads never write them)
 		if (L::KP0 > IN)
 			for (int idx = tid; idx < TS * (L::KP0 - IN); idx += NTHR)
-				smem[L::oX + (idx / (L::KP0 - IN)) * RS0 + IN + idx % (L::KP0 - IN)] = (_Float16)0.0f;
+				smem[L::oX + tile_ix<SWZ0, RS0>(idx / (L::KP0 - IN), IN + idx % (L::KP0 - IN))] = (_Float16)0.0f;
 	}
 	// staged matrices (m == 0 or m > NS); streamed ones (1 <= m <= NS) are read from global memory
 	auto Wm = [&](int m) -> const _Float16* { return m == 0 ? smem + L::oW0 : smem + L::oWh + (m - 1 - L::NS) * W * RSW; };
@@ -330,7 +323,7 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 #pragma unroll
 		for (int j = 0; j < XPT; ++j) {
 			const int idx = tid + NTHR * j;
-			if (idx < XV) *(h8*)(slot(0) + (idx / (IN / 8)) * RS0 + 8 * (idx % (IN / 8))) = xr[j];
+			if (idx < XV) *(h8*)(slot(0) + tile_ix<SWZ0, RS0>(idx / (IN / 8), 8 * (idx % (IN / 8)))) = xr[j];
 		}
 		if (tile + gridDim.x < n_tiles) load_x(tile + gridDim.x);
 		// targets / external dL/dy of this wave's output lanes (waves 0 .. NTAU-1: 16-sample column tau = wave)
@@ -516,7 +509,7 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 					const _Float16* amk = am + 32 * kh * rsm;
 					if (m == 0) {
 #pragma unroll
-						for (int k = 0; k < KT0; ++k) dW0[i][k] = mfma16(ad, lds_trfrag(amk, RS0, q, c, k), dW0[i][k]);
+						for (int k = 0; k < KT0; ++k) dW0[i][k] = mfma16(ad, trx(amk, k), dW0[i][k]);
 					} else {
 #pragma unroll
 						for (int k = 0; k < L::MT; ++k) dWh[m > 0 ? m - 1 : 0][i][k] = mfma16(ad, trw(amk, k), dWh[m > 0 ? m - 1 : 0][i][k]);
@@ -554,7 +547,7 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 					for (int tau = 0; tau < NTAU; ++tau) v[tau] = fz;
 #pragma unroll
 					for (int s = 0; s < W / 32; ++s) {
-						const h8 af = lds_trfrag(Mt + 32 * s * RS0, RS0, q, c, t);
+						const h8 af = trx(Mt + 32 * s * RS0, t);
 #pragma unroll
 						for (int tau = 0; tau < NTAU; ++tau) v[tau] = mfma16(af, *(const h8*)(dsl + ixf(false, 16 * tau, 32 * s)), v[tau]);
 					}

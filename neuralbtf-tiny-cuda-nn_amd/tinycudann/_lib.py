@@ -89,6 +89,7 @@ _SIGS = {
     "tcnn_trainer_update_hyperparams": (c_int, [c_void_p, c_char_p]),
     "tcnn_trainer_hyperparams": (c_char_p, [c_void_p]),
     "tcnn_trainer_initialize_params": (c_int, [c_void_p, c_uint32]),
+    "tcnn_trainer_initialize_params_rng": (c_int, [c_void_p, c_void_p, c_uint64]),
     "tcnn_trainer_engine": (c_char_p, [c_void_p]),
     "tcnn_trainer_optimizer_state": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "tcnn_dp_unique_id": (c_int, [c_void_p]),

@@ -31,6 +31,11 @@ def main():
     c = copy.deepcopy(ob); c["network"] = net(128, 2); cases.append(("OneBlob64+W128/H2 (IN 128)", c, 18))
     c = copy.deepcopy(ob); c["encoding"] = {"otype": "OneBlob", "n_bins": 32}; c["network"] = net(128, 4)
     cases.append(("OneBlob32+W128/H4 (IN 64)", c, 18))
+    # the other tile-engine configurations (W64, W128/H5: the TCNN_TILE_SAMPLES switch does not apply)
+    c = copy.deepcopy(ob); c["network"] = net(64, 2); cases.append(("configs[1] OneBlob64+W64/H2", c, 18))
+    c = copy.deepcopy(ob); c["encoding"] = {"otype": "OneBlob", "n_bins": 32}; c["network"] = net(64, 4)
+    cases.append(("sample default OneBlob32+W64/H4", c, 18))
+    cases.append(("config_oneblob as-is OneBlob64+W128/H5 (IN 128)", copy.deepcopy(ob), 18))
     iters = int(os.environ.get("ITERS", "30"))
     ts = os.environ.get("TCNN_TILE_SAMPLES", "default")
     for name, cfg, lb in cases:
