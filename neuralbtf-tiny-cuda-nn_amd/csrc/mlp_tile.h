@@ -226,6 +226,21 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 	// S[8q + e][16 t + c] of a W-wide buffer (Wout: the rows 8 (q & 1) + e of its 16)
 	auto trw = [&](const _Float16* S, int t) { return trpair(S + ltr + 16 * t, S + ltr4 + 16 * t); };
 	auto trwo = [&](const _Float16* S, int t) { return trpair(S + lto + 16 * t, S + lto4 + 16 * t); };
+	// Sample-indexed transposes (the weight-gradient operands: rows are the tile's samples, the MFMA's K):
+	// the lo read takes the even rows 8 q + 2 j and the hi read the odd ones (j = c >> 2), so each 32-lane
+	// half reads 8 rows two apart -- conflict-free at every row stride (rows four apart, as in trw, put two
+	// rows' 32-byte segments on overlapping banks: 2-way). K index 8 q + e then holds sample 8 q + 2 e
+	// (lo) / 8 q + 2 e + 1 (hi) in both operands of an MFMA, a permutation of its sum, so every
+	// weight-gradient MFMA reads both operands this way. (Not in the 4-wave W128 kernel: at its
+	// 512-register bound the extra lane offsets cost 13 spilled registers; it keeps rows four apart.)
+	const int lts = SWZ0 ? tile_ix<SWZ, RSW>(8 * q + 2 * (c >> 2), 0, 4 * (c & 3)) : 0;
+	const int lts1 = SWZ0 ? tile_ix<SWZ, RSW>(8 * q + 2 * (c >> 2) + 1, 0, 4 * (c & 3)) : 0;
+	const int ltsx = SWZ0 ? tile_ix<SWZ0, RS0>(8 * q + 2 * (c >> 2), 0, 4 * (c & 3)) : 0;
+	const int ltsx1 = SWZ0 ? tile_ix<SWZ0, RS0>(8 * q + 2 * (c >> 2) + 1, 0, 4 * (c & 3)) : 0;
+	const int ltsg = SWZ0 ? (8 * q + 2 * (c >> 2)) * RSG + 4 * (c & 3) : 0;
+	auto trs = [&](const _Float16* S, int t) { return trpair(S + lts + 16 * t, S + lts1 + 16 * t); };
+	auto trsx = [&](const _Float16* S, int t) { return trpair(S + ltsx + 16 * t, S + ltsx1 + 16 * t); };
+	auto trsg = [&](const _Float16* S) { return trpair(S + ltsg, S + ltsg + RSG); };
 	auto trx = [&](const _Float16* S, int t) {  // [.][RS0] buffers
 		if constexpr (SWZ0) return trpair(S + ltx + 16 * t, S + ltx4 + 16 * t);
 		else return lds_trfrag(S, RS0, q, c, t);
@@ -448,9 +463,15 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 			const _Float16* aN = slot(NH);
 #pragma unroll
 			for (int kh = 0; kh < KH; ++kh) {
-				const h8 ga = lds_trfrag(sG + 32 * kh * RSG, RSG, q, c, 0);  // A[out c][sample 32kh+8q+e]
+				if constexpr (SWZ0) {
+					const h8 ga = trsg(sG + 32 * kh * RSG);  // A[out c][sample 32kh+8q+e] (even/odd rows)
 #pragma unroll
-				for (int i = 0; i < NTW; ++i) dWo[i] = mfma16(ga, trw(aN + 32 * kh * RSW, wave * NTW + i), dWo[i]);
+					for (int i = 0; i < NTW; ++i) dWo[i] = mfma16(ga, trs(aN + 32 * kh * RSW, wave * NTW + i), dWo[i]);
+				} else {
+					const h8 ga = lds_trfrag(sG + 32 * kh * RSG, RSG, q, c, 0);  // A[out c][sample 32kh+8q+e]
+#pragma unroll
+					for (int i = 0; i < NTW; ++i) dWo[i] = mfma16(ga, trw(aN + 32 * kh * RSW, wave * NTW + i), dWo[i]);
+				}
 			}
 			h8 gb[NTAU];
 #pragma unroll
@@ -505,14 +526,25 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 			for (int i = 0; i < MTW; ++i)
 #pragma unroll
 				for (int kh = 0; kh < KH; ++kh) {
-					const h8 ad = trw(dsl + 32 * kh * RSW, wave * MTW + i);  // A[neuron][sample]
 					const _Float16* amk = am + 32 * kh * rsm;
-					if (m == 0) {
+					if constexpr (SWZ0) {
+						const h8 ad = trs(dsl + 32 * kh * RSW, wave * MTW + i);  // A[neuron][sample] (even/odd rows)
+						if (m == 0) {
 #pragma unroll
-						for (int k = 0; k < KT0; ++k) dW0[i][k] = mfma16(ad, trx(amk, k), dW0[i][k]);
+							for (int k = 0; k < KT0; ++k) dW0[i][k] = mfma16(ad, trsx(amk, k), dW0[i][k]);
+						} else {
+#pragma unroll
+							for (int k = 0; k < L::MT; ++k) dWh[m > 0 ? m - 1 : 0][i][k] = mfma16(ad, trs(amk, k), dWh[m > 0 ? m - 1 : 0][i][k]);
+						}
 					} else {
+						const h8 ad = trw(dsl + 32 * kh * RSW, wave * MTW + i);  // A[neuron][sample]
+						if (m == 0) {
 #pragma unroll
-						for (int k = 0; k < L::MT; ++k) dWh[m > 0 ? m - 1 : 0][i][k] = mfma16(ad, trw(amk, k), dWh[m > 0 ? m - 1 : 0][i][k]);
+							for (int k = 0; k < KT0; ++k) dW0[i][k] = mfma16(ad, trx(amk, k), dW0[i][k]);
+						} else {
+#pragma unroll
+							for (int k = 0; k < L::MT; ++k) dWh[m > 0 ? m - 1 : 0][i][k] = mfma16(ad, trw(amk, k), dWh[m > 0 ? m - 1 : 0][i][k]);
+						}
 					}
 				}
 			// delta_m = act'(a_m) * (M_m^T delta_{m+1})  (m == 0: dL/d(encoding), no transfer)
