@@ -44,9 +44,10 @@ constexpr int tile_imin(int a, int b) { return a < b ? a : b; }
 // LDS halves of a tile workgroup of TS-sample tiles with the first NS hidden matrices streamed from L2
 // instead of staged
 constexpr int tile_rsw(int W) { return W + 8; }  // row stride of the W-wide LDS buffers (halves)
-constexpr int tile_halves(int W, int IN, int NH, int NS, int TS = 32) {
+// (PP: one more [TS][RSW] slot, the backward's ping-pong delta buffer, tile_pp_ok)
+constexpr int tile_halves(int W, int IN, int NH, int NS, int TS = 32, int PP = 0) {
 	const int KP0 = (IN + 31) / 32 * 32, RS0 = KP0 + 8, RSW = tile_rsw(W), RSG = 24;
-	return W * RS0 + (NH - 1 - NS) * W * RSW + 16 * RSW + TS * RS0 + NH * TS * RSW + TS * RSG;
+	return W * RS0 + (NH - 1 - NS) * W * RSW + 16 * RSW + TS * RS0 + (NH + PP) * TS * RSW + TS * RSG;
 }
 // waves per workgroup: W128 runs 8 (2 per SIMD, one 16-row tile of every matrix each) up to 4 hidden
 // layers; with 5 its weight-gradient accumulators (>= 164 registers) spill at 256 registers per wave,
@@ -69,10 +70,10 @@ constexpr int tile_waves(int W, int NH, bool RA = false) { return W == 128 && NH
 constexpr int tile_lds_limit() { return 160 * 1024; }
 // fewest streamed hidden matrices that let the rest of the network + the tile's activations fit
 // (RA: all of them, from registers)
-constexpr int tile_n_streamed(int W, int IN, int NH, bool RA = false, int TS = 32) {
+constexpr int tile_n_streamed(int W, int IN, int NH, bool RA = false, int TS = 32, int PP = 0) {
 	if (RA) return NH - 1;
 	int ns = 0;
-	while (ns < NH - 1 && tile_halves(W, IN, NH, ns, TS) * 2 + tile_waves(W, NH) * 4 > tile_lds_limit()) ++ns;
+	while (ns < NH - 1 && tile_halves(W, IN, NH, ns, TS, PP) * 2 + tile_waves(W, NH) * 4 > tile_lds_limit()) ++ns;
 	return ns;
 }
 // 64-sample tiles (TS = 64): half the workgroup barriers per sample (each layer's barrier now covers
@@ -86,10 +87,21 @@ constexpr bool tile_ts64_ok(int W, int IN, int NH, bool RA) {
 }
 // workgroups per CU the launch aims for: two waves per SIMD where the LDS (and, for W128 RA, the
 // registers) allow
-constexpr int tile_train_wg_per_cu(int W, int IN, int NH, bool RA = false, int TS = 32) {
+constexpr int tile_train_wg_per_cu(int W, int IN, int NH, bool RA = false, int TS = 32, int PP = 0) {
 	return W == 128 && RA ? 1
 	                      : tile_imax(1, tile_imin(8 / tile_waves(W, NH, RA),
-	                                               tile_lds_limit() / (tile_halves(W, IN, NH, tile_n_streamed(W, IN, NH, RA, TS), TS) * 2 + tile_waves(W, NH, RA) * 4)));
+	                                               tile_lds_limit() / (tile_halves(W, IN, NH, tile_n_streamed(W, IN, NH, RA, TS, PP), TS, PP) * 2 +
+	                                                                   tile_waves(W, NH, RA) * 4)));
+}
+// Ping-pong delta buffer (PP): the backward writes delta_k into a spare [TS][RSW] slot or into a_NH's
+// slot, alternating (delta_NH -> spare, delta_{NH-1} -> a_NH's slot, delta_{NH-2} -> spare, ...), so a
+// delta never overwrites an operand another wave may still be reading and each backward layer needs
+// one workgroup barrier instead of two (H4: 15 -> 11 per tile). Taken wherever the spare slot fits
+// without streaming another hidden matrix or losing a workgroup per CU.
+constexpr bool tile_pp_ok(int W, int IN, int NH, bool RA, int TS) {
+	return tile_n_streamed(W, IN, NH, RA, TS, 1) == tile_n_streamed(W, IN, NH, RA, TS, 0) &&
+	       tile_train_wg_per_cu(W, IN, NH, RA, TS, 1) == tile_train_wg_per_cu(W, IN, NH, RA, TS, 0) &&
+	       tile_halves(W, IN, NH, tile_n_streamed(W, IN, NH, RA, TS, 1), TS, 1) * 2 + tile_waves(W, NH, RA) * 4 <= tile_lds_limit();
 }
 
 template <int WR, int IN, int NH, bool RA = false, int TS = 32>
@@ -111,7 +123,8 @@ struct TileLayout {
 	// hidden matrices 1..NS are not staged: their forward A fragments come from the fp16 parameters
 	// (L2-resident, every workgroup reads the same 32 KB), their backward ones from a transposed copy
 	// (RA: loaded once into registers)
-	static constexpr int NS = tile_n_streamed(W, IN, NH, RA, TS);
+	static constexpr int PP = tile_pp_ok(W, IN, NH, RA, TS) ? 1 : 0;
+	static constexpr int NS = tile_n_streamed(W, IN, NH, RA, TS, PP);
 	static constexpr int NTAU = TS / 16, KH = TS / 32;  // 16-sample MFMA columns / 32-sample K halves per tile
 	static_assert(TS == 32 || (TS == 64 && tile_ts64_ok(W, IN, NH, RA)), "tile samples: 32, or 64 where tile_ts64_ok");
 	static_assert(NTAU <= WAVES, "one wave per 16-sample column of the output layer");
@@ -120,14 +133,15 @@ struct TileLayout {
 	static constexpr int oX = oWo + 16 * RSW;                 // slot 0: the tile's input [TS][RS0]
 	static constexpr int oA = oX + TS * RS0;                  // slots 1..NH: [TS][RSW]
 	static constexpr int oG = oA + NH * TS * RSW;             // dL/dy of the tile [TS][RSG]
-	static constexpr int HALVES = oG + TS * RSG;
+	static constexpr int oD = oG + TS * RSG;                  // PP: the spare delta slot [TS][RSW]
+	static constexpr int HALVES = oD + PP * TS * RSW;
 	static constexpr int BYTES = HALVES * 2 + WAVES * 4;       // + per-wave loss
 	static constexpr int N_MLP = WR * IN + (NH - 1) * WR * WR + 16 * WR;  // parameters (unpadded)
-	static constexpr int WG_PER_CU = tile_train_wg_per_cu(W, IN, NH, RA, TS);
+	static constexpr int WG_PER_CU = tile_train_wg_per_cu(W, IN, NH, RA, TS, PP);
 	// waves per SIMD the launch runs (amdgpu_waves_per_eu: caps the registers so they fit)
 	static constexpr int WAVES_PER_EU = tile_imax(1, WG_PER_CU * WAVES / 4);
-	static_assert(HALVES == tile_halves(W, IN, NH, NS, TS), "layout");
-	static_assert(oWh % 8 == 0 && oWo % 8 == 0 && oX % 8 == 0 && oA % 8 == 0 && oG % 8 == 0, "16-byte alignment");
+	static_assert(HALVES == tile_halves(W, IN, NH, NS, TS, PP), "layout");
+	static_assert(oWh % 8 == 0 && oWo % 8 == 0 && oX % 8 == 0 && oA % 8 == 0 && oG % 8 == 0 && oD % 8 == 0, "16-byte alignment");
 	static_assert(BYTES <= tile_lds_limit(), "tile exceeds the LDS");
 };
 
@@ -191,7 +205,8 @@ __device__ __forceinline__ h4 out_act_fwd(int a, f4 y) {
 // launch bounds as plain function calls (a template-id's commas would split the macro arguments)
 constexpr int tile_train_nthr(int WR, int NH, bool RA) { return tile_waves(tile_kw(WR), NH, RA) * 64; }
 constexpr int tile_train_weu(int WR, int IN, int NH, bool RA, int TS) {
-	return tile_imax(1, tile_train_wg_per_cu(tile_kw(WR), IN, NH, RA, TS) * tile_waves(tile_kw(WR), NH, RA) / 4);
+	return tile_imax(1, tile_train_wg_per_cu(tile_kw(WR), IN, NH, RA, TS, tile_pp_ok(tile_kw(WR), IN, NH, RA, TS) ? 1 : 0) *
+	                        tile_waves(tile_kw(WR), NH, RA) / 4);
 }
 
 template <int WR, int IN, int NH, Act ACT, bool RA, int TS>
@@ -282,6 +297,8 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 	auto Wm = [&](int m) -> const _Float16* { return m == 0 ? smem + L::oW0 : smem + L::oWh + (m - 1 - L::NS) * W * RSW; };
 	auto streamed = [](int m) { return m >= 1 && m <= L::NS; };
 	auto slot = [&](int m) -> _Float16* { return m == 0 ? smem + L::oX : smem + L::oA + (m - 1) * TS * RSW; };
+	// where delta_k lives: PP -- the spare slot for even NH - k, a_NH's slot for odd; otherwise a_k's slot
+	auto dslot = [&](int k) -> _Float16* { return L::PP ? ((NH - k) % 2 == 0 ? smem + L::oD : slot(NH)) : slot(k); };
 	_Float16* sG = smem + L::oG;
 
 	// ---- register accumulators of this wave's weight-gradient rows ----
@@ -490,20 +507,20 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 				}
 			}
 		}
-		__syncthreads();
+		if constexpr (!L::PP) __syncthreads();  // a_NH is read above by every wave
 		{
-			_Float16* aN = slot(NH);
+			_Float16* dN = dslot(NH);
 #pragma unroll
 			for (int i = 0; i < MTW; ++i)
 #pragma unroll
-				for (int tau = 0; tau < NTAU; ++tau) *(h4*)(aN + ix4(16 * tau, 16 * (wave * MTW + i))) = dl[i][tau];
+				for (int tau = 0; tau < NTAU; ++tau) *(h4*)(dN + ix4(16 * tau, 16 * (wave * MTW + i))) = dl[i][tau];
 		}
 		__syncthreads();
 
 		// ---- hidden layers and the first layer, last to first ----
 #pragma unroll
 		for (int m = NH - 1; m >= 0; --m) {
-			const _Float16* dsl = slot(m + 1);  // delta_{m+1} [sample][neuron]
+			const _Float16* dsl = dslot(m + 1);  // delta_{m+1} [sample][neuron]
 			const _Float16* am = slot(m);       // a_m [sample][feature]
 			const int rsm = m == 0 ? RS0 : RSW;
 			// a streamed matrix's transposed A fragments (A[feature][neuron] = M^T rows of this wave's
@@ -565,8 +582,8 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 #pragma unroll
 					for (int tau = 0; tau < NTAU; ++tau) dl[i][tau] = act_bwd<ACT>(*(const h4*)(am + ix4(16 * tau, 16 * t)), v[tau]);
 				}
-				__syncthreads();
-				_Float16* dst = slot(m);  // a_m is dead: delta_m takes its slot
+				if constexpr (!L::PP) __syncthreads();  // without the spare slot delta_m overwrites a_m, read above
+				_Float16* dst = dslot(m);
 #pragma unroll
 				for (int i = 0; i < MTW; ++i)
 #pragma unroll
