@@ -201,3 +201,51 @@ def test_module_forward_context_reused_by_backward(torch_mod, name):
     for c in ctxs + [ctx_other]:
         lib.tcnn_context_destroy(c)
     lib.tcnn_module_destroy(m)
+
+
+_TS_SCRIPT = r"""
+import json, os, sys
+import numpy as np
+import torch
+sys.path[:0] = [sys.argv[1], os.path.join(sys.argv[1], "tests"), os.path.join(sys.argv[1], "neuralbtf-tiny-cuda-nn_amd")]
+from helpers import make_batch, trainer_arrays
+from tinycudann import Trainer
+cfg = json.loads(sys.argv[2])
+t = Trainer(2, 3, cfg, seed=1337)
+pos, tgt = make_batch(512)
+t.training_step(torch.from_numpy(pos).cuda(), torch.from_numpy(tgt).cuda(), run_optimizer=False)
+np.save(sys.argv[3], trainer_arrays(t)["g32"])
+print(json.dumps({"loss": t.loss()}))
+"""
+
+
+@pytest.mark.parametrize("name", ["configs3_hashgrid_w128_h4", "oneblob64_w128_h2"])
+def test_tile_samples_switch_matches_oracle(torch_mod, name, tmp_path):
+    """The 8-wave W128 kernel's two tile sizes (64 samples by default, TCNN_TILE_SAMPLES=32 -- read
+    once per process, so the 32-sample step runs in a child process) both match the oracle, and each
+    other within the fp32 summation-order difference of their weight-gradient sums."""
+    import os
+    import subprocess
+    import sys
+    torch = torch_mod
+    from tinycudann import Trainer
+    cfg = INFER[name] if name in INFER else _cfg({"otype": "OneBlob", "n_bins": 64}, 128, 2)
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "g32_ts32.npy"
+    env = dict(os.environ, TCNN_TILE_SAMPLES="32")
+    r = subprocess.run([sys.executable, "-c", _TS_SCRIPT, repo, json.dumps(cfg), str(out)], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    loss32 = json.loads(r.stdout.strip().splitlines()[-1])["loss"]
+    g32_ts32 = np.load(out)
+    t = Trainer(2, 3, cfg, seed=1337)
+    assert t.engine == "fused", t.engine
+    pos, tgt = make_batch(512)
+    t.training_step(torch.from_numpy(pos).cuda(), torch.from_numpy(tgt).cuda(), run_optimizer=False)
+    g64 = trainer_arrays(t)["g32"]
+    om = O.OracleModel(cfg, 2, 3, seed=1337)
+    loss_ref = om.train_step(pos, tgt, run_optimizer=False, n_threads=4)
+    for loss, g in ((t.loss(), g64), (loss32, g32_ts32)):
+        assert abs(loss - loss_ref) <= 1e-3 * abs(loss_ref), (loss, loss_ref)
+        assert rel_err(g, om.grad32) <= 2e-3
+    assert rel_err(g64, g32_ts32) <= 1e-3
