@@ -382,6 +382,18 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 					if (4 * q + r < (int)a.dims) tg[r] = a.target[(size_t)i * a.dims + 4 * q + r];
 			}
 		}
+		// streamed hidden matrices: each layer's A fragments are loaded one layer ahead (the first one
+		// before this barrier), so their L2 latency runs under the previous layer instead of in front of
+		// this layer's MFMAs (all waves of the workgroup reach a layer together: nothing else hides it)
+		auto load_ag = [&](int m, h8 (&dst)[MTW][W / 32]) {
+			const _Float16* Wg = a.params + (size_t)W * IN + (size_t)(m - 1) * W * W;
+#pragma unroll
+			for (int i = 0; i < MTW; ++i)
+#pragma unroll
+				for (int s = 0; s < W / 32; ++s) dst[i][s] = *(const h8*)(Wg + (size_t)(16 * (wave * MTW + i) + c) * W + 32 * s + 8 * q);
+		};
+		h8 agn[MTW][W / 32];
+		if (!RA && NH > 1 && streamed(1)) load_ag(1, agn);
 		__syncthreads();
 
 		// ---- forward: a_{m+1} = act(M_m a_m), this wave's output-row tiles ----
@@ -402,11 +414,11 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 #pragma unroll
 					for (int s = 0; s < W / 32; ++s) ag[i][s] = pag[m >= 1 ? m - 1 : 0][i][s];
 			} else if (streamed(m)) {
-				const _Float16* Wg = a.params + (size_t)W * IN + (size_t)(m - 1) * W * W;
 #pragma unroll
 				for (int i = 0; i < MTW; ++i)
 #pragma unroll
-					for (int s = 0; s < W / 32; ++s) ag[i][s] = *(const h8*)(Wg + (size_t)(16 * (wave * MTW + i) + c) * W + 32 * s + 8 * q);
+					for (int s = 0; s < W / 32; ++s) ag[i][s] = agn[i][s];
+				if (m + 1 < NH && streamed(m + 1)) load_ag(m + 1, agn);
 			}
 #pragma unroll
 			for (int s = 0; s < KS; ++s) {
