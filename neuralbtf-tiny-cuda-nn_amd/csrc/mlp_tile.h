@@ -486,6 +486,19 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 		}
 		__syncthreads();
 
+		// a streamed matrix's transposed A fragments (A[feature][neuron] = M^T rows of this wave's tiles)
+		// for the backward, loaded one layer ahead like the forward's -- not in the 4-wave W128 kernel, where
+		// the 32 extra registers spill at its 512-register bound
+		constexpr bool PFB = !RA && SWZ0;
+		auto load_agT = [&](int m, h8 (&dst)[MTW][W / 32]) {
+			const _Float16* WgT = a.wT + (size_t)(m - 1) * W * W;
+#pragma unroll
+			for (int i = 0; i < MTW; ++i)
+#pragma unroll
+				for (int s = 0; s < W / 32; ++s) dst[i][s] = *(const h8*)(WgT + (size_t)(16 * (wave * MTW + i) + c) * W + 32 * s + 8 * q);
+		};
+		h8 agTn[MTW][W / 32];
+		if (PFB && NH > 1 && streamed(NH - 1)) load_agT(NH - 1, agTn);
 		// ---- dWout += G^T a_NH ; delta_NH = act'(a_NH) * (Wout^T G) ----
 		h4 dl[MTW][NTAU];
 		{
@@ -543,13 +556,15 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 				for (int i = 0; i < MTW; ++i)
 #pragma unroll
 					for (int s = 0; s < W / 32; ++s) agT[i][s] = pagT[m >= 1 ? m - 1 : 0][i][s];
-			} else if (streamed(m)) {
-				const _Float16* WgT = a.wT + (size_t)(m - 1) * W * W;
+			} else if (PFB && streamed(m)) {
 #pragma unroll
 				for (int i = 0; i < MTW; ++i)
 #pragma unroll
-					for (int s = 0; s < W / 32; ++s) agT[i][s] = *(const h8*)(WgT + (size_t)(16 * (wave * MTW + i) + c) * W + 32 * s + 8 * q);
+					for (int s = 0; s < W / 32; ++s) agT[i][s] = agTn[i][s];
+			} else if (streamed(m)) {
+				load_agT(m, agT);
 			}
+			if (PFB && m - 1 >= 1 && streamed(m - 1)) load_agT(m - 1, agTn);  // the next layer's, one layer ahead
 			// dW_m += delta_{m+1} a_m^T (contraction over the tile's samples, 32 per MFMA)
 #pragma unroll
 			for (int i = 0; i < MTW; ++i)
