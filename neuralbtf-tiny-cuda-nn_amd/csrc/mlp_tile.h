@@ -84,7 +84,9 @@ constexpr int tile_n_streamed(int W, int IN, int NH, bool RA = false, int TS = 3
 // from L2, 158 KB; W128/H4 at IN 64: two instead of one, still 7 % faster with the streamed fragments
 // loaded a layer ahead).
 constexpr bool tile_ts64_ok(int W, int IN, int NH, bool RA) {
-	return !RA && W == 128 && tile_waves(W, NH) == 8 && tile_n_streamed(W, IN, NH, false, 64) <= tile_n_streamed(W, IN, NH, false, 32) + 1;
+	return (!RA && W == 128 && tile_waves(W, NH) == 8 && tile_n_streamed(W, IN, NH, false, 64) <= tile_n_streamed(W, IN, NH, false, 32) + 1) ||
+	       (RA && W == 64 && tile_ra_ok(W, IN, NH) && (IN <= 64 || NH <= 2));  // W64 register-resident: 4 waves
+	                                                                          // (IN 128 with 3+ layers spills)
 }
 // workgroups per CU the launch aims for: two waves per SIMD where the LDS (and, for W128 RA, the
 // registers) allow
@@ -900,6 +902,13 @@ inline void tile_info_fill(TileShapeInfo* info) {
 			using LR = TileLayout<WR, IN, NH, true>;
 			info->lds_bytes = LR::BYTES, info->n_streamed = LR::NS, info->wg_per_cu = LR::WG_PER_CU, info->waves = LR::WAVES;
 			info->reg_a = 1u;
+			if constexpr (tile_ts64_ok(tile_kw(WR), IN, NH, true)) {
+				if (tile_ts64_selected()) {
+					using LR6 = TileLayout<WR, IN, NH, true, 64>;
+					info->lds_bytes = tile_imax(LR::BYTES, LR6::BYTES), info->wg_per_cu = tile_imin(LR::WG_PER_CU, LR6::WG_PER_CU);
+					info->ts64 = 1u;
+				}
+			}
 			return;
 		}
 	}
@@ -927,6 +936,12 @@ inline void tile_info_fill(TileShapeInfo* info) {
 	static void tile_train_launch_##w(hipStream_t st, uint32_t blocks, const TileTrainArgs& a) {                                 \
 		if constexpr (tile_ra_ok(tile_kw(w), IN, NH)) {                                                                          \
 			if (tile_ra_selected(w, IN, NH)) {                                                                                   \
+				if constexpr (tile_ts64_ok(tile_kw(w), IN, NH, true)) {                                                          \
+					if (tile_ts64_selected() && a.B % 64 == 0) {                                                                 \
+						tile_train_launch_v_##w<IN, NH, A, true, 64>(st, blocks, a);                                             \
+						return;                                                                                                  \
+					}                                                                                                            \
+				}                                                                                                                \
 				tile_train_launch_v_##w<IN, NH, A, true>(st, blocks, a);                                                         \
 				return;                                                                                                          \
 			}                                                                                                                    \
