@@ -85,8 +85,9 @@ constexpr int tile_n_streamed(int W, int IN, int NH, bool RA = false, int TS = 3
 // loaded a layer ahead).
 constexpr bool tile_ts64_ok(int W, int IN, int NH, bool RA) {
 	return (!RA && W == 128 && tile_waves(W, NH) == 8 && tile_n_streamed(W, IN, NH, false, 64) <= tile_n_streamed(W, IN, NH, false, 32) + 1) ||
-	       (RA && W == 64 && tile_ra_ok(W, IN, NH) && (IN <= 64 || NH <= 2));  // W64 register-resident: 4 waves
-	                                                                          // (IN 128 with 3+ layers spills)
+	       // register-resident kernels, 4 waves, nothing staged: W64 (IN 128 with 3+ hidden layers spills)
+	       // and W128 (IN <= 32, <= 3 hidden layers)
+	       (RA && W == 64 && tile_ra_ok(W, IN, NH) && (IN <= 64 || NH <= 2)) || (RA && W == 128 && tile_ra_ok(W, IN, NH));
 }
 // workgroups per CU the launch aims for: two waves per SIMD where the LDS (and, for W128 RA, the
 // registers) allow

@@ -36,6 +36,9 @@ def main():
     c = copy.deepcopy(ob); c["encoding"] = {"otype": "OneBlob", "n_bins": 32}; c["network"] = net(64, 4)
     cases.append(("sample default OneBlob32+W64/H4", c, 18))
     cases.append(("config_oneblob as-is OneBlob64+W128/H5 (IN 128)", copy.deepcopy(ob), 18))
+    # the W128 register-resident kernel (IN <= 32, <= 3 hidden layers)
+    c = copy.deepcopy(hash_cfg); c["network"] = net(128, 3); cases.append(("HashGrid+W128/H3 (register-resident)", c, 20))
+    c = copy.deepcopy(hash_cfg); c["network"] = net(128, 2); cases.append(("HashGrid+W128/H2 (register-resident)", c, 20))
     iters = int(os.environ.get("ITERS", "30"))
     ts = os.environ.get("TCNN_TILE_SAMPLES", "default")
     for name, cfg, lb in cases:
