@@ -187,8 +187,10 @@ int tcnn_trainer_optimizer_step_range(tcnn_trainer* t, void* stream, uint64_t be
  * is sharded like the RCCL sharded schedule (tcnn_trainer_dp_gather_state completes it). Detach is
  * collective (every rank calls it); a trainer attached to peers must be detached by every rank before
  * it is destroyed. A rank that does not arrive within the timeout (tcnn_trainer_dp_peer_set_timeout;
- * default TCNN_PEER_TIMEOUT_S or 300 s) raises an error at the next call instead of hanging the GPU,
- * and the step that timed out leaves the parameters untouched. */
+ * default TCNN_PEER_TIMEOUT_S or 300 s) raises an error at the next call instead of hanging the GPU.
+ * A timeout while waiting for the gradients leaves the parameters untouched; a timeout while waiting
+ * for the other ranks' updated shards leaves this rank's own shard updated and the others not, so the
+ * ranks' parameters then differ: after any timeout restore every rank from a snapshot. */
 uint64_t tcnn_dp_peer_blob_bytes(void);
 int tcnn_trainer_dp_peer_export(tcnn_trainer* t, int nranks, int rank, void* blob);
 int tcnn_trainer_dp_peer_attach(tcnn_trainer* t, const void* blobs);
@@ -293,17 +295,6 @@ int tcnn_trainer_profile_begin(tcnn_trainer* t);
 /* same, recording phase events only on every `every`-th step (each event record idles the GPU briefly) */
 int tcnn_trainer_profile_begin_sampled(tcnn_trainer* t, uint32_t every);
 int tcnn_trainer_profile_end(tcnn_trainer* t, double* ms_per_phase, uint32_t n_phases, uint32_t* n_steps);
-
-/* ---- self test (layout probe for the MFMA / transpose-read operand maps) ---- */
-int tcnn_debug_probe(void* stream, float* mfma_out /* device [64*4] */, int16_t* tr_out /* device [64*8] */);
-/* Diagnostic build of the config_hash fused kernel with s_memtime stamps: per-phase wave-cycle sums
- * (0 grid encode, 1 hidden layers fwd, 2 output+loss, 3 bwd through hidden layers + their dW,
- * 4 first-layer dW, 5 dL/dx + store, 6 prologue, 7 epilogue reduction), summed over all waves, written to
- * host_cycles8[16] (slots 8.. used by newer builds). */
-int tcnn_debug_fused_phase_cycles(tcnn_trainer* t, void* stream, uint32_t n, const float* input, const float* target,
-                                  uint64_t* host_cycles8);
-/* out[i] = fma(a[i], b[i], c[i]) with the packed-fp16 FMA the grid forward uses (n_pairs half2 values) */
-int tcnn_debug_hfma(void* stream, const void* a, const void* b, const void* c, void* out, uint32_t n_pairs);
 
 #ifdef __cplusplus
 }

@@ -180,7 +180,7 @@ public:
 		// from the seed): a second call draws new values, as the reference's does
 		uint64_t state = m_rng.state;
 		detail::check_rc(tcnn_trainer_initialize_params_rng(m_h, &state, m_rng.inc));
-		m_rng.advance((int64_t)n_params());
+		m_rng.state = state;  // the generator as the engine left it (however many values it drew)
 		++m_n_steps;  // contexts of earlier steps no longer describe the parameters
 	}
 

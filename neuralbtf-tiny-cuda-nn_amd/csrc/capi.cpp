@@ -1,6 +1,7 @@
 // capi.cpp -- extern "C" boundary (include/tcnn_mi355x.h). Exceptions stop here and become return
 // codes + tcnn_last_error().
 #include "../../include/tcnn_mi355x.h"
+#include "debug_api.h"  // test-only diagnostics, not in the product header
 
 #include <algorithm>
 #include <cstring>
@@ -600,6 +601,9 @@ int tcnn_trainer_dp_peer_detach(tcnn_trainer* t) {
 }
 int tcnn_trainer_dp_peer_set_timeout(tcnn_trainer* t, double seconds) {
 	return guard([&] { t->t->dp_peer_set_timeout(seconds); });
+}
+int tcnn_debug_peer_loopback(tcnn_trainer* t, int nranks) {
+	return guard([&] { t->t->dp_peer_loopback(nranks); });
 }
 int tcnn_trainer_dp_peer_abandon(tcnn_trainer* t) {
 	return guard([&] { t->t->dp_peer_abandon(); });

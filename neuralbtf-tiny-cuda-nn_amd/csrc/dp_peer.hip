@@ -51,7 +51,7 @@ enum PeerSlot { SLOT_GRAD = 0, SLOT_WEIGHTS = 1, SLOT_GATHER = 2, SLOT_DETACH = 
 constexpr int PROBE_WORD = 16;  // the attach probe's token in each rank's counter page
 
 __host__ __device__ inline uint32_t probe_token(int rank) { return PEER_MAGIC ^ (0x9e3779b9u * (uint32_t)(rank + 1)); }
-enum PeerCtr { CTR_STEP = 0, CTR_SYNC = 1, CTR_ERR = 2 };
+enum PeerCtr { CTR_STEP = 0, CTR_SYNC = 1, CTR_ERR = 2, CTR_ARRIVE = 3 };
 
 struct PeerBlob {
 	uint32_t magic, nranks, rank, device;
@@ -114,30 +114,108 @@ __global__ void k_peer_probe(const PeerFlags fl, int nranks, int* __restrict__ e
 	}
 }
 
-// Adam on this rank's shard [a.begin, a.n) with the gradient summed over the ranks' gradient sums in
-// rank order (g_0 + g_1 + ...); the updated fp16 parameter also goes to the uncached mirror the other
-// ranks gather from
-__global__ __launch_bounds__(256) void k_peer_adam(const AdamArgs a, const AdamBuffers s, const float* const* __restrict__ gptrs,
-                                                   int nranks, _Float16* __restrict__ w16_mirror, const uint32_t* __restrict__ ctr) {
-	if (ctr[CTR_ERR]) return;  // a peer did not arrive: its gradient sums are not this step's
-	const uint32_t i = a.begin + blockIdx.x * blockDim.x + threadIdx.x;
-	if (i >= a.n) return;
-	float v[8];
-	float gsum = 0.0f;
-	for (int p0 = 0; p0 < nranks; p0 += 8) {  // loads in flight together, additions in rank order
-#pragma unroll
-		for (int u = 0; u < 8; ++u)
-			if (p0 + u < nranks) v[u] = gptrs[p0 + u][i];
-#pragma unroll
-		for (int u = 0; u < 8; ++u)
-			if (p0 + u < nranks) gsum = (p0 + u == 0) ? v[0] : gsum + v[u];  // no 0 + g_0: a -0 stays -0
+// The poll of a step kernel's head, by wave 0 of every workgroup: lane p reads rank p's flags[slot]
+// until every rank reached `target`. Returns false (and raises the error flags once) on a timeout.
+__device__ __forceinline__ bool peer_poll(const PeerFlags& fl, int nranks, int slot, uint32_t target, long long timeout_ticks,
+                                          int* __restrict__ err, uint32_t* __restrict__ ctr) {
+	const int p = threadIdx.x;
+	const long long t0 = wall_clock64();
+	for (;;) {
+		const bool ok = p >= nranks || (int32_t)(load_sys(fl.f[p] + slot) - target) >= 0;
+		const uint64_t pending = __builtin_amdgcn_ballot_w64(!ok);
+		if (pending == 0) return true;
+		if (wall_clock64() - t0 > timeout_ticks) {
+			if (p == (int)__builtin_ctzll(pending)) {
+				__hip_atomic_store(err, 1 + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+				__hip_atomic_store(ctr + CTR_ERR, 1u + (uint32_t)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			}
+			return false;
+		}
+		__builtin_amdgcn_s_sleep(1);
 	}
-	s.g32[i] = gsum;
-	w16_mirror[i] = adam_update(a, s, i, gsum);
+}
+
+struct PeerStepArgs {
+	PeerFlags fl;
+	const float* const* gptrs;  // device array [nranks] of the ranks' gradient-sum mirrors
+	_Float16* w16_mirror;       // this rank's fp16 shard mirror (the peers gather from it)
+	uint32_t* ctr;              // this rank's local counters
+	uint32_t* my_flags;         // this rank's exported counter page
+	int* err;                   // host-mapped error flag
+	long long timeout_ticks;
+	int nranks;
+};
+
+// One launch for "gradients ready -> wait -> sharded Adam -> weights ready" (r06; r05 ran a
+// one-workgroup wait kernel before and after Adam). Every workgroup reads the step number s + 1
+// from ctr[CTR_STEP], signals this rank's gradients (the same idempotent system-scope store from
+// every workgroup: the previous launches' writes went to uncached memory and ended with them), waits
+// for every rank's, runs Adam on its part of this rank's shard [a.begin, a.n) -- 4 parameters per
+// thread, the gradient of parameter i summed over the ranks' mirrors in rank order g_0 + g_1 + ...
+// -- writes the updated fp16 values to its mirror, and arrives on ctr[CTR_ARRIVE]. The last arrival
+// (every workgroup has read ctr[CTR_STEP] by then) resets the counter, bumps ctr[CTR_STEP] and
+// signals "weights ready" for the gather. Workgroups wait only on other ranks, never on each other,
+// so co-residency is not needed; the grid is sized to the shard (a few dozen workgroups at N = 8).
+__global__ __launch_bounds__(256) void k_peer_adam(const AdamArgs a, const AdamBuffers s, const PeerStepArgs pa) {
+	__shared__ int ok_s;
+	const uint32_t step = pa.ctr[CTR_STEP] + 1u;
+	if (threadIdx.x < 64) {
+		bool ok = pa.ctr[CTR_ERR] == 0u;  // an earlier wait failed: no signal, no wait (the step is abandoned)
+		if (ok && threadIdx.x == 0) __hip_atomic_store(pa.my_flags + SLOT_GRAD, step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+		if (ok) ok = peer_poll(pa.fl, pa.nranks, SLOT_GRAD, step, pa.timeout_ticks, pa.err, pa.ctr);
+		if (threadIdx.x == 0) ok_s = ok;
+	}
+	__syncthreads();
+	if (ok_s) {
+		const uint32_t stride = gridDim.x * blockDim.x * 4;
+		for (uint32_t i = a.begin + (blockIdx.x * blockDim.x + threadIdx.x) * 4; i < a.n; i += stride) {
+			if (i + 4 <= a.n) {
+				f4 g = *(const f4*)(pa.gptrs[0] + i);
+				for (int p0 = 1; p0 < pa.nranks; p0 += 8) {  // loads in flight together, additions in rank order
+					f4 v[8];
+#pragma unroll
+					for (int u = 0; u < 8; ++u)
+						if (p0 + u < pa.nranks) v[u] = *(const f4*)(pa.gptrs[p0 + u] + i);
+#pragma unroll
+					for (int u = 0; u < 8; ++u)
+						if (p0 + u < pa.nranks) g += v[u];
+				}
+				*(f4*)(s.g32 + i) = g;
+				const float gs[4] = {g.x, g.y, g.z, g.w};
+				AdamState4 st = adam_load4(s, i);
+				adam_store4(a, s, i, gs, st);
+				*(h4*)(pa.w16_mirror + i) = *(const h4*)(s.w16 + i);
+			} else {
+				for (uint32_t k = i; k < a.n; ++k) {
+					float g = pa.gptrs[0][k];
+					for (int p = 1; p < pa.nranks; ++p) g += pa.gptrs[p][k];
+					s.g32[k] = g;
+					pa.w16_mirror[k] = adam_update(a, s, k, g);
+				}
+			}
+		}
+	}
+	// what the peers read of this launch is the fp16 mirror, in UNCACHED memory: no L2 holds it, so
+	// every storing wave's vmcnt(0) wait (its stores complete) before the workgroup's arrival, and the
+	// arrival before the signal, order it (no release fence: an agent- or system-scope one writes back
+	// the XCD's whole L2, ~2-7 us, for the w32 / moment stores nobody else reads)
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		const uint32_t prev = __hip_atomic_fetch_add(pa.ctr + CTR_ARRIVE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		if (prev == gridDim.x - 1u) {  // the last arrival: every workgroup's mirror stores have completed
+			__hip_atomic_store(pa.ctr + CTR_ARRIVE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			__hip_atomic_store(pa.ctr + CTR_STEP, step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			if (__hip_atomic_load(pa.ctr + CTR_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+				__hip_atomic_store(pa.my_flags + SLOT_WEIGHTS, step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+		}
+	}
 }
 
 // copy every other rank's shard of up to 4 buffers (blockIdx.y) from its mirror into the local arrays,
-// 16 bytes per thread; shard bytes are multiples of 16
+// 16 bytes per thread in a grid-stride loop; shard bytes are multiples of 16. With poll != 0 (the
+// training step) wave 0 of every workgroup first waits until every rank signalled "weights ready"
+// for step ctr[CTR_STEP] (r06: was a one-workgroup wait kernel of its own).
 struct PeerGatherArgs {
 	uint8_t* local[4];
 	const uint8_t* const* peers[4];  // device arrays [nranks] of the peers' mirrors
@@ -145,18 +223,35 @@ struct PeerGatherArgs {
 	uint32_t elem_bytes[4];
 	uint32_t nranks, rank;
 	uint64_t per;  // elements per shard
-	const uint32_t* ctr;  // CTR_ERR set: the peers' mirrors are not this step's, copy nothing
+	uint32_t* ctr;  // CTR_ERR set: the peers' mirrors are not this step's, copy nothing
+	PeerFlags fl;
+	int* err;
+	long long timeout_ticks;
+	int poll;
 };
 __global__ __launch_bounds__(256) void k_peer_gather(const PeerGatherArgs g) {
-	if (g.ctr[CTR_ERR]) return;
+	__shared__ int ok_s;
+	if (g.poll) {
+		if (threadIdx.x < 64) {
+			bool ok = g.ctr[CTR_ERR] == 0u;
+			if (ok) ok = peer_poll(g.fl, (int)g.nranks, SLOT_WEIGHTS, g.ctr[CTR_STEP], g.timeout_ticks, g.err, g.ctr);
+			if (threadIdx.x == 0) ok_s = ok;
+		}
+		__syncthreads();
+		if (!ok_s) return;
+	} else if (g.ctr[CTR_ERR]) {
+		return;
+	}
 	const uint32_t b = blockIdx.y;
 	const uint64_t shard_bytes = g.per * g.elem_bytes[b];
-	const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // 16-byte unit over all ranks' shards
 	const uint64_t units = shard_bytes / 16;
-	const uint64_t p = q / units;
-	if (p >= g.nranks || p == g.rank) return;
-	const uint64_t off = p * shard_bytes + (q % units) * 16;
-	*(uint4*)(g.local[b] + off) = *(const uint4*)(g.peers[b][p] + g.peer_offset[b] + off);
+	const uint64_t total = units * g.nranks;
+	for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (uint64_t)gridDim.x * blockDim.x) {
+		const uint64_t p = q / units;  // 16-byte unit q over all ranks' shards
+		if (p == g.rank) continue;
+		const uint64_t off = p * shard_bytes + (q % units) * 16;
+		*(uint4*)(g.local[b] + off) = *(const uint4*)(g.peers[b][p] + g.peer_offset[b] + off);
+	}
 }
 
 // this rank's shard of the optimizer state into its uncached staging mirror (for the peers' gather)
@@ -223,6 +318,7 @@ void TrainerHost::dp_peer_set_timeout(double seconds) {
 	TCNN_CHECK(seconds > 0.0, "peer exchange: the timeout must be positive");
 	peer_timeout_s = seconds;
 	if (peer) peer->timeout_ticks = (long long)((double)peer->clock_khz * 1000.0 * seconds);
+	if (graph) set_graph(use_graph);  // captured peer steps carry the old timeout as a kernel argument
 }
 
 void TrainerHost::peer_check() const {
@@ -337,6 +433,32 @@ void TrainerHost::dp_peer_attach(const void* blobs) {
 	if (graph) set_graph(use_graph);
 }
 
+// MEASUREMENT ONLY (debug_api.h tcnn_debug_peer_loopback): attach as rank 0 of `nranks` ranks whose
+// buffers are all this rank's own, so one process runs exactly the per-rank kernels of an N-rank peer
+// step -- Adam on a 1/N shard summing N mirrors, the gather of N - 1 shards, every poll -- without
+// peers or links (the "other" shards it gathers are its own mirror's: the parameters it trains are
+// meaningless; the time is what this rehearses).
+void TrainerHost::dp_peer_loopback(int nranks) {
+	std::vector<uint8_t> blob(sizeof(PeerBlob));
+	dp_peer_export(nranks, 0, blob.data());
+	PeerDp& pd = *peer;
+	const int N = pd.nranks;
+	std::vector<void*> host((size_t)PEER_NBUF * N);
+	for (int k = 0; k < PEER_NBUF; ++k)
+		for (int p = 0; p < N; ++p) host[(size_t)k * N + p] = pd.x[k];
+	for (int p = 0; p < N; ++p) pd.flags_arg.f[p] = (uint32_t*)pd.x[PB_FLAGS];
+	pd.ptrs.reserve(host.size() * sizeof(void*));
+	TCNN_HIP_CHECK(hipMemcpy(pd.ptrs.p, host.data(), host.size() * sizeof(void*), hipMemcpyHostToDevice));
+	pd.attached = true;
+	peer_attached = true;
+	peer_nranks = N;
+	dp_sharded = true;
+	dp_state_partial = false;
+	dp_per = pd.per;
+	grad_scale = grad_scale_user / (float)dp_nranks();
+	if (graph) set_graph(use_graph);
+}
+
 // wait for every rank's flags[slot] to reach counter c; with signal_bump >= 0 this rank signals first
 // (bumping the counter when 1) in the same one-workgroup launch
 void TrainerHost::peer_wait(hipStream_t st, int c, int slot, int signal_bump) {
@@ -360,7 +482,6 @@ void TrainerHost::training_step_peer(hipStream_t st, uint32_t B, const float* in
 		launch_sum(st, ws.loss_partial.as<float>(), ws.n_loss_partials, d_loss.as<float>());
 		mark(st, 4);
 	}
-	peer_wait(st, CTR_STEP, SLOT_GRAD, 1);  // signal "gradients ready" and wait for every rank's
 	const uint64_t lo = std::min<uint64_t>(n_params, (uint64_t)pd.rank * pd.per), hi = std::min<uint64_t>(n_params, lo + pd.per);
 	++adam_step;
 	AdamArgs a = adam_args_table(st, adam_step);
@@ -368,12 +489,21 @@ void TrainerHost::training_step_peer(hipStream_t st, uint32_t B, const float* in
 	a.n = (uint32_t)hi;
 	const AdamBuffers s{w32.as<float>(), w16.as<_Float16>(), g32.as<float>(), g16.as<_Float16>(), m1.as<float>(), m2.as<float>(),
 	                    steps.as<uint32_t>()};
-	if (hi > lo)
-		hipLaunchKernelGGL(k_peer_adam, dim3(div_round_up(hi - lo, 256)), dim3(256), 0, st, a, s, pd.table<const float>(PB_G32), pd.nranks,
-		                   (_Float16*)pd.x[PB_W16], pd.ctr.as<uint32_t>());
+	PeerStepArgs pa{};
+	pa.fl = pd.flags_arg;
+	pa.gptrs = pd.table<const float>(PB_G32);
+	pa.w16_mirror = (_Float16*)pd.x[PB_W16];
+	pa.ctr = pd.ctr.as<uint32_t>();
+	pa.my_flags = (uint32_t*)pd.x[PB_FLAGS];
+	pa.err = pd.err_dev;
+	pa.timeout_ticks = pd.timeout_ticks;
+	pa.nranks = pd.nranks;
+	// signal + wait + Adam on this rank's shard + "weights ready", one launch (a rank with an empty
+	// shard still launches one workgroup: it signals and arrives)
+	const uint32_t nwg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(div_round_up(hi > lo ? hi - lo : 0, 1024), 512));
+	hipLaunchKernelGGL(k_peer_adam, dim3(nwg), dim3(256), 0, st, a, s, pa);
 	TCNN_HIP_CHECK(hipGetLastError());
-	peer_wait(st, CTR_STEP, SLOT_WEIGHTS, 0);  // signal "weights ready" and wait
-	peer_gather(st, 1);
+	peer_gather(st, 1, true);  // waits for every rank's "weights ready" in its head
 	ws.wimage_valid = false;
 	dp_state_partial = true;
 	last_B = B;
@@ -381,10 +511,14 @@ void TrainerHost::training_step_peer(hipStream_t st, uint32_t B, const float* in
 
 // copy the other ranks' shards from their mirrors: what = 1: the fp16 parameters; 4: fp32 masters,
 // both moments, step counts (from the staging mirror)
-void TrainerHost::peer_gather(hipStream_t st, int what) {
+void TrainerHost::peer_gather(hipStream_t st, int what, bool poll) {
 	PeerDp& pd = *peer;
 	PeerGatherArgs g{};
 	g.ctr = pd.ctr.as<uint32_t>();
+	g.fl = pd.flags_arg;
+	g.err = pd.err_dev;
+	g.timeout_ticks = pd.timeout_ticks;
+	g.poll = poll ? 1 : 0;
 	g.nranks = (uint32_t)pd.nranks;
 	g.rank = (uint32_t)pd.rank;
 	g.per = pd.per;
@@ -405,7 +539,8 @@ void TrainerHost::peer_gather(hipStream_t st, int what) {
 	uint32_t maxb = 0;
 	for (int k = 0; k < what; ++k) maxb = std::max(maxb, g.elem_bytes[k]);
 	const uint64_t units = pd.per * maxb / 16 * (uint64_t)pd.nranks;
-	hipLaunchKernelGGL(k_peer_gather, dim3(div_round_up(units, 256), what), dim3(256), 0, st, g);
+	const uint32_t nwg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(div_round_up(units, 256), poll ? 256 : 4096));
+	hipLaunchKernelGGL(k_peer_gather, dim3(nwg, what), dim3(256), 0, st, g);
 	TCNN_HIP_CHECK(hipGetLastError());
 }
 
@@ -418,7 +553,7 @@ void TrainerHost::dp_peer_gather_state(hipStream_t st) {
 		                   steps.as<uint32_t>(), (uint32_t*)pd.x[PB_STATE], lo, hi - lo, pd.per * (uint64_t)pd.nranks, pd.ctr.as<uint32_t>());
 	TCNN_HIP_CHECK(hipGetLastError());
 	peer_wait(st, CTR_SYNC, SLOT_GATHER, 1);
-	peer_gather(st, 4);
+	peer_gather(st, 4, false);
 	TCNN_HIP_CHECK(hipStreamSynchronize(st));
 	pd.check();
 	dp_state_partial = false;

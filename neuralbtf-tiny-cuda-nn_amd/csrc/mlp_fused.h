@@ -853,7 +853,10 @@ __global__ __launch_bounds__(64 * FUSED_WAVES, 8 / FUSED_WAVES) void k_fused_tra
 					}
 		}
 		if (image_pending) {  // uniform: every wave passes here exactly once, on its first slice
-			__syncthreads();  // vmcnt(0): this wave's image copies landed; the barrier: everyone's did
+			// the LDS-DMA copies count in vmcnt only: wait for this wave's explicitly (a gfx950 barrier does
+			// not imply it), then the barrier makes everyone's visible
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			__syncthreads();
 			image_pending = false;
 		}
 		if constexpr (PROF) { t1 = stamp(); ph[0] += t1 - t0; t0 = t1; }
@@ -862,7 +865,10 @@ __global__ __launch_bounds__(64 * FUSED_WAVES, 8 / FUSED_WAVES) void k_fused_tra
 		fused_slice<W, IN, NH, ACT, EXT_DOUT, PROF>(a, base, c, q, xt, target, after_loss, Gext, smem + L::oW0,
 		                                            smem + L::oWh, smem + L::oWo, bufA, bufD, acc, ph, t0);
 	}
-	if (image_pending) __syncthreads();  // a wave without a slice (B % 128 != 0) still meets that barrier
+	if (image_pending) {  // a wave without a slice (B % 128 != 0) still meets that barrier, its copies landed
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		__syncthreads();
+	}
 	if constexpr (PROF) {
 		if (lane == 0) {
 			unsigned long long* o = a.prof + (size_t)(blockIdx.x * FUSED_WAVES + wave) * 16;

@@ -419,6 +419,7 @@ struct TrainerHost {
 	void dp_peer_export(int nranks, int rank, void* blob);
 	void dp_peer_attach(const void* blobs);
 	void dp_peer_detach();
+	void dp_peer_loopback(int nranks);  // measurement only: an N-rank attachment whose peers are all this rank
 	void dp_peer_abandon();  // local, no barrier: only before any exchange step (a failed attach on some rank)
 	double peer_timeout_s = peer_default_timeout_s();
 	void dp_peer_set_timeout(double seconds);
@@ -429,7 +430,7 @@ struct TrainerHost {
 	void dp_peer_gather_state(hipStream_t st);
 	void training_step_peer(hipStream_t st, uint32_t B, const float* input, const float* target);
 	void peer_wait(hipStream_t st, int c, int slot, int signal_bump = -1);
-	void peer_gather(hipStream_t st, int what);
+	void peer_gather(hipStream_t st, int what, bool poll);
 	// Adam on parameters [begin, end) only (data-parallel sharded optimizer: each rank updates its
 	// shard of the reduce-scattered gradient, then the fp16 parameters are all-gathered)
 	void optimizer_step_range(hipStream_t st, uint64_t begin, uint64_t end);

@@ -112,9 +112,14 @@ _SIGS = {
     "tcnn_trainer_serialize_json": (c_int, [c_void_p, c_int, c_void_p, c_uint64, c_void_p]),
     "tcnn_trainer_deserialize": (c_int, [c_void_p, c_void_p, c_uint64]),
     "tcnn_trainer_profile_end": (c_int, [c_void_p, c_void_p, c_uint32, c_void_p]),
+}
+
+# test-only diagnostics (neuralbtf-tiny-cuda-nn_amd/csrc/debug_api.h, not the product C-ABI header)
+_DEBUG_SIGS = {
     "tcnn_debug_probe": (c_int, [c_void_p, c_void_p, c_void_p]),
     "tcnn_debug_fused_phase_cycles": (c_int, [c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_void_p]),
     "tcnn_debug_hfma": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint32]),
+    "tcnn_debug_peer_loopback": (c_int, [c_void_p, c_int]),
 }
 
 
@@ -130,7 +135,7 @@ def lib():
                 f"tinycudann (MI355X): HIP library not built: {LIB_PATH} is missing. "
                 "Run `make -C neuralbtf-tiny-cuda-nn_amd` or __graft_entry__.build().")
         _lib = ctypes.CDLL(LIB_PATH)
-        for name, (res, args) in _SIGS.items():
+        for name, (res, args) in list(_SIGS.items()) + list(_DEBUG_SIGS.items()):
             f = getattr(_lib, name)
             f.restype = res
             f.argtypes = args
@@ -139,6 +144,10 @@ def lib():
 
 def exported_symbols():
     return list(_SIGS.keys())
+
+
+def debug_symbols():
+    return list(_DEBUG_SIGS.keys())
 
 
 def check(rc):

@@ -147,12 +147,14 @@ class PeerExchange:
     close = detach
 
     def __del__(self):
-        # last resort: a collective detach from a finaliser only works when every rank drops its
-        # exchange at the same point; call close() explicitly
-        try:
-            self.detach()
-        except Exception:
-            pass
+        # no collective from a finaliser: a rank collected on its own (or while unwinding an exception)
+        # would wait for peers that never match it. Only warn; the trainer's own destructor drops the
+        # local mappings. close() -- or `with DataParallelTrainer(...)` -- is the teardown path.
+        if getattr(self, "attached", False):
+            import warnings
+            warnings.warn("PeerExchange collected while attached: call close() on every rank (collective) "
+                          "before the trainer goes away; the sharded optimizer state was not gathered",
+                          ResourceWarning, stacklevel=2)
 
 
 class DataParallelTrainer:
@@ -271,6 +273,16 @@ class DataParallelTrainer:
         elif isinstance(self.comm, EngineComm):
             self.trainer.set_dp(None)
         self.comm = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, exc_type, exc, tb):
+        # on an exception the ranks may not all reach this point: skip the collective teardown then
+        # (PeerExchange.__del__ warns) rather than wait on peers that never arrive
+        if exc_type is None:
+            self.close()
+        return False
 
     def training_step(self, input, target):
         if self.world == 1 or self.exchange in ("engine", "peer"):

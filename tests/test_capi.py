@@ -10,11 +10,12 @@ import pytest
 from conftest import REPO
 
 HDR = os.path.join(REPO, "include", "tcnn_mi355x.h")
+DEBUG_HDR = os.path.join(REPO, "neuralbtf-tiny-cuda-nn_amd", "csrc", "debug_api.h")
 LIB = os.path.join(REPO, "neuralbtf-tiny-cuda-nn_amd", "lib", "libtcnn_mi355x.so")
 
 
-def header_functions():
-    txt = open(HDR).read()
+def header_functions(path=HDR):
+    txt = open(path).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     return sorted(set(re.findall(r"\b(tcnn_[a-z0-9_]+)\s*\(", txt)))
 
@@ -23,13 +24,16 @@ def test_header_parses():
     fns = header_functions()
     assert "tcnn_trainer_training_step" in fns and "tcnn_module_backward" in fns
     assert len(fns) > 40
+    # the test-only diagnostics live in the package's debug_api.h, not in the product C-ABI header
+    assert not [f for f in fns if f.startswith("tcnn_debug_")]
+    assert header_functions(DEBUG_HDR) == ["tcnn_debug_fused_phase_cycles", "tcnn_debug_hfma", "tcnn_debug_peer_loopback", "tcnn_debug_probe"]
 
 
 @pytest.mark.skipif(not os.path.exists(LIB), reason="library not built")
 def test_library_exports_every_declared_symbol():
     out = subprocess.check_output(["nm", "-D", "--defined-only", LIB]).decode()
     exported = set(l.split()[-1] for l in out.splitlines() if l.strip())
-    missing = [f for f in header_functions() if f not in exported]
+    missing = [f for f in header_functions() + header_functions(DEBUG_HDR) if f not in exported]
     assert not missing, missing
 
 
@@ -37,6 +41,7 @@ def test_library_exports_every_declared_symbol():
 def test_ctypes_table_covers_header_and_loads():
     from tinycudann import _lib
     assert sorted(_lib.exported_symbols()) == header_functions()
+    assert sorted(_lib.debug_symbols()) == header_functions(DEBUG_HDR)
     L = _lib.lib()
     assert L.tcnn_batch_size_granularity() == 256
     assert L.tcnn_default_loss_scale(1) == 128.0 and L.tcnn_default_loss_scale(0) == 1.0

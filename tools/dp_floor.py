@@ -93,6 +93,17 @@ def main():
         row("peer (xGMI exchange, sharded)", measure(lambda: t.training_step(pos, tgt)))
         px.detach()
         del t, px
+    # loopback rehearsal of an N-rank peer step (debug_api.h tcnn_debug_peer_loopback): rank 0 of N whose
+    # peers are all itself -- Adam on the 1/N shard over N mirrors, the gather of N - 1 shards, the polls
+    # -- i.e. the per-rank kernels of the real N-rank step minus the link transfers
+    for sch in sorted(w for w in want if w.startswith("peerloop")):
+        n = int(sch[len("peerloop"):])
+        t = Trainer(2, 3, cfg, seed=1337)
+        from tinycudann import _lib as LL
+        LL.check(LL.lib().tcnn_debug_peer_loopback(t.h, n))
+        row(f"peer loopback N={n} (per-rank kernels of the {n}-rank step, no links)", measure(lambda: t.training_step(pos, tgt)))
+        LL.check(LL.lib().tcnn_trainer_dp_peer_abandon(t.h))
+        del t
     real_ws = P.dist.get_world_size
     P.dist.get_world_size = lambda group=None: 2  # take the wrapper's all-reduce path on the one-rank group
     try:
