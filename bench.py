@@ -308,6 +308,7 @@ def main():
             dist.barrier()
 
     loss = trainer.loss()
+    dp.close()  # collective teardown on every rank (the peer exchange gathers its sharded state)
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()

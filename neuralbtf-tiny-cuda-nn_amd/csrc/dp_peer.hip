@@ -56,6 +56,7 @@ enum PeerCtr { CTR_STEP = 0, CTR_SYNC = 1, CTR_ERR = 2, CTR_ARRIVE = 3 };
 struct PeerBlob {
 	uint32_t magic, nranks, rank, device;
 	uint64_t n_params, per;
+	uint64_t pci;  // hash of the device's PCI bus id: ranks that share one GPU (the 1-GPU tests) see equal values
 	hipIpcMemHandle_t h[PEER_NBUF];
 };
 
@@ -137,89 +138,102 @@ __device__ __forceinline__ bool peer_poll(const PeerFlags& fl, int nranks, int s
 
 struct PeerStepArgs {
 	PeerFlags fl;
-	const float* const* gptrs;  // device array [nranks] of the ranks' gradient-sum mirrors
-	_Float16* w16_mirror;       // this rank's fp16 shard mirror (the peers gather from it)
-	uint32_t* ctr;              // this rank's local counters
-	uint32_t* my_flags;         // this rank's exported counter page
-	int* err;                   // host-mapped error flag
+	const float* g[PEER_MAX_RANKS];  // the ranks' gradient-sum mirrors, by value (no pointer-table load)
+	_Float16* w16_mirror;            // this rank's fp16 shard mirror (the peers gather from it)
+	uint32_t* ctr;                   // this rank's local counters
+	uint32_t* my_flags;              // this rank's exported counter page
+	int* err;                        // host-mapped error flag
 	long long timeout_ticks;
 	int nranks;
+	int signal;  // 1: signal "gradients ready" here (every workgroup; the previous launches' stores completed)
 };
 
-// One launch for "gradients ready -> wait -> sharded Adam -> weights ready" (r06; r05 ran a
-// one-workgroup wait kernel before and after Adam). Every workgroup reads the step number s + 1
-// from ctr[CTR_STEP], signals this rank's gradients (the same idempotent system-scope store from
-// every workgroup: the previous launches' writes went to uncached memory and ended with them), waits
-// for every rank's, runs Adam on its part of this rank's shard [a.begin, a.n) -- 4 parameters per
-// thread, the gradient of parameter i summed over the ranks' mirrors in rank order g_0 + g_1 + ...
-// -- writes the updated fp16 values to its mirror, and arrives on ctr[CTR_ARRIVE]. The last arrival
-// (every workgroup has read ctr[CTR_STEP] by then) resets the counter, bumps ctr[CTR_STEP] and
-// signals "weights ready" for the gather. Workgroups wait only on other ranks, never on each other,
-// so co-residency is not needed; the grid is sized to the shard (a few dozen workgroups at N = 8).
+// arrival of a workgroup whose stores the signal covers: every storing wave's vmcnt(0) wait, the
+// barrier, then one agent-scope add; returns true in the last-arriving workgroup's thread 0. What
+// the peers read is in UNCACHED memory (no L2 holds it), so completed stores are visible -- no release
+// fence (an agent- or system-scope one writes back the XCD's whole L2, ~2-7 us, for stores nobody
+// else reads)
+__device__ __forceinline__ bool peer_arrive(uint32_t* __restrict__ ctr, int slot_ctr) {
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	__syncthreads();
+	if (threadIdx.x != 0) return false;
+	const uint32_t prev = __hip_atomic_fetch_add(ctr + slot_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	if (prev != gridDim.x * gridDim.y * gridDim.z - 1u) return false;
+	__hip_atomic_store(ctr + slot_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	return true;
+}
+
+// One launch for "wait for every rank's gradients -> sharded Adam -> weights ready" (r06; r05 ran a
+// one-workgroup wait kernel before and after Adam). Every workgroup reads the step number s + 1 from
+// ctr[CTR_STEP] (signalling this rank's gradients itself when the previous launch did not: the same
+// idempotent system-scope store from every workgroup), issues the Adam-state loads of its first
+// parameter group, waits for every rank's signal, runs Adam on its part of this rank's shard
+// [a.begin, a.n) -- 4 parameters per thread, the gradient of parameter i summed over the ranks'
+// mirrors in rank order g_0 + g_1 + ... -- writes the updated fp16 values to its mirror, and arrives
+// on ctr[CTR_ARRIVE]. The last arrival (every workgroup has read ctr[CTR_STEP] by then) bumps
+// ctr[CTR_STEP] and signals "weights ready" for the gather. Workgroups wait only on other ranks,
+// never on each other, so co-residency is not needed.
 __global__ __launch_bounds__(256) void k_peer_adam(const AdamArgs a, const AdamBuffers s, const PeerStepArgs pa) {
 	__shared__ int ok_s;
 	const uint32_t step = pa.ctr[CTR_STEP] + 1u;
+	const uint32_t stride = gridDim.x * blockDim.x * 4;
+	const uint32_t i0 = a.begin + (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+	AdamState4 st0{};
+	if (i0 + 4 <= a.n) st0 = adam_load4(s, i0);  // local state: in flight across the wait
 	if (threadIdx.x < 64) {
 		bool ok = pa.ctr[CTR_ERR] == 0u;  // an earlier wait failed: no signal, no wait (the step is abandoned)
-		if (ok && threadIdx.x == 0) __hip_atomic_store(pa.my_flags + SLOT_GRAD, step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+		if (ok && pa.signal && threadIdx.x == 0) {
+			__hip_atomic_store(pa.my_flags + SLOT_GRAD, step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // landed before this wave's first poll reads it back
+		}
 		if (ok) ok = peer_poll(pa.fl, pa.nranks, SLOT_GRAD, step, pa.timeout_ticks, pa.err, pa.ctr);
 		if (threadIdx.x == 0) ok_s = ok;
 	}
 	__syncthreads();
 	if (ok_s) {
-		const uint32_t stride = gridDim.x * blockDim.x * 4;
-		for (uint32_t i = a.begin + (blockIdx.x * blockDim.x + threadIdx.x) * 4; i < a.n; i += stride) {
+		for (uint32_t i = i0; i < a.n; i += stride) {
 			if (i + 4 <= a.n) {
-				f4 g = *(const f4*)(pa.gptrs[0] + i);
+				f4 g = *(const f4*)(pa.g[0] + i);
 				for (int p0 = 1; p0 < pa.nranks; p0 += 8) {  // loads in flight together, additions in rank order
 					f4 v[8];
 #pragma unroll
 					for (int u = 0; u < 8; ++u)
-						if (p0 + u < pa.nranks) v[u] = *(const f4*)(pa.gptrs[p0 + u] + i);
+						if (p0 + u < pa.nranks) v[u] = *(const f4*)(pa.g[p0 + u] + i);
 #pragma unroll
 					for (int u = 0; u < 8; ++u)
 						if (p0 + u < pa.nranks) g += v[u];
 				}
 				*(f4*)(s.g32 + i) = g;
 				const float gs[4] = {g.x, g.y, g.z, g.w};
-				AdamState4 st = adam_load4(s, i);
+				const AdamState4 st = i == i0 ? st0 : adam_load4(s, i);
 				adam_store4(a, s, i, gs, st);
 				*(h4*)(pa.w16_mirror + i) = *(const h4*)(s.w16 + i);
 			} else {
 				for (uint32_t k = i; k < a.n; ++k) {
-					float g = pa.gptrs[0][k];
-					for (int p = 1; p < pa.nranks; ++p) g += pa.gptrs[p][k];
+					float g = pa.g[0][k];
+					for (int p = 1; p < pa.nranks; ++p) g += pa.g[p][k];
 					s.g32[k] = g;
 					pa.w16_mirror[k] = adam_update(a, s, k, g);
 				}
 			}
 		}
 	}
-	// what the peers read of this launch is the fp16 mirror, in UNCACHED memory: no L2 holds it, so
-	// every storing wave's vmcnt(0) wait (its stores complete) before the workgroup's arrival, and the
-	// arrival before the signal, order it (no release fence: an agent- or system-scope one writes back
-	// the XCD's whole L2, ~2-7 us, for the w32 / moment stores nobody else reads)
-	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-	__syncthreads();
-	if (threadIdx.x == 0) {
-		const uint32_t prev = __hip_atomic_fetch_add(pa.ctr + CTR_ARRIVE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-		if (prev == gridDim.x - 1u) {  // the last arrival: every workgroup's mirror stores have completed
-			__hip_atomic_store(pa.ctr + CTR_ARRIVE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-			__hip_atomic_store(pa.ctr + CTR_STEP, step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-			if (__hip_atomic_load(pa.ctr + CTR_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
-				__hip_atomic_store(pa.my_flags + SLOT_WEIGHTS, step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-		}
+	if (peer_arrive(pa.ctr, CTR_ARRIVE)) {  // the last arrival: every workgroup's mirror stores completed
+		__hip_atomic_store(pa.ctr + CTR_STEP, step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		if (__hip_atomic_load(pa.ctr + CTR_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+			__hip_atomic_store(pa.my_flags + SLOT_WEIGHTS, step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 	}
 }
 
-// copy every other rank's shard of up to 4 buffers (blockIdx.y) from its mirror into the local arrays,
-// 16 bytes per thread in a grid-stride loop; shard bytes are multiples of 16. With poll != 0 (the
-// training step) wave 0 of every workgroup first waits until every rank signalled "weights ready"
-// for step ctr[CTR_STEP] (r06: was a one-workgroup wait kernel of its own).
+// copy every other rank's shard of up to 4 buffers (blockIdx.z) from its mirror into the local
+// arrays; blockIdx.y = the rank copied from (its mirror pointer a kernel argument), 16 bytes per
+// thread in a grid-stride loop; shard bytes are multiples of 16. With poll != 0 (the training step)
+// wave 0 of every workgroup first waits until every rank signalled "weights ready" for step
+// ctr[CTR_STEP] (r06: was a one-workgroup wait kernel of its own).
 struct PeerGatherArgs {
 	uint8_t* local[4];
-	const uint8_t* const* peers[4];  // device arrays [nranks] of the peers' mirrors
-	uint64_t peer_offset[4];         // byte offset of this buffer inside each mirror
+	const uint8_t* peer[PEER_MAX_RANKS];  // the ranks' mirror (fp16 shard mirror or state staging) base
+	uint64_t peer_offset[4];              // byte offset of buffer z inside each mirror
 	uint32_t elem_bytes[4];
 	uint32_t nranks, rank;
 	uint64_t per;  // elements per shard
@@ -231,6 +245,8 @@ struct PeerGatherArgs {
 };
 __global__ __launch_bounds__(256) void k_peer_gather(const PeerGatherArgs g) {
 	__shared__ int ok_s;
+	const uint32_t p = blockIdx.y, b = blockIdx.z;
+	if (p == g.rank) return;
 	if (g.poll) {
 		if (threadIdx.x < 64) {
 			bool ok = g.ctr[CTR_ERR] == 0u;
@@ -242,16 +258,12 @@ __global__ __launch_bounds__(256) void k_peer_gather(const PeerGatherArgs g) {
 	} else if (g.ctr[CTR_ERR]) {
 		return;
 	}
-	const uint32_t b = blockIdx.y;
 	const uint64_t shard_bytes = g.per * g.elem_bytes[b];
 	const uint64_t units = shard_bytes / 16;
-	const uint64_t total = units * g.nranks;
-	for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (uint64_t)gridDim.x * blockDim.x) {
-		const uint64_t p = q / units;  // 16-byte unit q over all ranks' shards
-		if (p == g.rank) continue;
-		const uint64_t off = p * shard_bytes + (q % units) * 16;
-		*(uint4*)(g.local[b] + off) = *(const uint4*)(g.peers[b][p] + g.peer_offset[b] + off);
-	}
+	const uint8_t* src = g.peer[p] + g.peer_offset[b] + p * shard_bytes;
+	uint8_t* dst = g.local[b] + p * shard_bytes;
+	for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < units; q += (uint64_t)gridDim.x * blockDim.x)
+		*(uint4*)(dst + q * 16) = *(const uint4*)(src + q * 16);
 }
 
 // this rank's shard of the optimizer state into its uncached staging mirror (for the peers' gather)
@@ -280,11 +292,16 @@ struct TrainerHost::PeerDp {
 	// [4][N*per] (w32, m1, m2, steps), counters [64] uint32
 	void* x[PEER_NBUF] = {nullptr, nullptr, nullptr, nullptr};
 	std::vector<void*> opened;  // IPC mappings of the peers' buffers
+	std::vector<void*> host_ptr;  // [PEER_NBUF][nranks] the same pointers as `ptrs`, host copy (kernel arguments)
 	int* err_host = nullptr;
 	int* err_dev = nullptr;
 	long long timeout_ticks = 0;
 	int clock_khz = 1;  // wall_clock64 rate
 	PeerFlags flags_arg{};  // the ranks' counter arrays (k_peer_wait's argument)
+	// another rank runs on this rank's GPU (time-shared tests and rehearsals): the step kernels that
+	// poll other ranks then keep to a few workgroups, so their spinning waves leave the other ranks'
+	// kernels the CUs they need (a 1024-thread grid-backward workgroup needs a whole CU's registers)
+	bool shared_device = false;
 	PeerDp() = default;
 	~PeerDp() {
 		// this rank's kernels may still read the peers' mappings (an asynchronous step just issued):
@@ -384,6 +401,13 @@ void TrainerHost::dp_peer_export(int nranks, int rank, void* blob_out) {
 	b.device = (uint32_t)dev;
 	b.n_params = n_params;
 	b.per = per;
+	{
+		char bus[64] = {0};
+		TCNN_HIP_CHECK(hipDeviceGetPCIBusId(bus, (int)sizeof(bus) - 1, dev));
+		uint64_t h = 1469598103934665603ull;  // FNV-1a
+		for (const char* c = bus; *c; ++c) h = (h ^ (uint64_t)(uint8_t)*c) * 1099511628211ull;
+		b.pci = h;
+	}
 	for (int k = 0; k < PEER_NBUF; ++k) TCNN_HIP_CHECK(hipIpcGetMemHandle(&b.h[k], pd->x[k]));
 	std::memcpy(blob_out, &b, sizeof(b));
 	peer = std::move(pd);
@@ -395,9 +419,12 @@ void TrainerHost::dp_peer_attach(const void* blobs) {
 	PeerDp& pd = *peer;
 	const int N = pd.nranks;
 	std::vector<void*> host((size_t)PEER_NBUF * N);
+	PeerBlob mine;
+	std::memcpy(&mine, (const uint8_t*)blobs + (size_t)pd.rank * sizeof(PeerBlob), sizeof(mine));
 	for (int p = 0; p < N; ++p) {
 		PeerBlob b;
 		std::memcpy(&b, (const uint8_t*)blobs + (size_t)p * sizeof(PeerBlob), sizeof(b));
+		if (p != pd.rank && b.pci == mine.pci) pd.shared_device = true;
 		TCNN_CHECK(b.magic == PEER_MAGIC && (int)b.nranks == N && (int)b.rank == p && b.n_params == n_params && b.per == pd.per,
 		           "peer exchange: blob " + std::to_string(p) + " does not describe rank " + std::to_string(p) + " of the same model");
 		for (int k = 0; k < PEER_NBUF; ++k) {
@@ -414,6 +441,7 @@ void TrainerHost::dp_peer_attach(const void* blobs) {
 	for (int p = 0; p < N; ++p) pd.flags_arg.f[p] = (uint32_t*)host[(size_t)PB_FLAGS * N + p];
 	pd.ptrs.reserve(host.size() * sizeof(void*));
 	TCNN_HIP_CHECK(hipMemcpy(pd.ptrs.p, host.data(), host.size() * sizeof(void*), hipMemcpyHostToDevice));
+	pd.host_ptr = host;
 	// probe (collective): every rank's token readable through every mapping, checked once here so a
 	// broken mapping fails the attach (and the caller falls back) instead of a step
 	hipLaunchKernelGGL(k_peer_token, dim3(1), dim3(64), 0, nullptr, (uint32_t*)pd.x[PB_FLAGS], probe_token(pd.rank));
@@ -449,6 +477,7 @@ void TrainerHost::dp_peer_loopback(int nranks) {
 	for (int p = 0; p < N; ++p) pd.flags_arg.f[p] = (uint32_t*)pd.x[PB_FLAGS];
 	pd.ptrs.reserve(host.size() * sizeof(void*));
 	TCNN_HIP_CHECK(hipMemcpy(pd.ptrs.p, host.data(), host.size() * sizeof(void*), hipMemcpyHostToDevice));
+	pd.host_ptr = host;
 	pd.attached = true;
 	peer_attached = true;
 	peer_nranks = N;
@@ -475,6 +504,9 @@ void TrainerHost::training_step_peer(hipStream_t st, uint32_t B, const float* in
 	// two-launch step, or any other engine's pass (tile, layer-wise) with its reductions writing there
 	float* gx = (float*)pd.x[PB_G32];
 	if (overlapped_ok()) {
+		// (r06, tried: the slab reduction with the "gradients ready" signal from its last-arriving
+		// workgroup, to take the signal's trip off k_peer_adam's head: 2,800 workgroups adding to one
+		// counter serialise at ~88 adds / us -- 35 us)
 		training_step_overlapped(st, B, input, target, false, gx);
 	} else {
 		mark(st, 0);
@@ -491,16 +523,18 @@ void TrainerHost::training_step_peer(hipStream_t st, uint32_t B, const float* in
 	                    steps.as<uint32_t>()};
 	PeerStepArgs pa{};
 	pa.fl = pd.flags_arg;
-	pa.gptrs = pd.table<const float>(PB_G32);
+	for (int p = 0; p < pd.nranks; ++p) pa.g[p] = (const float*)pd.host_ptr[(size_t)PB_G32 * pd.nranks + p];
 	pa.w16_mirror = (_Float16*)pd.x[PB_W16];
 	pa.ctr = pd.ctr.as<uint32_t>();
 	pa.my_flags = (uint32_t*)pd.x[PB_FLAGS];
 	pa.err = pd.err_dev;
 	pa.timeout_ticks = pd.timeout_ticks;
 	pa.nranks = pd.nranks;
-	// signal + wait + Adam on this rank's shard + "weights ready", one launch (a rank with an empty
-	// shard still launches one workgroup: it signals and arrives)
-	const uint32_t nwg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(div_round_up(hi > lo ? hi - lo : 0, 1024), 512));
+	pa.signal = 1;
+	// wait + Adam on this rank's shard + "weights ready", one launch (a rank with an empty shard still
+	// launches one workgroup: it arrives and, last, signals)
+	// at most 128 workgroups: each adds once to the arrival counter, and one word takes ~88 adds per us
+	const uint32_t nwg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(div_round_up(hi > lo ? hi - lo : 0, 1024), pd.shared_device ? 8 : 128));
 	hipLaunchKernelGGL(k_peer_adam, dim3(nwg), dim3(256), 0, st, a, s, pa);
 	TCNN_HIP_CHECK(hipGetLastError());
 	peer_gather(st, 1, true);  // waits for every rank's "weights ready" in its head
@@ -523,24 +557,25 @@ void TrainerHost::peer_gather(hipStream_t st, int what, bool poll) {
 	g.rank = (uint32_t)pd.rank;
 	g.per = pd.per;
 	const uint64_t pad = pd.per * (uint64_t)pd.nranks;
+	const int kb = what == 1 ? PB_W16 : PB_STATE;
+	for (int p = 0; p < pd.nranks; ++p) g.peer[p] = (const uint8_t*)pd.host_ptr[(size_t)kb * pd.nranks + p];
 	if (what == 1) {
 		g.local[0] = (uint8_t*)w16.p;
-		g.peers[0] = pd.table<const uint8_t>(PB_W16);
 		g.elem_bytes[0] = 2;
 	} else {
 		void* loc[4] = {w32.p, m1.p, m2.p, steps.p};
 		for (int k = 0; k < 4; ++k) {
 			g.local[k] = (uint8_t*)loc[k];
-			g.peers[k] = pd.table<const uint8_t>(PB_STATE);
 			g.peer_offset[k] = (uint64_t)k * pad * 4;
 			g.elem_bytes[k] = 4;
 		}
 	}
 	uint32_t maxb = 0;
 	for (int k = 0; k < what; ++k) maxb = std::max(maxb, g.elem_bytes[k]);
-	const uint64_t units = pd.per * maxb / 16 * (uint64_t)pd.nranks;
-	const uint32_t nwg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(div_round_up(units, 256), poll ? 256 : 4096));
-	hipLaunchKernelGGL(k_peer_gather, dim3(nwg, what), dim3(256), 0, st, g);
+	const uint64_t units = pd.per * maxb / 16;  // 16-byte units of one rank's shard
+	const uint32_t cap = poll ? (pd.shared_device ? 1u : 64u) : 1024u;
+	const uint32_t nx = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(div_round_up(units, 256), cap));
+	hipLaunchKernelGGL(k_peer_gather, dim3(nx, pd.nranks, what), dim3(256), 0, st, g);
 	TCNN_HIP_CHECK(hipGetLastError());
 }
 

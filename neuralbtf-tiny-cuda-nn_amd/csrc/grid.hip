@@ -608,7 +608,8 @@ extern template void grid_bwd_f<4>(hipStream_t, uint32_t, HashType, int, uint32_
 void launch_grid_bwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_t B, const float* pos,
                      uint32_t pos_stride, const void* dLdy16, int dy_layout, uint32_t dy_stride, const GridSlice* slices,
                      uint32_t n_slices, uint32_t n_chunks, float* partial, uint32_t partial_stride,
-                     const LevelInfo* levels, bool hash_grid, Interp interp, const GridBwdEpilogue* ep, const GridOpts& go) {
+                     const LevelInfo* levels, bool hash_grid, Interp interp, const GridBwdEpilogue* ep, const GridOpts& go,
+                     const GridSlice* host_slices, const LevelInfo* host_levels, uint32_t n_levels) {
 	const uint32_t n_tail = (ep && ep->enabled) ? ep->n_mlp_groups : 0u;
 	if (n_tail == 0 && (n_slices == 0 || B == 0)) return;  // callers zero the gradient of empty batches
 	if (B == 0) n_slices = 0;
@@ -620,6 +621,13 @@ void launch_grid_bwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_
 	else gl.ep.enabled = 0;
 	gl.dbg_times = nullptr;
 	gl.opts = go;
+	gl.tb.n_items = gl.tb.n_levels = 0;
+	if (host_slices && host_levels && n_slices <= GRID_BWD_ARG_ITEMS && n_levels <= GRID_BWD_ARG_LEVELS) {
+		gl.tb.n_items = n_slices;
+		gl.tb.n_levels = n_levels;
+		std::copy(host_slices, host_slices + n_slices, gl.tb.items);
+		std::copy(host_levels, host_levels + n_levels, gl.tb.levels);
+	}
 	dim3 g(n_slices * n_chunks + n_tail);
 	if (dbg_grid_times()) gl.dbg_times = (unsigned long long*)g_dbg_times.get((size_t)g.x * 64);
 	const size_t lds = GRID_BWD_LDS_BYTES;

@@ -393,12 +393,22 @@ __device__ __forceinline__ void grid_bwd_mlp_tail(const GridBwdEpilogue& ep, uin
 	}
 }
 
+// The work plan by value (kernel arguments, read with scalar loads): the first thing every workgroup
+// needs, so it must not cost a dependent global load at the head of the launch (r06). Plans larger
+// than the tables keep reading the device copies.
+constexpr uint32_t GRID_BWD_ARG_ITEMS = 32, GRID_BWD_ARG_LEVELS = 24;
+struct GridBwdTables {
+	uint32_t n_items, n_levels;  // entries valid below (0: read the device arrays)
+	GridSlice items[GRID_BWD_ARG_ITEMS];
+	LevelInfo levels[GRID_BWD_ARG_LEVELS];
+};
+
 template <uint32_t D, uint32_t F, HashType H, bool OPTS>
 __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 	int layout, uint32_t B, const float* __restrict__ pos, uint32_t pstride, const _Float16* __restrict__ dLdy, uint32_t dy_stride,
 	const GridSlice* __restrict__ items, float* __restrict__ partial, uint32_t partial_stride,
 	const LevelInfo* __restrict__ levels, uint32_t hash_grid, uint32_t interp_u, uint32_t pts_per_chunk, uint32_t n_items,
-	uint32_t n_chunks, const GridBwdEpilogue ep, unsigned long long* dbg_times, const GridOpts o) {
+	uint32_t n_chunks, const GridBwdEpilogue ep, unsigned long long* dbg_times, const GridOpts o, const GridBwdTables tb) {
 	extern __shared__ __attribute__((aligned(16))) int acc[];
 	const unsigned long long t_start = dbg_times ? wall_clock64() : 0ull;
 	__shared__ float red[GRID_BWD_THREADS / 64];
@@ -414,7 +424,16 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 	// item of chunk c lands on one XCD and the chunk's positions (re-read by all 26 items of
 	// config_hash) stay in that XCD's L2
 	const uint32_t item = blockIdx.x / n_chunks, chunk = blockIdx.x % n_chunks;
-	const GridSlice it = items[item];
+	GridSlice it;
+	if (item < tb.n_items) {  // wave-uniform: scalar loads from the kernel arguments
+		it.level = tb.items[item].level;
+		it.begin = tb.items[item].begin;
+		it.end = tb.items[item].end;
+		it.f0 = tb.items[item].f0;
+		it.nf = tb.items[item].nf;
+	} else {
+		it = items[item];
+	}
 	const uint32_t len = it.end - it.begin;
 	const uint32_t nf = it.nf, f0 = it.f0;
 	const Interp interp = (Interp)interp_u;
@@ -448,7 +467,15 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 			load_pos_batch<D>(pos, pstride, i0, i1, 0, xs0);
 		}
 	}
-	const LevelInfo li = levels[it.level];
+	LevelInfo li;
+	if (it.level < tb.n_levels) {
+		li.scale = tb.levels[it.level].scale;
+		li.res = tb.levels[it.level].res;
+		li.offset = tb.levels[it.level].offset;
+		li.size = tb.levels[it.level].size;
+	} else {
+		li = levels[it.level];
+	}
 	// Replicas: a small level's accumulators fit the LDS several times; wave w adds into replica
 	// w % R, which divides the same-address atomic serialisation on the coarse dense levels
 	// (level 0: 256 entries hit by every point) by up to R. Integer sums: the replica merge below is
@@ -605,6 +632,7 @@ struct GridBwdLaunch {
 	GridBwdEpilogue ep;
 	unsigned long long* dbg_times;
 	GridOpts opts;
+	GridBwdTables tb;
 };
 
 template <uint32_t D, uint32_t F, HashType H>
@@ -617,10 +645,10 @@ static void grid_bwd_t(hipStream_t st, int layout, uint32_t dys, dim3 g, size_t 
 	set_dyn_lds((const void*)k_grid_bwd_lds<D, F, H, true>, (int)GRID_BWD_LDS_BYTES, done1);
 	if (gl.opts.active)
 		hipLaunchKernelGGL((k_grid_bwd_lds<D, F, H, true>), g, dim3(GRID_BWD_THREADS), lds, st, layout, B, pos, ps, dy, dys, sl, part, pstr, lv, hg, in,
-		                   ppc, gl.n_items, gl.n_chunks, gl.ep, gl.dbg_times, gl.opts);
+		                   ppc, gl.n_items, gl.n_chunks, gl.ep, gl.dbg_times, gl.opts, gl.tb);
 	else
 		hipLaunchKernelGGL((k_grid_bwd_lds<D, F, H, false>), g, dim3(GRID_BWD_THREADS), lds, st, layout, B, pos, ps, dy, dys, sl, part, pstr, lv, hg, in,
-		                   ppc, gl.n_items, gl.n_chunks, gl.ep, gl.dbg_times, gl.opts);
+		                   ppc, gl.n_items, gl.n_chunks, gl.ep, gl.dbg_times, gl.opts, gl.tb);
 }
 
 template <uint32_t D, uint32_t F>

@@ -176,11 +176,14 @@ void launch_grid_fwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_
 // Grid backward: dLdy layout 0 = level-major pairs ([l][i][F] halves), 1 = SoA ([(l*F+f)*B + i]),
 // 2 = AoS ([i*dy_stride + l*F + f]).
 uint32_t grid_bwd_slot_budget();
+// host_slices / host_levels: the work plan's host copies, passed by value as kernel arguments when
+// they fit (grid_bwd_lds.h GridBwdTables)
 void launch_grid_bwd(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_t B, const float* pos,
                      uint32_t pos_stride, const void* dLdy16, int dy_layout, uint32_t dy_stride, const GridSlice* slices,
                      uint32_t n_slices, uint32_t n_chunks, float* partial, uint32_t partial_stride,
                      const LevelInfo* levels, bool hash_grid, Interp interp, const GridBwdEpilogue* ep = nullptr,
-                     const GridOpts& opts = GridOpts{});
+                     const GridOpts& opts = GridOpts{}, const GridSlice* host_slices = nullptr, const LevelInfo* host_levels = nullptr,
+                     uint32_t n_levels = 0);
 // Binned backward, pass 1: counting-sort the updates of the binned levels by slice (GridBinArgs).
 void launch_grid_bin(hipStream_t st, uint32_t D, uint32_t F, HashType h, uint32_t B, const float* pos, uint32_t pos_stride,
                      const void* dLdy16, int dy_layout, uint32_t dy_stride, const LevelInfo* levels, bool hash_grid, Interp interp,

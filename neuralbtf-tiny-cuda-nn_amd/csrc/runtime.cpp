@@ -305,7 +305,7 @@ void GridEncodingHost::backward_items(hipStream_t st, GridBwdBufs& w, uint32_t B
 	if (!slices.empty()) w.partial.reserve((size_t)n_chunks * n_lds_params * 4);
 	launch_grid_bwd(st, desc.n_pos_dims, desc.n_features_per_level, desc.hash_type, B, pos, pstride, dy, layout, dy_stride,
 	                d_slices.as<GridSlice>(), (uint32_t)slices.size(), n_chunks, w.partial.as<float>(), n_lds_params, dev_levels(),
-	                hash_grid(), desc.interp, ep, opts());
+	                hash_grid(), desc.interp, ep, opts(), slices.data(), levels.data(), (uint32_t)levels.size());
 }
 
 void GridEncodingHost::backward_bin(hipStream_t st, GridBwdBufs& w, uint32_t B, const float* pos, uint32_t pstride, const void* dy,
@@ -1015,7 +1015,7 @@ void TrainerHost::training_step_sequential(hipStream_t st, uint32_t B, const flo
 // all-reduce sits between the gradients and Adam) the slab reduction into the fp32 gradient.
 // Summation orders are the same either way (bit-identical parameters).
 void TrainerHost::training_step_overlapped(hipStream_t st, uint32_t B, const float* input, const float* target, bool run_optimizer,
-                                           float* grad_out) {
+                                           float* grad_out, bool skip_reduce) {
 	NetworkHost& m = *model;
 	float* const gsum = (grad_out && !run_optimizer) ? grad_out : g32.as<float>();
 	mark(st, 0);
@@ -1064,7 +1064,7 @@ void TrainerHost::training_step_overlapped(hipStream_t st, uint32_t B, const flo
 	} else {
 		g.backward_acc(st, ws.gbw, B, ws.dLdenc.p, 0, 0, gsum + n_mlp);
 		mark(st, 2);
-		g.reduce_items(st, ws.gbw, gsum + n_mlp);
+		if (!skip_reduce) g.reduce_items(st, ws.gbw, gsum + n_mlp);
 	}
 	mark(st, 3);
 	last_B = B;

@@ -378,7 +378,7 @@ struct TrainerHost {
 	bool overlapped_ok() const { return model->fused_ok(); }
 	// grad_out (run_optimizer = false only): where the fp32 gradient sums go (default g32)
 	void training_step_overlapped(hipStream_t st, uint32_t B, const float* input, const float* target, bool run_optimizer,
-	                              float* grad_out = nullptr);
+	                              float* grad_out = nullptr, bool skip_reduce = false);
 	AdamArgs adam_args() const;
 
 	TrainerHost(uint32_t n_in, uint32_t n_out, const json& cfg, uint32_t seed);

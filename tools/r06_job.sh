@@ -3,7 +3,7 @@
 # default bench
 cd "${GRAFT_REPO_ROOT:-.}"; export TMPDIR=/tmp; D=gpurun_out/${OUT:-r06_job}; mkdir -p $D
 if [ "$1" != "-" ]; then
-  timeout -k 10 900 python -u -m pytest $1 -m gpu -x -q --timeout 300 --timeout-method thread > $D/tests.log 2>&1; rc=$?
+  timeout -k 10 900 python -u -m pytest $1 -m gpu -x -v --timeout 240 --timeout-method thread > $D/tests.log 2>&1; rc=$?
   tail -4 $D/tests.log
   [ $rc -eq 0 ] || { grep -E "Error|error|assert" $D/tests.log | head -20; exit $rc; }
 fi
