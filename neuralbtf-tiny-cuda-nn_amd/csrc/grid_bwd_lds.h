@@ -41,11 +41,14 @@ __device__ __forceinline__ void lds_add_i32(int* acc, float v) {
 //   HASH_POW2  hashed level of power-of-two size: index = hash & (size - 1)
 //   DENSE      res^D <= size: index = sum g_d res^d, < 2 size, so `% size` is one conditional subtract
 //   GENERIC    anything else (tiled grids, non-power-of-two hashed sizes): grid_index()
-enum : int { IDX_HASH_POW2 = 0, IDX_DENSE = 1, IDX_GENERIC = 2 };
+//   HASH_RANGE a contiguous entry range [begin, begin + len) of such a hashed level (r06: a hashed
+//              level too large for the LDS is split into entry ranges holding all F features, so its
+//              slab is in parameter order; corners outside the range are skipped)
+enum : int { IDX_HASH_POW2 = 0, IDX_DENSE = 1, IDX_GENERIC = 2, IDX_HASH_RANGE = 3 };
 
 template <uint32_t D, HashType H, int KIND>
 __device__ __forceinline__ uint32_t level_index(bool hash_grid, uint32_t size, uint32_t res, const uint32_t* g) {
-	if constexpr (KIND == IDX_HASH_POW2) {
+	if constexpr (KIND == IDX_HASH_POW2 || KIND == IDX_HASH_RANGE) {
 		uint32_t h = 0;
 #pragma unroll
 		for (uint32_t d = 0; d < D; ++d) h ^= g[d] * hash_prime<H>(d);
@@ -102,7 +105,7 @@ __device__ __forceinline__ void accum_point(const float (&x)[D], const float (&d
 		}
 		const float wh = single ? 1.0f : (float)f16_rn(w);
 		const uint32_t rel = level_index<D, H, KIND>(hash_grid, li.size, li.res, local) - begin;
-		if constexpr (KIND == IDX_GENERIC) {  // entry slices may not cover the level
+		if constexpr (KIND == IDX_GENERIC || KIND == IDX_HASH_RANGE) {  // entry slices may not cover the level
 			if (rel >= len) continue;
 		}
 		if constexpr (MODE == 0) {
@@ -130,13 +133,13 @@ __device__ __forceinline__ void accum_point(const float (&x)[D], const float (&d
 // around every corner, as in the fused kernel's encode, r03.)
 template <uint32_t F, HashType H, int KIND, int MODE>
 __device__ __forceinline__ void accum_point_2d_fast(const float (&x)[2], const float (&dy)[F], const LevelInfo& li, uint32_t f0,
-                                                    uint32_t nf, int* acc) {
+                                                    uint32_t nf, int* acc, uint32_t begin = 0, uint32_t len = 0) {
 	float p[2];
 	uint32_t g[2];
 	pos_fract(x[0], li.scale, Interp::Linear, p[0], g[0]);
 	pos_fract(x[1], li.scale, Interp::Linear, p[1], g[1]);
 	uint32_t t[2][2];
-	if constexpr (KIND == IDX_HASH_POW2) {
+	if constexpr (KIND == IDX_HASH_POW2 || KIND == IDX_HASH_RANGE) {
 		t[0][0] = g[0] * hash_prime<H>(0);
 		t[0][1] = t[0][0] + hash_prime<H>(0);
 		t[1][0] = g[1] * hash_prime<H>(1);
@@ -155,6 +158,9 @@ __device__ __forceinline__ void accum_point_2d_fast(const float (&x)[2], const f
 		uint32_t rel;
 		if constexpr (KIND == IDX_HASH_POW2) {
 			rel = (t[0][bx] ^ t[1][by]) & (li.size - 1u);
+		} else if constexpr (KIND == IDX_HASH_RANGE) {
+			rel = ((t[0][bx] ^ t[1][by]) & (li.size - 1u)) - begin;
+			if (rel >= len) continue;  // another range's corner (exec-masked, no branch around the point)
 		} else {
 			const uint32_t d = t[0][bx] + t[1][by];
 			rel = __builtin_elementwise_min(d, d - li.size);  // d % size for d < 2 size
@@ -200,8 +206,8 @@ __device__ __forceinline__ void grid_bwd_points_regs(const uint32_t (&dyb)[GRID_
                                                      Interp interp, uint32_t begin, uint32_t len, uint32_t f0, uint32_t nf,
                                                      uint32_t i0, uint32_t i1, float scale, int* acc, const GridOpts& o) {
 	constexpr uint32_t U = GRID_BWD_PU, NB = GRID_BWD_PR / U;
-	constexpr bool FAST_KIND = D == 2 && (KIND == IDX_HASH_POW2 || KIND == IDX_DENSE);
-	const bool fast = FAST_KIND && interp == Interp::Linear && begin == 0;  // whole levels (kind HASH_POW2 / DENSE)
+	constexpr bool FAST_KIND = D == 2 && (KIND == IDX_HASH_POW2 || KIND == IDX_DENSE || KIND == IDX_HASH_RANGE);
+	const bool fast = FAST_KIND && interp == Interp::Linear && (begin == 0 || KIND == IDX_HASH_RANGE);  // whole levels or hash ranges
 	float xs[2][U][D];
 #pragma unroll
 	for (uint32_t u = 0; u < U; ++u)
@@ -229,7 +235,7 @@ __device__ __forceinline__ void grid_bwd_points_regs(const uint32_t (&dyb)[GRID_
 						float dy[F];
 #pragma unroll
 						for (uint32_t f = 0; f < F; ++f) dy[f] = dy_bits_feature(dyb[p], f) * scale;
-						accum_point_2d_fast<F, H, KIND, MODE>(*(const float(*)[2]) & xs[k & 1][u][0], dy, li, f0, nf, acc);
+						accum_point_2d_fast<F, H, KIND, MODE>(*(const float(*)[2]) & xs[k & 1][u][0], dy, li, f0, nf, acc, begin, len);
 					}
 				} else {
 					// the chunk's last, partial batch (e.g. 4 points per thread at 4096-point chunks: the
@@ -242,7 +248,7 @@ __device__ __forceinline__ void grid_bwd_points_regs(const uint32_t (&dyb)[GRID_
 						float dy[F];
 #pragma unroll
 						for (uint32_t f = 0; f < F; ++f) dy[f] = dy_bits_feature(dyb[p], f) * scale;
-						accum_point_2d_fast<F, H, KIND, MODE>(*(const float(*)[2]) & xs[k & 1][u][0], dy, li, f0, nf, acc);
+						accum_point_2d_fast<F, H, KIND, MODE>(*(const float(*)[2]) & xs[k & 1][u][0], dy, li, f0, nf, acc, begin, len);
 					}
 				}
 			}
@@ -272,8 +278,8 @@ __device__ __forceinline__ void grid_bwd_points(int layout, uint32_t B, const fl
                                                 int* acc, const GridOpts& o) {
 	constexpr uint32_t NF = F;
 	constexpr uint32_t U = 8;  // points in flight per thread
-	constexpr bool FAST_KIND = D == 2 && !OPTS && (KIND == IDX_HASH_POW2 || KIND == IDX_DENSE);
-	const bool fast = FAST_KIND && interp == Interp::Linear && begin == 0;  // accum_point_2d_fast
+	constexpr bool FAST_KIND = D == 2 && !OPTS && (KIND == IDX_HASH_POW2 || KIND == IDX_DENSE || KIND == IDX_HASH_RANGE);
+	const bool fast = FAST_KIND && interp == Interp::Linear && (begin == 0 || KIND == IDX_HASH_RANGE);  // accum_point_2d_fast
 	for (uint32_t base = i0 + threadIdx.x; base < i1; base += U * blockDim.x) {
 		float xs[U][D], dy[U][NF];
 #pragma unroll
@@ -310,7 +316,7 @@ __device__ __forceinline__ void grid_bwd_points(int layout, uint32_t B, const fl
 			if (fast_b && base + (U - 1) * blockDim.x < i1) {
 #pragma unroll
 				for (uint32_t u = 0; u < U; ++u)
-					accum_point_2d_fast<F, H, KIND, MODE>(*(const float(*)[2]) & xs[u][0], dy[u], li, f0, nf, acc);
+					accum_point_2d_fast<F, H, KIND, MODE>(*(const float(*)[2]) & xs[u][0], dy[u], li, f0, nf, acc, begin, len);
 				continue;
 			}
 		}
@@ -549,11 +555,14 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 	int kind = IDX_GENERIC;
 	if (whole && full <= li.size) kind = IDX_DENSE;
 	else if (whole && hash_grid && (li.size & (li.size - 1)) == 0) kind = IDX_HASH_POW2;
+	else if (!whole && hash_grid && (li.size & (li.size - 1)) == 0 && full > li.size) kind = IDX_HASH_RANGE;
 	const int mode = nf < F ? 1 : (F == 2 ? 0 : 2);
 	if constexpr (REGS_OK) {
 		if (use_regs) {
 			if (kind == IDX_HASH_POW2)
 				grid_bwd_mode_regs<D, F, H, IDX_HASH_POW2>(mode, dyb, xs0, B, pos, pstride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, nf, i0, i1, scale, acc_w, o);
+			else if (kind == IDX_HASH_RANGE)
+				grid_bwd_mode_regs<D, F, H, IDX_HASH_RANGE>(mode, dyb, xs0, B, pos, pstride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, nf, i0, i1, scale, acc_w, o);
 			else if (kind == IDX_DENSE)
 				grid_bwd_mode_regs<D, F, H, IDX_DENSE>(mode, dyb, xs0, B, pos, pstride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, nf, i0, i1, scale, acc_w, o);
 			else
@@ -563,6 +572,8 @@ __global__ __launch_bounds__(GRID_BWD_THREADS) void k_grid_bwd_lds(
 	if (!use_regs) {
 	if (kind == IDX_HASH_POW2)
 		grid_bwd_mode<D, F, H, IDX_HASH_POW2, OPTS>(mode, layout, B, pos, pstride, dLdy, dy_stride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, nf, i0, i1, scale, acc_w, o);
+	else if (kind == IDX_HASH_RANGE)
+		grid_bwd_mode<D, F, H, IDX_HASH_RANGE, OPTS>(mode, layout, B, pos, pstride, dLdy, dy_stride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, nf, i0, i1, scale, acc_w, o);
 	else if (kind == IDX_DENSE)
 		grid_bwd_mode<D, F, H, IDX_DENSE, OPTS>(mode, layout, B, pos, pstride, dLdy, dy_stride, it.level, li, hash_grid != 0, interp, it.begin, len, f0, nf, i0, i1, scale, acc_w, o);
 	else

@@ -243,10 +243,22 @@ uint32_t tile_train_wT_bytes(uint32_t W, uint32_t IN, uint32_t NH);
 // dldenc (optional): dL/d(encoding) as level-major pairs [IN/2][B] (dldenc_pairs) or AoS fp16 [B][IN]
 // wT: tile_train_wT_bytes of scratch (nullptr when 0), rewritten from params16 by this launch
 // out_act: output activation (ACT_*) applied to the output, its transfer applied to dL/d(output)
+// The grid encoding gathered inside the tile kernel (enc16 == nullptr; r06): 2-D positions, the fp16
+// table, the level table, hash type / flag and the in-range-index flag of a 2-feature grid
+struct TileGridEnc {
+	const float* pos;
+	const void* table16;
+	const LevelInfo* levels;
+	HashType hash;
+	uint32_t hash_grid, inrange;
+};
+// whether the tile kernel gathers the grid encoding itself for this shape / batch (8-wave W128 kernel,
+// IN 32 = 16 levels x 2 features, 64-sample tiles; TCNN_TILE_GENC=0 turns it off: A/B switch)
+bool tile_train_genc_ok(uint32_t W, uint32_t IN, uint32_t NH, int act, uint32_t B, HashType h);
 void launch_mlp_tile_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, int act, int out_act, uint32_t B, uint32_t dims,
                            float loss_scale, uint32_t loss_l2, const void* params16, const void* enc16, const float* target,
                            const void* dout16, void* out16, void* dldenc, int dldenc_pairs, float* wgrad_partial, float* loss_partial,
-                           void* wT);
+                           void* wT, const TileGridEnc* genc = nullptr);
 // forward only (the reference's INFERENCE instantiation): enc16 fp16 [B][IN] -> out16 fp16 [B][16]
 bool tile_infer_supported(uint32_t W, uint32_t IN, uint32_t NH, uint32_t outp, int act);
 uint32_t tile_infer_blocks(uint32_t B, uint32_t W, uint32_t IN, uint32_t NH);

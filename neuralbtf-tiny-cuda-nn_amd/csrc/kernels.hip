@@ -44,7 +44,7 @@ __global__ __launch_bounds__(256) void k_grid_slab_reduce(const float* __restric
                                                            float* __restrict__ out, const GridSlabMap* __restrict__ map, GradFinalize fin) {
 	const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
 	if (p >= n) return;
-	const float s = slab_sum(in + grid_slab_index(map, p), stride, n_parts);
+	const float s = slab_sum(in + (map ? grid_slab_index(map, p) : p), stride, n_parts);
 	if (fin.out) grad_finalize_store(s, fin.s, fin.out, p, fin.out_f32);
 	else out[p] = s;
 }

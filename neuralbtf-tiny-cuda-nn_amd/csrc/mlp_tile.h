@@ -188,7 +188,19 @@ struct TileTrainArgs {
 	int dldenc_pairs;
 	float* wgrad_partial;    // [gridDim.x][N_MLP]
 	float* loss_partial;     // [gridDim.x]
+	// GENC kernels (the grid encoding gathered in-kernel instead of read from `enc`, r06): positions
+	// fp32 [B][2], the fp16 grid table as half2 entries, the level table, the hash-grid flag, and whether
+	// the branch-free in-range index applies (GridEncodingHost::inrange_index_ok)
+	const float* gpos;
+	const uint32_t* gtable;
+	const LevelInfo* glevels;
+	uint32_t ghash, ginrange;
 };
+
+// LDS beyond the layout that the in-kernel grid encode (GENC) uses: the level table (16 B per level)
+// and one 64-byte position buffer per wave (8 samples x 2 dimensions)
+constexpr int tile_genc_extra_bytes(int IN, int WAVES) { return (IN / 2) * 16 + WAVES * 64; }
+constexpr int tile_genc_base_bytes(int bytes) { return (bytes + 15) / 16 * 16; }
 
 __device__ __forceinline__ h8 zero8() { return h8{0, 0, 0, 0, 0, 0, 0, 0}; }
 
@@ -213,7 +225,16 @@ constexpr int tile_train_weu(int WR, int IN, int NH, bool RA, int TS) {
 	                        tile_waves(tile_kw(WR), NH, RA) / 4);
 }
 
-template <int WR, int IN, int NH, Act ACT, bool RA, int TS>
+// GENC = 0: the tile's input rows come from a.enc (AoS fp16 [B][IN]). GENC = 1 + (int)HashType: the
+// 2-D, 2-feature grid encoding is gathered in the kernel (r06, VERDICT r05 item 3: configs[3]'s separate
+// 122 us AoS encode pass and its 64 MB write + re-read go away). The gathers of tile t+1 are issued as
+// LDS-DMA (global_load_lds_dword: no registers held) into a slot the backward of tile t no longer needs,
+// two backward layers before the tile ends, so their latency runs under those layers' MFMAs; at the
+// start of tile t+1 each lane combines its 2 levels x 4 corners with the weights (the fp16 FMA chain of
+// encode_level_f2 / _inrange, bit-identical) into slot 0. Every staging buffer is wave-local: a wave
+// waits only on its own DMA (vmcnt) before reading it back. The tile's positions arrive the same way
+// one tile ahead. Shape: 8 waves, 64-sample tiles, IN = 32 (16 levels: lane = 8 samples x 8 level pairs).
+template <int WR, int IN, int NH, Act ACT, bool RA, int TS, int GENC = 0>
 __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN, NH, RA, TS)) void k_mlp_tile_train(const TileTrainArgs a) {
 	using L = TileLayout<WR, IN, NH, RA, TS>;
 	constexpr int W = L::W, NTAU = L::NTAU, KH = L::KH;
@@ -339,7 +360,7 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 	float loss = 0.0f;
 
 	// input rows of a tile: IN/8 16-byte vectors per sample
-	constexpr int XV = TS * IN / 8, XPT = (XV + NTHR - 1) / NTHR;
+	constexpr int XV = TS * IN / 8, XPT = GENC ? 1 : (XV + NTHR - 1) / NTHR;
 	const uint32_t n_tiles = a.B / TS;
 	uint32_t tile = blockIdx.x;
 	h8 xr[XPT];
@@ -350,18 +371,135 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 			if (idx < XV) xr[j] = *(const h8*)(a.enc + ((size_t)t * TS + idx / (IN / 8)) * IN + 8 * (idx % (IN / 8)));
 		}
 	};
-	if (tile < n_tiles) load_x(tile);
+
+	// ---- in-kernel grid encode (GENC) ----
+	static_assert(!GENC || (TS == 64 && WAVES == 8 && IN == 32 && !L::PP && NH >= 2), "GENC: the 8-wave W128 kernel, IN 32, no ping-pong slot");
+	constexpr HashType GH = (HashType)(GENC > 0 ? GENC - 1 : 0);
+	const int wave_s = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform offsets stay in SGPRs
+	LevelInfo* gLvl = (LevelInfo*)((char*)smem + tile_genc_base_bytes(L::BYTES));
+	float* gPos = (float*)((char*)gLvl + (IN / 2) * 16) + wave_s * 16;  // this wave's 8 samples x 2 dims
+	// staging of the wave's 8 gathers per lane ([k][corner][lane] dwords): slot NH, dead from the start of
+	// the backward's layer NH - 2 to the end of the tile (its delta_NH was last read by layer NH - 1)
+	uint32_t* gStage = (uint32_t*)(smem + L::oA + (NH - 1) * TS * RSW) + wave_s * 8 * 64;
+	// The LDS-DMA loads are inline asm, not __builtin_amdgcn_global_load_lds: the compiler cannot tell the
+	// staging buffers from the rest of the one dynamic LDS array, so with the builtin it put a vmcnt(0)
+	// wait in front of every later LDS read and barrier -- each gather's latency exposed at once, +30 %
+	// kernel time (r06, measured). Opaque to the compiler, the waits are ours: each reader of a buffer
+	// waits for its own wave's DMA (vmcnt) first. (The compiler then counts fewer outstanding vector-memory
+	// operations than there are, which only makes its own vmcnt waits stricter.)
+	auto lds_dma = [](const void* g, const void* l) {
+		const uint32_t la = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)l;
+		asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(g), "s"(la) : "memory", "m0");
+	};
+	auto genc_pos_dma = [&](uint32_t t) {  // positions of tile t's samples 8 wave .. +7 -> gPos (lanes 0..15)
+		if (lane < 16) lds_dma(a.gpos + ((size_t)t * TS + 8 * wave_s) * 2 + lane, gPos);
+	};
+	auto genc_issue = [&]() {  // corner gathers of the tile whose positions are in gPos -> gStage
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's position DMA landed
+		const int sl = lane >> 3, j = lane & 7;
+		const float x0 = gPos[2 * sl], x1 = gPos[2 * sl + 1];
+		const bool inr = x0 >= 0.0f && x0 <= 1.0f && x1 >= 0.0f && x1 <= 1.0f;
+		const bool fast = a.ginrange && __builtin_amdgcn_ballot_w64(!inr) == 0;
+#pragma unroll
+		for (int k = 0; k < 2; ++k) {
+			const LevelInfo li = gLvl[2 * j + k];
+			float pos[2];
+			uint32_t pg[2];
+			pos_fract(x0, li.scale, Interp::Linear, pos[0], pg[0]);
+			pos_fract(x1, li.scale, Interp::Linear, pos[1], pg[1]);
+			uint32_t idx[4];
+			if (fast) {  // grid_index_inrange's arithmetic (encode_level_f2_inrange)
+				const LevelConsts<2> lc = level_consts<2>(li, a.ghash != 0);
+#pragma unroll
+				for (int cc = 0; cc < 4; ++cc) {
+					uint32_t h = 0, dn = 0;
+#pragma unroll
+					for (int d = 0; d < 2; ++d) {
+						const uint32_t bb = (cc >> d) & 1u;
+						h ^= (pg[d] + bb) * hash_prime<GH>(d);
+						dn += (pg[d] + bb) * lc.sd[d];
+					}
+					const uint32_t dm = __builtin_elementwise_min(dn, dn - lc.size);
+					idx[cc] = li.offset + (((h & lc.hmask) & lc.m) | (dm & ~lc.m));
+				}
+			} else {
+#pragma unroll
+				for (int cc = 0; cc < 4; ++cc) {
+					uint32_t local[2] = {pg[0] + (cc & 1u), pg[1] + ((cc >> 1) & 1u)};
+					idx[cc] = li.offset + grid_index<2, GH>(a.ghash != 0, li.size, li.res, local);
+				}
+			}
+#pragma unroll
+			for (int cc = 0; cc < 4; ++cc)
+				lds_dma(a.gtable + idx[cc], gStage + (4 * k + cc) * 64);
+		}
+	};
+	auto genc_finish = [&](bool first) {  // gStage + gPos -> this wave's 8 samples x 16 levels of slot 0
+		// this wave's gathers landed: vector-memory operations complete in issue order (gfx9 vmcnt), and
+		// the only ones issued after them are the previous tile's dL/d(encoding) stores (waves < KT0: 2
+		// per 16-sample column as level pairs, 1 as AoS), whose write acknowledgements need not be awaited
+		if (!first && a.dldenc && wave < KT0) {
+			if (a.dldenc_pairs) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NTAU) : "memory");
+			else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NTAU) : "memory");
+		} else {
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		}
+		const int sl = lane >> 3, j = lane & 7;
+		const float x0 = gPos[2 * sl], x1 = gPos[2 * sl + 1];
+#pragma unroll
+		for (int k = 0; k < 2; ++k) {
+			const int level = 2 * j + k;
+			const float sc = gLvl[level].scale;
+			float pos[2];
+			uint32_t pg[2];
+			pos_fract(x0, sc, Interp::Linear, pos[0], pg[0]);
+			pos_fract(x1, sc, Interp::Linear, pos[1], pg[1]);
+			float wf[4];
+			_Float16 w16[4];
+#pragma unroll
+			for (int cc = 0; cc < 4; ++cc) {
+				float w = 1.0f;
+#pragma unroll
+				for (int d = 0; d < 2; ++d) w *= ((cc >> d) & 1) ? pos[d] : 1.0f - pos[d];
+				wf[cc] = w;
+			}
+			f16_rn_pairs(wf, w16);
+			h2 r = {(_Float16)0.0f, (_Float16)0.0f};
+#pragma unroll
+			for (int cc = 0; cc < 4; ++cc) {
+				const h2 wv = {w16[cc], w16[cc]};
+				r = pk_fma_f16(wv, __builtin_bit_cast(h2, gStage[(4 * k + cc) * 64 + lane]), r);
+			}
+			*(h2*)(slot(0) + tile_ix<SWZ0, RS0>(8 * wave_s + sl, 2 * level)) = r;
+		}
+	};
+	if constexpr (GENC) {
+		for (int l = tid; l < IN / 2; l += NTHR) gLvl[l] = a.glevels[l];
+		__syncthreads();
+		if (tile < n_tiles) {
+			genc_pos_dma(tile);
+			genc_issue();
+		}
+	} else {
+		if (tile < n_tiles) load_x(tile);
+	}
 	__syncthreads();
 
 	for (; tile < n_tiles; tile += gridDim.x) {
 		const uint32_t base = tile * TS;
-		// ---- input tile -> slot 0; prefetch the next tile's rows ----
+		// ---- input tile -> slot 0; prefetch the next tile's rows (GENC: positions) ----
+		if constexpr (GENC) {
+			genc_finish(tile == blockIdx.x);  // the first tile has no stores issued after its gathers
+			if (tile + gridDim.x < n_tiles) genc_pos_dma(tile + gridDim.x);  // gPos read above (data-dependent) first
+		} else {
 #pragma unroll
-		for (int j = 0; j < XPT; ++j) {
-			const int idx = tid + NTHR * j;
-			if (idx < XV) *(h8*)(slot(0) + tile_ix<SWZ0, RS0>(idx / (IN / 8), 8 * (idx % (IN / 8)))) = xr[j];
+			for (int j = 0; j < XPT; ++j) {
+				const int idx = tid + NTHR * j;
+				if (idx < XV) *(h8*)(slot(0) + tile_ix<SWZ0, RS0>(idx / (IN / 8), 8 * (idx % (IN / 8)))) = xr[j];
+			}
+			if (tile + gridDim.x < n_tiles) load_x(tile + gridDim.x);
 		}
-		if (tile + gridDim.x < n_tiles) load_x(tile + gridDim.x);
+
 		// targets / external dL/dy of this wave's output lanes (waves 0 .. NTAU-1: 16-sample column tau = wave)
 		// (the external dL/dy's h4 rides in tg[0..1]: the two cases exclude each other, 2 registers saved)
 		float tg[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -549,6 +687,9 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 		// ---- hidden layers and the first layer, last to first ----
 #pragma unroll
 		for (int m = NH - 1; m >= 0; --m) {
+			if constexpr (GENC) {  // slot NH is dead from here on: the next tile's gathers go there
+				if (m == NH - 2 && tile + gridDim.x < n_tiles) genc_issue();
+			}
 			const _Float16* dsl = dslot(m + 1);  // delta_{m+1} [sample][neuron]
 			const _Float16* am = slot(m);       // a_m [sample][feature]
 			const int rsm = m == 0 ? RS0 : RSW;
@@ -883,6 +1024,8 @@ bool tile_shape_w16(uint32_t IN, uint32_t NH, TileShapeInfo* info);
 bool tile_shape_w32(uint32_t IN, uint32_t NH, TileShapeInfo* info);
 bool tile_shape_w64(uint32_t IN, uint32_t NH, TileShapeInfo* info);
 bool tile_shape_w128(uint32_t IN, uint32_t NH, TileShapeInfo* info);
+// the in-kernel grid encode instantiation (mlp_tile_w128.hip): <128, 32, 4>, ReLU, 64-sample tiles
+bool tile_train_w128_genc(hipStream_t st, HashType h, uint32_t blocks, const TileTrainArgs& a);
 bool tile_train_w16(hipStream_t st, uint32_t IN, uint32_t NH, int act, uint32_t blocks, const TileTrainArgs& a);
 bool tile_train_w32(hipStream_t st, uint32_t IN, uint32_t NH, int act, uint32_t blocks, const TileTrainArgs& a);
 bool tile_train_w64(hipStream_t st, uint32_t IN, uint32_t NH, int act, uint32_t blocks, const TileTrainArgs& a);

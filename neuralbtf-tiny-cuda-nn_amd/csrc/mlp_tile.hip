@@ -89,10 +89,19 @@ uint32_t tile_train_blocks(uint32_t B, uint32_t W, uint32_t IN, uint32_t NH) {
 	return std::max(1u, std::min(cu_count() * per_cu, B / ts));
 }
 
+bool tile_train_genc_ok(uint32_t W, uint32_t IN, uint32_t NH, int act, uint32_t B, HashType h) {
+	static const bool off = [] {
+		const char* e = std::getenv("TCNN_TILE_GENC");
+		return e && std::atoi(e) == 0;
+	}();
+	return !off && W == 128 && IN == 32 && NH == 4 && act == ACT_RELU && B % 64 == 0 && tile_ts64_selected() &&
+	       !tile_ra_selected(W, IN, NH) && (h == HashType::CoherentPrime || h == HashType::Prime);
+}
+
 void launch_mlp_tile_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, int act, int out_act, uint32_t B, uint32_t dims,
                            float loss_scale, uint32_t loss_l2, const void* params16, const void* enc16, const float* target,
                            const void* dout16, void* out16, void* dldenc, int dldenc_pairs, float* wgrad_partial, float* loss_partial,
-                           void* wT) {
+                           void* wT, const TileGridEnc* genc) {
 	TCNN_CHECK(B % 32 == 0, "tile train: batch must be a multiple of 32");
 	TCNN_CHECK(tile_train_supported(W, IN, NH, 16, act), "tile train: unsupported shape");
 	TCNN_CHECK(dout16 || dims <= 16, "tile train: at most 16 outputs");
@@ -123,6 +132,18 @@ void launch_mlp_tile_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH,
 	a.loss_partial = loss_partial;
 	const uint32_t blocks = tile_train_blocks(B, W, IN, NH);
 	bool ok = false;
+	if (genc) {
+		TCNN_CHECK(!enc16 && tile_train_genc_ok(W, IN, NH, act, B, genc->hash), "tile train: in-kernel grid encode not available for this shape");
+		a.gpos = genc->pos;
+		a.gtable = (const uint32_t*)genc->table16;
+		a.glevels = genc->levels;
+		a.ghash = genc->hash_grid;
+		a.ginrange = genc->inrange;
+		ok = tile_train_w128_genc(st, genc->hash, blocks, a);
+		TCNN_CHECK(ok, "tile train: in-kernel grid encode not instantiated");
+		TCNN_HIP_CHECK(hipGetLastError());
+		return;
+	}
 	switch (W) {
 		case 16: ok = tile_train_w16(st, IN, NH, act, blocks, a); break;
 		case 32: ok = tile_train_w32(st, IN, NH, act, blocks, a); break;

@@ -105,6 +105,9 @@ EngineSwitches EngineSwitches::from_env() {
 	s.grid_bin_all = bin && std::string(bin) == "all";
 	if (const char* e = std::getenv("TCNN_GRID_BWD_CHUNKS"))
 		if (std::atoi(e) > 0) s.grid_bwd_chunks = (uint32_t)std::atoi(e);
+	if (const char* e = std::getenv("TCNN_GRID_BWD_RANGES"))
+		if (std::atoi(e) > 0) s.grid_bwd_ranges = (uint32_t)std::atoi(e);
+	s.grid_bwd_feature_split = on("TCNN_GRID_BWD_FEATURE_SPLIT");
 	return s;
 }
 
@@ -223,6 +226,20 @@ GridEncodingHost::GridEncodingHost(uint32_t n_dims, const json& enc) {
 			slices.push_back(GridSlice{l, 0, size, 0, F});
 			continue;
 		}
+		// r06: a hashed power-of-two level is split into entry ranges that hold all F features (its
+		// chunk slabs are then in parameter order, the packed-pair LDS adds of MODE 0 apply for F = 2,
+		// and Adam reads the slabs without the map); other levels split by feature groups
+		uint32_t full = 1;
+		for (uint32_t d = 0; d < desc.n_pos_dims && full <= size; ++d) full *= levels[l].res;
+		const bool hashed_pow2 = gt == GridType::Hash && (size & (size - 1)) == 0 && full > size;
+		if (hashed_pow2 && !sw.grid_bwd_feature_split) {
+			uint32_t R = 1;
+			while ((uint64_t)size * F / R > S) R *= 2;
+			R = std::max(R, std::min(sw.grid_bwd_ranges, size / 256));  // tuning override (TCNN_GRID_BWD_RANGES)
+			const uint32_t len = size / R;
+			for (uint32_t r = 0; r < R; ++r) single.push_back(GridSlice{l, r * len, (r + 1) * len, 0, F});
+			continue;
+		}
 		uint32_t nf = F;
 		while (nf > 1 && ((uint64_t)size * nf > S || F % nf)) --nf;
 		map.nf[l] = nf;
@@ -230,6 +247,8 @@ GridEncodingHost::GridEncodingHost(uint32_t n_dims, const json& enc) {
 	}
 	slices.insert(slices.end(), single.begin(), single.end());
 	map.pbase[first_binned] = n_lds_params;
+	slab_identity = true;
+	for (uint32_t l = 0; l < first_binned; ++l) slab_identity = slab_identity && map.nf[l] == F;
 	d_slab_map.reserve(sizeof(GridSlabMap));
 	TCNN_HIP_CHECK(hipMemcpy(d_slab_map.p, &map, sizeof(GridSlabMap), hipMemcpyHostToDevice));
 
@@ -788,7 +807,19 @@ void NetworkHost::fwd_bwd_tile(hipStream_t st, StepWorkspace& ws, uint32_t B, co
 	const uint32_t W = mlp.width, IN = mlp.n_input, NH = mlp.n_hidden_layers;
 	const uint32_t n_mlp = mlp.n_params();
 	const uint8_t* eparams = (const uint8_t*)params16 + (size_t)n_mlp * 2;
-	if (!enc_aos) {
+	// configs[3]-shaped networks gather the grid encoding inside the tile kernel (no AoS pass)
+	TileGridEnc genc{};
+	const bool in_kernel = !enc_aos && grid && grid->desc.n_pos_dims == 2 && grid->desc.n_features_per_level == 2 &&
+	                       grid->n_to_pad == 0 && grid->desc.interp == Interp::Linear && !grid->opts().active &&
+	                       tile_train_genc_ok(W, IN, NH, mlp.activation, B, grid->desc.hash_type);
+	if (in_kernel) {
+		genc.pos = pos;
+		genc.table16 = eparams;
+		genc.levels = grid->dev_levels();
+		genc.hash = grid->desc.hash_type;
+		genc.hash_grid = grid->hash_grid() ? 1u : 0u;
+		genc.inrange = grid->opts().inrange_index;
+	} else if (!enc_aos) {
 		ws.enc16.reserve((size_t)B * IN * 2);
 		enc->forward_aos(st, B, pos, eparams, ws.enc16.p);
 		enc_aos = ws.enc16.p;
@@ -805,7 +836,7 @@ void NetworkHost::fwd_bwd_tile(hipStream_t st, StepWorkspace& ws, uint32_t B, co
 	launch_mlp_tile_train(st, W, IN, NH, mlp.activation, mlp.output_activation, B, dims, loss_scale, loss_l2, params16, enc_aos, target,
 	                      dout16, out16,
 	                      enc_grad ? ws.delta0.p : nullptr, pairs ? 1 : 0, ws.wgrad_partial.as<float>(), ws.loss_partial.as<float>(),
-	                      wT_bytes ? ws.tile_wT.p : nullptr);
+	                      wT_bytes ? ws.tile_wT.p : nullptr, in_kernel ? &genc : nullptr);
 	ws.n_loss_partials = dout16 ? 0 : nb;
 	const size_t tf = reduce_partials_tmp_floats(nb, n_mlp);
 	if (tf) ws.red_tmp.reserve(tf * 4);

@@ -66,6 +66,8 @@ struct EngineSwitches {
 	bool split_forward = false;     // TCNN_SPLIT_FORWARD: grid forward + k_mlp_infer instead of k_fused_fwd_grid
 	bool grid_bin_all = false;      // TCNN_GRID_BIN=all: bin every grid level that does not fit whole
 	uint32_t grid_bwd_chunks = 0;   // TCNN_GRID_BWD_CHUNKS: grid backward point chunks (0: automatic)
+	uint32_t grid_bwd_ranges = 0;   // TCNN_GRID_BWD_RANGES: at least this many entry ranges per hashed level (tuning)
+	bool grid_bwd_feature_split = false;  // TCNN_GRID_BWD_FEATURE_SPLIT: r05's per-feature items (A/B)
 	static EngineSwitches from_env();
 };
 
@@ -108,7 +110,10 @@ struct GridEncodingHost {
 		o.inrange_index = (inrange_index_ok && desc.interp == Interp::Linear && !sw.no_inrange_index) ? 1u : 0u;
 		return o;
 	}
-	const GridSlabMap* slab_map() const { return d_slab_map.as<GridSlabMap>(); }
+	// the slabs' element order; nullptr when it is the parameter order (every LDS item holds all F
+	// features of its entries: the readers then index the slabs directly, no dependent map load)
+	bool slab_identity = false;
+	const GridSlabMap* slab_map() const { return slab_identity ? nullptr : d_slab_map.as<GridSlabMap>(); }
 	// point chunks of the backward: items x chunks workgroups of 1024 threads (one per CU: 128 KiB
 	// of LDS each) fit the CUs left after `reserved` other workgroups in ONE round, with one chunk of
 	// slack (config_hash, 26 items + 16 tail workgroups: 7 / 8 / 9 / 10 chunks -> 68.8 / 65.8 /

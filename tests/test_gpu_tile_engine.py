@@ -249,3 +249,44 @@ def test_tile_samples_switch_matches_oracle(torch_mod, name, tmp_path):
         assert abs(loss - loss_ref) <= 1e-3 * abs(loss_ref), (loss, loss_ref)
         assert rel_err(g, om.grad32) <= 2e-3
     assert rel_err(g64, g32_ts32) <= 1e-3
+
+
+_GENC_SCRIPT = r"""
+import json, os, sys
+import numpy as np
+import torch
+sys.path[:0] = [sys.argv[1], os.path.join(sys.argv[1], "tests"), os.path.join(sys.argv[1], "neuralbtf-tiny-cuda-nn_amd")]
+from helpers import make_batch, trainer_arrays
+from tinycudann import Trainer
+cfg = json.loads(sys.argv[2])
+B, spread = int(sys.argv[4]), float(sys.argv[5])
+t = Trainer(2, 3, cfg, seed=1337)
+pos, tgt = make_batch(B)
+pos = (pos * (1.0 + 2.0 * spread) - spread).astype(np.float32)
+for k in range(2):
+    t.training_step(torch.from_numpy(pos).cuda(), torch.from_numpy(tgt).cuda(), run_optimizer=(k == 0))
+np.save(sys.argv[3], np.concatenate([trainer_arrays(t)["g32"], trainer_arrays(t)["w32"], [t.loss()]]))
+"""
+
+
+@pytest.mark.parametrize("B,spread", [(512, 0.0), (65536, 0.0), (1024, 0.1), (131072, 0.05)])
+def test_tile_in_kernel_grid_encode_bit_identical(torch_mod, B, spread, tmp_path):
+    """configs[3]'s shape gathers the grid encoding inside the tile kernel (mlp_tile.h GENC, r06): two
+    training steps (Adam, then gradients) are bit-identical to the same steps with the encoding as its
+    own AoS pass (TCNN_TILE_GENC=0, read once per process: a child process). spread > 0 moves positions
+    outside [0, 1] (the general grid index instead of the in-range one)."""
+    import os
+    import subprocess
+    import sys
+    cfg = INFER["configs3_hashgrid_w128_h4"]
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = {}
+    for genc in ("1", "0"):
+        out = tmp_path / f"genc{genc}.npy"
+        env = dict(os.environ, TCNN_TILE_GENC=genc)
+        r = subprocess.run([sys.executable, "-c", _GENC_SCRIPT, repo, json.dumps(cfg), str(out), str(B), str(spread)], env=env,
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs[genc] = np.load(out)
+    assert np.isfinite(outs["1"]).all()
+    np.testing.assert_array_equal(outs["1"], outs["0"])
