@@ -253,7 +253,7 @@ struct TileGridEnc {
 	uint32_t hash_grid, inrange;
 };
 // whether the tile kernel gathers the grid encoding itself for this shape / batch (8-wave W128 kernel,
-// IN 32 = 16 levels x 2 features, 64-sample tiles; TCNN_TILE_GENC=0 turns it off: A/B switch)
+// IN 32 = 16 levels x 2 features, 64-sample tiles; opt-in with TCNN_TILE_GENC=1, measured slower)
 bool tile_train_genc_ok(uint32_t W, uint32_t IN, uint32_t NH, int act, uint32_t B, HashType h);
 void launch_mlp_tile_train(hipStream_t st, uint32_t W, uint32_t IN, uint32_t NH, int act, int out_act, uint32_t B, uint32_t dims,
                            float loss_scale, uint32_t loss_l2, const void* params16, const void* enc16, const float* target,

@@ -90,11 +90,14 @@ uint32_t tile_train_blocks(uint32_t B, uint32_t W, uint32_t IN, uint32_t NH) {
 }
 
 bool tile_train_genc_ok(uint32_t W, uint32_t IN, uint32_t NH, int act, uint32_t B, HashType h) {
-	static const bool off = [] {
+	// opt-in (TCNN_TILE_GENC=1): measured 1.5 % slower than the separate AoS pass for configs[3] (tile kernel
+	// 563 -> 667 us against the pass's 122 us: the combine at each tile's start sits between two workgroup
+	// barriers, on the critical path of a barrier-bound kernel; profiles/r06_configs3_genc_ab.txt)
+	static const bool on = [] {
 		const char* e = std::getenv("TCNN_TILE_GENC");
-		return e && std::atoi(e) == 0;
+		return e && std::atoi(e) != 0;
 	}();
-	return !off && W == 128 && IN == 32 && NH == 4 && act == ACT_RELU && B % 64 == 0 && tile_ts64_selected() &&
+	return on && W == 128 && IN == 32 && NH == 4 && act == ACT_RELU && B % 64 == 0 && tile_ts64_selected() &&
 	       !tile_ra_selected(W, IN, NH) && (h == HashType::CoherentPrime || h == HashType::Prime);
 }
 

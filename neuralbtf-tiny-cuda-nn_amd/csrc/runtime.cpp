@@ -107,7 +107,7 @@ EngineSwitches EngineSwitches::from_env() {
 		if (std::atoi(e) > 0) s.grid_bwd_chunks = (uint32_t)std::atoi(e);
 	if (const char* e = std::getenv("TCNN_GRID_BWD_RANGES"))
 		if (std::atoi(e) > 0) s.grid_bwd_ranges = (uint32_t)std::atoi(e);
-	s.grid_bwd_feature_split = on("TCNN_GRID_BWD_FEATURE_SPLIT");
+	if (const char* e = std::getenv("TCNN_GRID_BWD_PLAN")) s.grid_bwd_plan = std::string(e) == "feature" ? 1 : (std::string(e) == "range" ? 0 : -1);
 	return s;
 }
 
@@ -213,42 +213,54 @@ GridEncodingHost::GridEncodingHost(uint32_t n_dims, const json& enc) {
 		if (need > S) { first_binned = l; break; }
 	}
 	n_lds_params = (first_binned < L ? levels[first_binned].offset : offset) * F;
-	std::vector<GridSlice> single;
+	// Two work plans for the LDS levels (r06), chosen per launch (plan_for). Both: a level whose F
+	// features fit the budget is one item; the others split --
+	//   PLAN_RANGE:   a hashed power-of-two level into entry ranges holding all F features: the chunk
+	//                 slabs are in parameter order (Adam and the slab sums read them without the map),
+	//                 the packed-pair LDS adds of MODE 0 apply for F = 2;
+	//   PLAN_FEATURE: into feature groups (r05): each writes a feature-group-major run, read back
+	//                 through GridSlabMap.
+	// Measured (profiles/r06_grid_plan_ab.json): the range plan takes 2^15 / 2^18-point steps 2 us /
+	// 1.4 % faster (Adam 15.0 -> 13.0 us at 2^18), the feature plan is 25 % faster in configs[3]'s
+	// 2^20-point backward, whose chunks run in several rounds.
 	GridSlabMap map{};
 	map.n_levels = std::max(1u, first_binned);
 	while ((1u << map.log2F) < F) ++map.log2F;
-	for (uint32_t l = 0; l < first_binned; ++l) {
-		const uint32_t size = levels[l].size;
-		map.pbase[l] = levels[l].offset * F;
-		map.size[l] = size;
-		map.nf[l] = F;
-		if ((uint64_t)size * F <= S) {
-			slices.push_back(GridSlice{l, 0, size, 0, F});
-			continue;
+	for (int plan = 0; plan < 2; ++plan) {
+		std::vector<GridSlice>& out = plans[plan].slices;
+		std::vector<GridSlice> single;
+		for (uint32_t l = 0; l < first_binned; ++l) {
+			const uint32_t size = levels[l].size;
+			map.pbase[l] = levels[l].offset * F;
+			map.size[l] = size;
+			if (plan == PLAN_FEATURE) map.nf[l] = F;
+			if ((uint64_t)size * F <= S) {
+				out.push_back(GridSlice{l, 0, size, 0, F});
+				continue;
+			}
+			uint32_t full = 1;
+			for (uint32_t d = 0; d < desc.n_pos_dims && full <= size; ++d) full *= levels[l].res;
+			const bool hashed_pow2 = gt == GridType::Hash && (size & (size - 1)) == 0 && full > size;
+			if (plan == PLAN_RANGE && hashed_pow2) {
+				uint32_t R = 1;
+				while ((uint64_t)size * F / R > S) R *= 2;
+				R = std::max(R, std::min(sw.grid_bwd_ranges, size / 256));  // tuning override (TCNN_GRID_BWD_RANGES)
+				const uint32_t len = size / R;
+				for (uint32_t r = 0; r < R; ++r) single.push_back(GridSlice{l, r * len, (r + 1) * len, 0, F});
+				continue;
+			}
+			uint32_t nf = F;
+			while (nf > 1 && ((uint64_t)size * nf > S || F % nf)) --nf;
+			if (plan == PLAN_FEATURE) map.nf[l] = nf;
+			else plans[plan].identity = false;  // a non-hashed level split by features: the range plan needs the map too
+			for (uint32_t f = 0; f < F; f += nf) single.push_back(GridSlice{l, 0, size, f, nf});
 		}
-		// r06: a hashed power-of-two level is split into entry ranges that hold all F features (its
-		// chunk slabs are then in parameter order, the packed-pair LDS adds of MODE 0 apply for F = 2,
-		// and Adam reads the slabs without the map); other levels split by feature groups
-		uint32_t full = 1;
-		for (uint32_t d = 0; d < desc.n_pos_dims && full <= size; ++d) full *= levels[l].res;
-		const bool hashed_pow2 = gt == GridType::Hash && (size & (size - 1)) == 0 && full > size;
-		if (hashed_pow2 && !sw.grid_bwd_feature_split) {
-			uint32_t R = 1;
-			while ((uint64_t)size * F / R > S) R *= 2;
-			R = std::max(R, std::min(sw.grid_bwd_ranges, size / 256));  // tuning override (TCNN_GRID_BWD_RANGES)
-			const uint32_t len = size / R;
-			for (uint32_t r = 0; r < R; ++r) single.push_back(GridSlice{l, r * len, (r + 1) * len, 0, F});
-			continue;
-		}
-		uint32_t nf = F;
-		while (nf > 1 && ((uint64_t)size * nf > S || F % nf)) --nf;
-		map.nf[l] = nf;
-		for (uint32_t f = 0; f < F; f += nf) single.push_back(GridSlice{l, 0, size, f, nf});
+		out.insert(out.end(), single.begin(), single.end());
 	}
-	slices.insert(slices.end(), single.begin(), single.end());
+	plans[PLAN_FEATURE].identity = true;
+	for (uint32_t l = 0; l < first_binned; ++l) plans[PLAN_FEATURE].identity = plans[PLAN_FEATURE].identity && map.nf[l] == F;
+	if (!plans[PLAN_RANGE].identity) plans[PLAN_RANGE] = plans[PLAN_FEATURE];  // (no hashed split: one plan)
 	map.pbase[first_binned] = n_lds_params;
-	slab_identity = true;
-	for (uint32_t l = 0; l < first_binned; ++l) slab_identity = slab_identity && map.nf[l] == F;
 	d_slab_map.reserve(sizeof(GridSlabMap));
 	TCNN_HIP_CHECK(hipMemcpy(d_slab_map.p, &map, sizeof(GridSlabMap), hipMemcpyHostToDevice));
 
@@ -290,8 +302,10 @@ GridEncodingHost::GridEncodingHost(uint32_t n_dims, const json& enc) {
 	}
 	d_levels.reserve(levels.size() * sizeof(LevelInfo));
 	TCNN_HIP_CHECK(hipMemcpy(d_levels.p, levels.data(), levels.size() * sizeof(LevelInfo), hipMemcpyHostToDevice));
-	d_slices.reserve(slices.size() * sizeof(GridSlice));
-	TCNN_HIP_CHECK(hipMemcpy(d_slices.p, slices.data(), slices.size() * sizeof(GridSlice), hipMemcpyHostToDevice));
+	for (GridPlan& pl : plans) {
+		pl.d_slices.reserve(pl.slices.size() * sizeof(GridSlice));
+		TCNN_HIP_CHECK(hipMemcpy(pl.d_slices.p, pl.slices.data(), pl.slices.size() * sizeof(GridSlice), hipMemcpyHostToDevice));
+	}
 }
 
 void GridEncodingHost::initialize_params(Pcg32& rng, float* out, float scale) const {
@@ -321,10 +335,12 @@ void GridEncodingHost::backward_items(hipStream_t st, GridBwdBufs& w, uint32_t B
                                       int layout, uint32_t dy_stride, const GridBwdEpilogue* ep, uint32_t reserved) const {
 	const uint32_t n_chunks = bwd_chunks(B, reserved);
 	w.n_chunks = n_chunks;
-	if (!slices.empty()) w.partial.reserve((size_t)n_chunks * n_lds_params * 4);
+	w.plan = plan_for(B, reserved);
+	const GridPlan& pl = plans[w.plan];
+	if (!pl.slices.empty()) w.partial.reserve((size_t)n_chunks * n_lds_params * 4);
 	launch_grid_bwd(st, desc.n_pos_dims, desc.n_features_per_level, desc.hash_type, B, pos, pstride, dy, layout, dy_stride,
-	                d_slices.as<GridSlice>(), (uint32_t)slices.size(), n_chunks, w.partial.as<float>(), n_lds_params, dev_levels(),
-	                hash_grid(), desc.interp, ep, opts(), slices.data(), levels.data(), (uint32_t)levels.size());
+	                pl.d_slices.as<GridSlice>(), (uint32_t)pl.slices.size(), n_chunks, w.partial.as<float>(), n_lds_params, dev_levels(),
+	                hash_grid(), desc.interp, ep, opts(), pl.slices.data(), levels.data(), (uint32_t)levels.size());
 }
 
 void GridEncodingHost::backward_bin(hipStream_t st, GridBwdBufs& w, uint32_t B, const float* pos, uint32_t pstride, const void* dy,
@@ -347,8 +363,8 @@ void GridEncodingHost::backward_acc(hipStream_t st, GridBwdBufs& w, uint32_t B, 
 }
 
 void GridEncodingHost::reduce_items(hipStream_t st, GridBwdBufs& w, float* grad32, GradFinalize fin) const {
-	if (slices.empty()) return;
-	launch_grid_slab_reduce(st, w.partial.as<float>(), w.n_chunks, n_lds_params, n_lds_params, grad32, slab_map(), fin);
+	if (plans[0].slices.empty()) return;
+	launch_grid_slab_reduce(st, w.partial.as<float>(), w.n_chunks, n_lds_params, n_lds_params, grad32, slab_map(w.plan), fin);
 }
 
 void GridEncodingHost::backward(hipStream_t st, GridBwdBufs& w, uint32_t B, const float* pos, uint32_t pstride, const void* dy,
@@ -1089,8 +1105,8 @@ void TrainerHost::training_step_overlapped(hipStream_t st, uint32_t B, const flo
 		ag.part = ws.gbw.partial.as<float>();
 		ag.n_parts = ws.gbw.n_chunks;
 		ag.part_stride = g.n_lds_params;
-		ag.part_map = g.slab_map();
-		if (!g.slices.empty())
+		ag.part_map = g.slab_map(ws.gbw.plan);
+		if (!g.plans[0].slices.empty())
 			launch_adam(st, ag, w32.as<float>(), w16.p, g32.as<float>(), g16.p, m1.as<float>(), m2.as<float>(), steps.as<uint32_t>());
 	} else {
 		g.backward_acc(st, ws.gbw, B, ws.dLdenc.p, 0, 0, gsum + n_mlp);

@@ -50,7 +50,22 @@ bool ieq(const std::string& a, const std::string& b);
 struct GridBwdBufs {
 	DevBuf partial, recs, dir, dysum;
 	uint32_t n_chunks = 0;  // LDS items: point chunks = slabs in `partial`
+	int plan = 0;           // the LDS work plan the slabs in `partial` follow (GridEncodingHost::plans)
 };
+// LDS work plan of the grid backward: items, their device copy, and whether the chunk slabs are in
+// parameter order (no GridSlabMap needed to read them)
+struct GridPlan {
+	std::vector<GridSlice> slices;
+	DevBuf d_slices;
+	bool identity = true;
+	GridPlan() = default;
+	GridPlan& operator=(const GridPlan& o) {
+		slices = o.slices;
+		identity = o.identity;
+		return *this;
+	}
+};
+enum : int { PLAN_RANGE = 0, PLAN_FEATURE = 1 };
 
 // ---- multiresolution grid (reference encodings/grid.h:652-1208) ----
 // The engine's A/B and tuning switches (TCNN_* environment variables). Read once when an engine
@@ -67,7 +82,7 @@ struct EngineSwitches {
 	bool grid_bin_all = false;      // TCNN_GRID_BIN=all: bin every grid level that does not fit whole
 	uint32_t grid_bwd_chunks = 0;   // TCNN_GRID_BWD_CHUNKS: grid backward point chunks (0: automatic)
 	uint32_t grid_bwd_ranges = 0;   // TCNN_GRID_BWD_RANGES: at least this many entry ranges per hashed level (tuning)
-	bool grid_bwd_feature_split = false;  // TCNN_GRID_BWD_FEATURE_SPLIT: r05's per-feature items (A/B)
+	int grid_bwd_plan = -1;         // TCNN_GRID_BWD_PLAN=range|feature: force one work plan (A/B; -1: by batch)
 	static EngineSwitches from_env();
 };
 
@@ -83,13 +98,13 @@ struct GridEncodingHost {
 	std::vector<LevelInfo> levels;
 	// backward plan: levels [0, first_binned) are LDS work items (`slices`, per-chunk slabs), levels
 	// [first_binned, L) go through the binned backward (grid_bin.hip), one slot each
-	std::vector<GridSlice> slices;
+	GridPlan plans[2];  // PLAN_RANGE, PLAN_FEATURE (ctor); both have the same items when no level splits
 	uint32_t first_binned = 0;
 	bool inrange_index_ok = false;  // grid_index_inrange is exact for in-range positions (ctor)
 	uint32_t n_lds_params = 0;  // offset[first_binned] * F
 	std::vector<GridBinLevel> bin_levels;
 	uint32_t n_buckets = 0, acc_lds_bytes = 0;
-	DevBuf d_levels, d_slices, d_slab_map, d_bin_levels;
+	DevBuf d_levels, d_slab_map, d_bin_levels;
 
 	GridEncodingHost(uint32_t n_dims_to_encode, const json& enc);
 	uint32_t padded_output_width() const { return n_features + n_to_pad; }
@@ -110,15 +125,22 @@ struct GridEncodingHost {
 		o.inrange_index = (inrange_index_ok && desc.interp == Interp::Linear && !sw.no_inrange_index) ? 1u : 0u;
 		return o;
 	}
-	// the slabs' element order; nullptr when it is the parameter order (every LDS item holds all F
-	// features of its entries: the readers then index the slabs directly, no dependent map load)
-	bool slab_identity = false;
-	const GridSlabMap* slab_map() const { return slab_identity ? nullptr : d_slab_map.as<GridSlabMap>(); }
+	// the slabs' element order under a plan; nullptr when it is the parameter order (every LDS item holds
+	// all F features of its entries: the readers then index the slabs directly, no dependent map load)
+	const GridSlabMap* slab_map(int plan) const { return plans[plan].identity ? nullptr : d_slab_map.as<GridSlabMap>(); }
+	// the plan of a launch: TCNN_GRID_BWD_PLAN=range|feature, else the range plan while the items x
+	// chunks run in one round on the CUs (2^15 .. 2^18 points), the feature plan beyond (configs[3])
+	int plan_for(uint32_t B, uint32_t reserved = 0) const {
+		if (sw.grid_bwd_plan >= 0) return sw.grid_bwd_plan;
+		const uint32_t n_items = (uint32_t)plans[PLAN_RANGE].slices.size();
+		return (uint64_t)bwd_chunks(B, reserved) * n_items + reserved <= 256 ? PLAN_RANGE : PLAN_FEATURE;
+	}
 	// point chunks of the backward: items x chunks workgroups of 1024 threads (one per CU: 128 KiB
 	// of LDS each) fit the CUs left after `reserved` other workgroups in ONE round, with one chunk of
 	// slack (config_hash, 26 items + 16 tail workgroups: 7 / 8 / 9 / 10 chunks -> 68.8 / 65.8 /
 	// 67.5 / 109 us, the last spilling into a second round); >= 4096 points each
 	uint32_t bwd_chunks(uint32_t B, uint32_t reserved = 0) const {
+		const std::vector<GridSlice>& slices = plans[PLAN_RANGE].slices;  // (both plans: the same count for F = 2)
 		if (slices.empty()) return 1;
 		const uint32_t n_cu = 256;
 		const uint32_t fit = (n_cu > reserved ? n_cu - reserved : 1u) / (uint32_t)slices.size();

@@ -271,10 +271,11 @@ np.save(sys.argv[3], np.concatenate([trainer_arrays(t)["g32"], trainer_arrays(t)
 
 @pytest.mark.parametrize("B,spread", [(512, 0.0), (65536, 0.0), (1024, 0.1), (131072, 0.05)])
 def test_tile_in_kernel_grid_encode_bit_identical(torch_mod, B, spread, tmp_path):
-    """configs[3]'s shape gathers the grid encoding inside the tile kernel (mlp_tile.h GENC, r06): two
-    training steps (Adam, then gradients) are bit-identical to the same steps with the encoding as its
-    own AoS pass (TCNN_TILE_GENC=0, read once per process: a child process). spread > 0 moves positions
-    outside [0, 1] (the general grid index instead of the in-range one)."""
+    """configs[3]'s shape can gather the grid encoding inside the tile kernel (mlp_tile.h GENC, r06,
+    opt-in TCNN_TILE_GENC=1): two training steps (Adam, then gradients) are bit-identical to the same
+    steps with the encoding as its own AoS pass (the default; the switch is read once per process, so
+    both run in child processes). spread > 0 moves positions outside [0, 1] (the general grid index
+    instead of the in-range one)."""
     import os
     import subprocess
     import sys
