@@ -1,13 +1,15 @@
-// ref_known_answers.cpp -- TEST INFRASTRUCTURE. Links the reference's own host-compilable sources
-// (dependencies/pcg32/pcg32.h, include/tiny-cuda-nn/common.h, both compiled as they lie under
+// ref_known_answers.cpp -- TEST INFRASTRUCTURE. Includes the reference's own host-compilable headers
+// (dependencies/pcg32/pcg32.h and include/tiny-cuda-nn/common.h, both compiled as they lie under
 // /root/reference with g++, no stand-ins) and prints known answers as JSON. The output is committed
 // as tests/golden/ref_known_answers.json and pins the oracle's RNG / seeding / Xavier / grid-table
-// restatements. Build + run: `make -C oracle ref` (writes only into oracle/_ref/).
+// restatements (pcg32.h) and the engine's batch granularity, default loss scale and enum orders
+// (common.h). Build + run: `make -C oracle ref` (writes only into oracle/_ref/).
 //
 // The strided loop below restates random.h:39-65 (CUDA-only, not compilable here) on top of the
 // reference's pcg32; the level-resolution loop restates grid.h:688-719 with the reference's
 // host-side expression (common_device.h:709-718 is CUDA-only).
 #include <pcg32/pcg32.h>
+#include <tiny-cuda-nn/common.h>
 
 #include <cmath>
 #include <cstdio>
@@ -57,6 +59,19 @@ static std::vector<float> ends(const std::vector<float>& v, size_t k) {
 
 int main() {
 	std::printf("{\n");
+	// common.h:126-170, 229-241: the constants and enum orders the engine's C-ABI and JSON parser mirror
+	std::printf("  \"common_h\": {\"batch_size_granularity\": %u, \"n_threads_linear\": %u, \"default_loss_scale_float\": %.9g, "
+	            "\"activation\": {\"ReLU\": %d, \"LeakyReLU\": %d, \"Exponential\": %d, \"Sine\": %d, \"Sigmoid\": %d, "
+	            "\"Squareplus\": %d, \"Softplus\": %d, \"Tanh\": %d, \"None\": %d}, "
+	            "\"grid_type\": {\"Hash\": %d, \"Dense\": %d, \"Tiled\": %d}, "
+	            "\"hash_type\": {\"Prime\": %d, \"CoherentPrime\": %d, \"ReversedPrime\": %d, \"Rng\": %d}, "
+	            "\"interpolation\": {\"Nearest\": %d, \"Linear\": %d, \"Smoothstep\": %d}},\n",
+	            tcnn::BATCH_SIZE_GRANULARITY, tcnn::N_THREADS_LINEAR, tcnn::default_loss_scale<float>(),
+	            (int)tcnn::Activation::ReLU, (int)tcnn::Activation::LeakyReLU, (int)tcnn::Activation::Exponential, (int)tcnn::Activation::Sine,
+	            (int)tcnn::Activation::Sigmoid, (int)tcnn::Activation::Squareplus, (int)tcnn::Activation::Softplus, (int)tcnn::Activation::Tanh,
+	            (int)tcnn::Activation::None, (int)tcnn::GridType::Hash, (int)tcnn::GridType::Dense, (int)tcnn::GridType::Tiled,
+	            (int)tcnn::HashType::Prime, (int)tcnn::HashType::CoherentPrime, (int)tcnn::HashType::ReversedPrime, (int)tcnn::HashType::Rng,
+	            (int)tcnn::InterpolationType::Nearest, (int)tcnn::InterpolationType::Linear, (int)tcnn::InterpolationType::Smoothstep);
 	// trainer.h:52-55
 	std::seed_seq seq{1337u};
 	std::vector<uint32_t> seeds(2);

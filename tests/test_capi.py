@@ -47,3 +47,22 @@ def test_ctypes_table_covers_header_and_loads():
     assert L.tcnn_default_loss_scale(1) == 128.0 and L.tcnn_default_loss_scale(0) == 1.0
     assert L.tcnn_has_networks() == 1
     assert b"gfx950" in L.tcnn_version()
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="library not built")
+def test_constants_and_enum_orders_match_reference_common_h():
+    """The engine's batch granularity, default loss scales and grid enum orders equal the reference's
+    include/tiny-cuda-nn/common.h as compiled by oracle/_ref (tests/golden/ref_known_answers.json
+    'common_h'): the C-ABI values and the enums of csrc/common.h."""
+    import json
+    ka = json.load(open(os.path.join(REPO, "tests", "golden", "ref_known_answers.json")))["common_h"]
+    from tinycudann import _lib
+    L = _lib.lib()
+    assert L.tcnn_batch_size_granularity() == ka["batch_size_granularity"]
+    assert L.tcnn_default_loss_scale(0) == ka["default_loss_scale_float"]
+    txt = open(os.path.join(REPO, "neuralbtf-tiny-cuda-nn_amd", "csrc", "common.h")).read()
+    for ours, ref in (("GridType", "grid_type"), ("HashType", "hash_type"), ("Interp", "interpolation")):
+        body = re.search(r"enum class %s : uint32_t \{([^}]*)\}" % ours, txt).group(1)
+        vals = {k.strip(): int(v) for k, v in (e.split("=") for e in body.split(",") if "=" in e)}
+        for name, v in vals.items():
+            assert ka[ref][name] == v, (ours, name)
