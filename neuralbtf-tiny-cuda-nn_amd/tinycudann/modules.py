@@ -10,6 +10,8 @@ null-tensor conventions, output slicing -- callers such as NeuralBTF depend on."
 import ctypes
 import gc
 import json
+import os
+import sys
 import warnings
 
 import torch
@@ -74,6 +76,19 @@ def _ptr(t):
 
 
 _GRANULARITY = None
+
+# The C++ autograd node (csrc/torch_ext.cpp, built in-tree next to the engine library): one pybind call per
+# forward and a C++ backward. The Python autograd.Function below is the same node and stays the fallback
+# (TCNN_TORCH_PY=1 selects it: A/B switch).
+_EXT = None
+if not os.environ.get("TCNN_TORCH_PY"):
+    try:
+        _libdir = os.path.dirname(L.LIB_PATH)
+        if _libdir not in sys.path:
+            sys.path.append(_libdir)
+        import _tcnn_torch as _EXT  # noqa: E402
+    except ImportError:
+        _EXT = None
 
 
 def _granularity():
@@ -310,7 +325,10 @@ class Module(torch.nn.Module):
             params = params.to(pdtype)
         if not params.is_contiguous():
             params = params.contiguous()
-        output = _module_function.apply(self.native_tcnn_module, x_padded, params, self.loss_scale)
+        if _EXT is not None:
+            output = _EXT.module_apply(self.native_tcnn_module.h, x_padded, params, float(self.loss_scale))
+        else:
+            output = _module_function.apply(self.native_tcnn_module, x_padded, params, self.loss_scale)
         if batch_size == padded and output.shape[1] == self.n_output_dims:
             return output
         return output[:batch_size, :self.n_output_dims]

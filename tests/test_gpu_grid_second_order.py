@@ -119,5 +119,6 @@ def test_network_double_backward_not_implemented(torch_mod):
     x = torch.rand(256, 2, device="cuda", requires_grad=True)
     y = model(x)
     gx = torch.autograd.grad(y.float().sum(), x, create_graph=True)[0]
-    with pytest.raises(L.TcnnError, match="not implemented"):
+    # a RuntimeError, as the reference's C++ exception through pybind11 (TcnnError, the ctypes path's, is one)
+    with pytest.raises(RuntimeError, match="not implemented"):
         gx.sum().backward()
