@@ -94,14 +94,19 @@ def cpu_baseline(cfg):
     c3, n3, e3 = timed(1 << 18, threads, 8.0, 50)
     c1, n1, e1 = timed(1 << 16, threads, 4.0, 100)
     s1, ns1, es1 = timed(1 << 16, 1, 6.0, 20)
+    # `value`: the faster of all affinity-visible cores and the box's CPU share (on the GPU box the
+    # affinity mask shows the whole host, 256 cores, but the job's CPU share is 16: the 256-thread run
+    # is oversubscribed and slower -- both are reported)
+    best_all = ca >= c3
     return {
-        "value": ca,
+        "value": ca if best_all else c3,
         "unit": "training steps/s (2^18-sample batches)",
-        "cores": all_cores,
+        "cores": all_cores if best_all else threads,
         "kind": "port",
         "cpu": _cpu_model(),
         "sample": f"oracle training steps of config_hash.json on the GPU box's host ({_cpu_model()}): "
-                  f"C3 B=2^18 on all {all_cores} affinity-visible cores: {na} steps in {ea:.1f} s",
+                  f"C3 B=2^18 on {all_cores} affinity-visible cores: {na} steps in {ea:.1f} s ({ca:.3f}/s); "
+                  f"on the {threads}-thread CPU share: {n3} steps in {e3:.1f} s ({c3:.3f}/s)",
         "variants": {
             f"C3_2^18_{all_cores}threads_all_affinity_cores_steps_per_s": ca,
             f"C3_2^18_{threads}threads_steps_per_s": c3,
