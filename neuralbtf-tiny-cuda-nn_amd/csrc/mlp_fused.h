@@ -23,6 +23,7 @@
 
 #include "common.h"
 #include "grid_device.h"
+#include "lds_dma.h"
 #include "kernels.h"
 
 namespace tcnn_amd {

@@ -381,16 +381,9 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 	// staging of the wave's 8 gathers per lane ([k][corner][lane] dwords): slot NH, dead from the start of
 	// the backward's layer NH - 2 to the end of the tile (its delta_NH was last read by layer NH - 1)
 	uint32_t* gStage = (uint32_t*)(smem + L::oA + (NH - 1) * TS * RSW) + wave_s * 8 * 64;
-	// The LDS-DMA loads are inline asm, not __builtin_amdgcn_global_load_lds: the compiler cannot tell the
-	// staging buffers from the rest of the one dynamic LDS array, so with the builtin it put a vmcnt(0)
-	// wait in front of every later LDS read and barrier -- each gather's latency exposed at once, +30 %
-	// kernel time (r06, measured). Opaque to the compiler, the waits are ours: each reader of a buffer
-	// waits for its own wave's DMA (vmcnt) first. (The compiler then counts fewer outstanding vector-memory
-	// operations than there are, which only makes its own vmcnt waits stricter.)
-	auto lds_dma = [](const void* g, const void* l) {
-		const uint32_t la = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)l;
-		asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(g), "s"(la) : "memory", "m0");
-	};
+	// The LDS-DMA loads: lds_dma.h (inline asm; the waits are ours -- each reader of a buffer waits for its
+	// own wave's DMA first)
+	auto lds_dma = [](const void* g, const void* l) { lds_dma_u32(g, l); };
 	auto genc_pos_dma = [&](uint32_t t) {  // positions of tile t's samples 8 wave .. +7 -> gPos (lanes 0..15)
 		if (lane < 16) lds_dma(a.gpos + ((size_t)t * TS + 8 * wave_s) * 2 + lane, gPos);
 	};
@@ -435,15 +428,12 @@ __global__ __launch_bounds__(tile_train_nthr(WR, NH, RA), tile_train_weu(WR, IN,
 		}
 	};
 	auto genc_finish = [&](bool first) {  // gStage + gPos -> this wave's 8 samples x 16 levels of slot 0
-		// this wave's gathers landed: vector-memory operations complete in issue order (gfx9 vmcnt), and
-		// the only ones issued after them are the previous tile's dL/d(encoding) stores (waves < KT0: 2
-		// per 16-sample column as level pairs, 1 as AoS), whose write acknowledgements need not be awaited
-		if (!first && a.dldenc && wave < KT0) {
-			if (a.dldenc_pairs) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NTAU) : "memory");
-			else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NTAU) : "memory");
-		} else {
-			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-		}
+		// this wave's gathers landed. vmcnt(0), not vmcnt(the stores issued after them): loads and stores
+		// share the counter but need not complete in order with each other -- a count that skipped the
+		// previous tile's dL/d(encoding) stores read stale staging (r06, the same wait in the fused
+		// kernel's prefetch experiment: non-deterministic results at 2^18 points)
+		(void)first;
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 		const int sl = lane >> 3, j = lane & 7;
 		const float x0 = gPos[2 * sl], x1 = gPos[2 * sl + 1];
 #pragma unroll

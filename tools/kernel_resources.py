@@ -1,7 +1,7 @@
 """VGPR / AGPR / scratch / LDS of the library's kernels whose mangled name contains a pattern
 (from the code-object metadata notes of the .hip_fatbin bundles).
 
-  python tools/kernel_resources.py k_grid_bwd_lds
+  python tools/kernel_resources.py k_grid_bwd_lds      (TCNN_LIB_PATH: another build of the library)
 """
 import os
 import re
@@ -31,8 +31,8 @@ def code_objects(lib, d):
 
 def main():
     pat = sys.argv[1] if len(sys.argv) > 1 else ""
-    lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "neuralbtf-tiny-cuda-nn_amd", "lib",
-                       "libtcnn_mi355x.so")
+    lib = os.environ.get("TCNN_LIB_PATH") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                          "neuralbtf-tiny-cuda-nn_amd", "lib", "libtcnn_mi355x.so")
     keys = (".vgpr_count", ".agpr_count", ".private_segment_fixed_size", ".group_segment_fixed_size", ".vgpr_spill_count")
     with tempfile.TemporaryDirectory() as d:
         for co in code_objects(lib, d):
