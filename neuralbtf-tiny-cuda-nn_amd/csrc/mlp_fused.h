@@ -378,7 +378,7 @@ struct WgradAcc {
 
 // One 32-sample slice through the network: forward, output + RelativeL2 (relative_l2.h:40-76) or
 // external dL/dy, backward, weight-gradient accumulation, dL/d(encoding) stores.
-// xt: encoded input (B fragments, 16-sample tiles tau = 0, 1); target(tau, o): the target of sample
+// xt: encoded input (B fragments, 16-sample tiles tau = 0, 1); target(tau, r, o): the target of sample
 // base + 16 tau + c, output o (read only for o < dims); after_loss(): hook run once the targets are used.
 // Forward + loss of one 32-sample slice (shared by both fused kernels): post-activations act[j] (B
 // fragments of the next layer), dL/dy G (loss-scaled fp16, or Gext with EXT_DOUT), loss sum.
@@ -458,7 +458,7 @@ __device__ __forceinline__ void slice_fwd_loss(const FusedTrainArgs& a, uint32_t
 				if (o < a.dims) {
 					const float p = (float)y[r];
 					const float pse = a.loss_l2 ? 1.0f : __builtin_fmaf(p, p, 0.01f);  // L2: pdf = 1
-					const float d = p - target(tau, o);
+					const float d = p - target(tau, r, o);
 					loss += d * d / pse / a.n_total;
 					const float gr = 2.0f * d / pse;
 					g[r] = f16_rn(a.loss_scale * gr / a.n_total);
@@ -759,16 +759,13 @@ __global__ __launch_bounds__(64 * FUSED_WAVES, 8 / FUSED_WAVES) void k_fused_tra
 		const uint32_t base = chunk * 32;
 		h4 xt[2][NTI];
 		h4 Gext[2];
-		float tg[2][4];  // this lane's targets (outputs 4q .. 4q+3 < dims), loaded up front so the
-		                 // loss does not wait on them
+		float tg[2];  // this lane's target of output q (register r = 0 of lane group q: out_row), loaded up
+		              // front so the loss does not wait on it; outputs 4r + q (r >= 1, more than 4 outputs)
+		              // are read at the loss (6 registers fewer across the encode and the forward)
 #pragma unroll
 		for (int tau = 0; tau < 2; ++tau) {
 			const uint32_t i = base + 16 * tau + c;
-#pragma unroll
-			for (int r = 0; r < 4; ++r) {
-				const uint32_t o = 4 * r + q;  // out_row: register r of lane group q holds output 4r + q
-				tg[tau][r] = (!EXT_DOUT && o < a.dims) ? a.target[(size_t)i * a.dims + o] : 0.0f;
-			}
+			tg[tau] = (!EXT_DOUT && (uint32_t)q < a.dims) ? a.target[(size_t)i * a.dims + q] : 0.0f;
 		}
 #pragma unroll
 		for (int tau = 0; tau < 2; ++tau) {
@@ -861,7 +858,7 @@ __global__ __launch_bounds__(64 * FUSED_WAVES, 8 / FUSED_WAVES) void k_fused_tra
 			image_pending = false;
 		}
 		if constexpr (PROF) { t1 = stamp(); ph[0] += t1 - t0; t0 = t1; }
-		auto target = [&](int tau, uint32_t o) { return tg[tau][o >> 2]; };
+		auto target = [&](int tau, int r, uint32_t o) { return r == 0 ? tg[tau] : a.target[(size_t)(base + 16 * tau + c) * a.dims + o]; };
 		auto after_loss = [] {};
 		fused_slice<W, IN, NH, ACT, EXT_DOUT, PROF>(a, base, c, q, xt, target, after_loss, Gext, smem + L::oW0,
 		                                            smem + L::oWh, smem + L::oWo, bufA, bufD, acc, ph, t0);
