@@ -231,6 +231,10 @@ def main():
         print(workload_tag(cfg, B))
         return
 
+    if args.graph:
+        # the HIP runtime's graph packet capture costs ~5 us between consecutive replays; without it
+        # replay is within ~1 us of the eager step (profiles/r06_graph_env.txt). Read at HIP init.
+        os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
     import torch
     import torch.distributed as dist
 
