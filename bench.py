@@ -277,8 +277,10 @@ def main():
     exchange = args.exchange if args.allreduce_dtype == "fp32" else "torch"
     if exchange == "peer":
         sharded = world > 1  # the peer exchange is the sharded schedule
+    # a peer wait that cannot complete ends the run after 60 s instead of the library's 300 s default
+    # (a benchmark step is microseconds; nothing rank-0-only runs between its steps)
     dp = DataParallelTrainer(trainer, overlap=not args.no_overlap, allreduce_dtype=args.allreduce_dtype,
-                             shard_optimizer=sharded, exchange=exchange, peer_fallback=True)
+                             shard_optimizer=sharded, exchange=exchange, peer_fallback=True, peer_timeout_s=60.0)
     exchange = dp.exchange  # what actually runs (peer falls back to engine collectively)
     if args.graph:
         trainer.set_graph(True)

@@ -443,10 +443,12 @@ void TrainerHost::dp_peer_attach(const void* blobs) {
 	TCNN_HIP_CHECK(hipMemcpy(pd.ptrs.p, host.data(), host.size() * sizeof(void*), hipMemcpyHostToDevice));
 	pd.host_ptr = host;
 	// probe (collective): every rank's token readable through every mapping, checked once here so a
-	// broken mapping fails the attach (and the caller falls back) instead of a step
+	// broken mapping fails the attach (and the caller falls back) instead of a step. The ranks reach this
+	// point together (their blobs were just all-gathered): its wait -- also the first proof that the
+	// peers' signals arrive through the mappings -- gives up after at most 30 s, not the step timeout
 	hipLaunchKernelGGL(k_peer_token, dim3(1), dim3(64), 0, nullptr, (uint32_t*)pd.x[PB_FLAGS], probe_token(pd.rank));
 	TCNN_HIP_CHECK(hipGetLastError());
-	peer_wait(nullptr, CTR_SYNC, SLOT_PROBE, 1);
+	peer_wait(nullptr, CTR_SYNC, SLOT_PROBE, 1, std::min<long long>(pd.timeout_ticks, (long long)pd.clock_khz * 1000LL * 30));
 	hipLaunchKernelGGL(k_peer_probe, dim3(1), dim3(64), 0, nullptr, pd.flags_arg, N, pd.err_dev, pd.ctr.as<uint32_t>());
 	TCNN_HIP_CHECK(hipGetLastError());
 	TCNN_HIP_CHECK(hipDeviceSynchronize());
@@ -490,9 +492,10 @@ void TrainerHost::dp_peer_loopback(int nranks) {
 
 // wait for every rank's flags[slot] to reach counter c; with signal_bump >= 0 this rank signals first
 // (bumping the counter when 1) in the same one-workgroup launch
-void TrainerHost::peer_wait(hipStream_t st, int c, int slot, int signal_bump) {
+void TrainerHost::peer_wait(hipStream_t st, int c, int slot, int signal_bump, long long timeout_ticks) {
 	PeerDp& pd = *peer;
-	hipLaunchKernelGGL(k_peer_wait, dim3(1), dim3(64), 0, st, pd.flags_arg, pd.nranks, slot, pd.ctr.as<uint32_t>(), c, pd.timeout_ticks,
+	hipLaunchKernelGGL(k_peer_wait, dim3(1), dim3(64), 0, st, pd.flags_arg, pd.nranks, slot, pd.ctr.as<uint32_t>(), c,
+	                   timeout_ticks >= 0 ? timeout_ticks : pd.timeout_ticks,
 	                   pd.err_dev, signal_bump >= 0 ? (uint32_t*)pd.x[PB_FLAGS] : nullptr, signal_bump > 0 ? 1 : 0);
 	TCNN_HIP_CHECK(hipGetLastError());
 }

@@ -456,7 +456,7 @@ struct TrainerHost {
 	int dp_nranks() const { return dp ? dp->nranks : (peer_attached ? peer_nranks : 1); }
 	void dp_peer_gather_state(hipStream_t st);
 	void training_step_peer(hipStream_t st, uint32_t B, const float* input, const float* target);
-	void peer_wait(hipStream_t st, int c, int slot, int signal_bump = -1);
+	void peer_wait(hipStream_t st, int c, int slot, int signal_bump = -1, long long timeout_ticks = -1);  // -1: the peer timeout
 	void peer_gather(hipStream_t st, int what, bool poll);
 	// Adam on parameters [begin, end) only (data-parallel sharded optimizer: each rank updates its
 	// shard of the reduce-scattered gradient, then the fp16 parameters are all-gathered)
