@@ -401,6 +401,87 @@ __device__ __forceinline__ h2 encode_level_f2_pair(const uint32_t* __restrict__ 
 	return res;
 }
 
+// encode_level_f2_pair in two halves (r06, the fused kernel's small-batch schedule): _gather issues the
+// lane's 2 NR corner loads and returns them unconsumed, so a caller can have every level's loads in
+// flight before the first combine; _combine is the rest of encode_level_f2_pair -- the same DPP swap,
+// weights and fp16 FMA chain, bit-identical.
+template <uint32_t NR>
+struct PairGather {
+	uint32_t vA[NR], vB[NR];
+};
+template <uint32_t D, HashType H>
+__device__ __forceinline__ PairGather<(1u << D) / 2> encode_level_f2_pair_gather(const uint32_t* __restrict__ table_u32, const LevelConsts<D>& lc,
+                                                                                 const float* xA, const float* xB, uint32_t par) {
+	constexpr uint32_t NR = (1u << D) / 2;
+	const uint32_t m = lc.m, hmask = lc.hmask, obytes = lc.obytes;
+	PairGather<NR> g;
+#pragma unroll
+	for (uint32_t P = 0; P < 2; ++P) {
+		const float* x = P ? xB : xA;
+		uint32_t pg[D];
+		float pos;
+#pragma unroll
+		for (uint32_t d = 0; d < D; ++d) pos_fract(x[d], lc.scale, Interp::Linear, pos, pg[d]);
+		uint32_t th[D][2], td[D][2];
+		th[0][0] = th[0][1] = (pg[0] + par) * hash_prime<H>(0);
+		td[0][0] = td[0][1] = (pg[0] + par) * lc.sd[0];
+#pragma unroll
+		for (uint32_t d = 1; d < D; ++d) {
+			th[d][0] = pg[d] * hash_prime<H>(d);
+			th[d][1] = th[d][0] + hash_prime<H>(d);
+			td[d][0] = pg[d] * lc.sd[d];
+			td[d][1] = td[d][0] + lc.sd[d];
+		}
+#pragma unroll
+		for (uint32_t r = 0; r < NR; ++r) {
+			uint32_t h = th[0][0], dn = td[0][0];
+#pragma unroll
+			for (uint32_t d = 1; d < D; ++d) {
+				const uint32_t b = (r >> (d - 1)) & 1u;
+				h ^= th[d][b];
+				dn += td[d][b];
+			}
+			const uint32_t dm = __builtin_elementwise_min(dn, dn - lc.size);
+			const uint32_t idx = ((h & hmask) & m) | (dm & ~m);
+			(P ? g.vB : g.vA)[r] = *(const uint32_t*)((const char*)table_u32 + (obytes + (idx << 2)));
+		}
+	}
+	return g;
+}
+template <uint32_t D>
+__device__ __forceinline__ h2 encode_level_f2_pair_combine(const PairGather<(1u << D) / 2>& g, float scale, const float* xA, const float* xB,
+                                                           uint32_t par) {
+	constexpr uint32_t NC = 1u << D, NR = NC / 2;
+	float pos[D];
+	uint32_t pg;
+#pragma unroll
+	for (uint32_t d = 0; d < D; ++d) pos_fract(par ? xB[d] : xA[d], scale, Interp::Linear, pos[d], pg);
+	uint32_t v[NC];
+#pragma unroll
+	for (uint32_t r = 0; r < NR; ++r) {
+		const uint32_t recv = dpp_swap_pair(par ? g.vA[r] : g.vB[r]);  // the partner's corners of my point
+		v[2 * r] = par ? recv : g.vA[r];
+		v[2 * r + 1] = par ? g.vB[r] : recv;
+	}
+	_Float16 w16[NC];
+	float wf[NC];
+#pragma unroll
+	for (uint32_t c = 0; c < NC; ++c) {
+		float w = 1.0f;
+#pragma unroll
+		for (uint32_t d = 0; d < D; ++d) w *= ((c >> d) & 1u) ? pos[d] : 1.0f - pos[d];
+		wf[c] = w;
+	}
+	f16_rn_pairs(wf, w16);
+	h2 res = {(_Float16)0.0f, (_Float16)0.0f};
+#pragma unroll
+	for (uint32_t c = 0; c < NC; ++c) {
+		h2 wv = {w16[c], w16[c]};
+		res = pk_fma_f16(wv, __builtin_bit_cast(h2, v[c]), res);
+	}
+	return res;
+}
+
 template <uint32_t D, HashType H>
 __device__ __forceinline__ h2 encode_level_f2_inrange(const uint32_t* __restrict__ table_u32, const LevelInfo& li, bool hash_grid,
                                                       const float* x) {

@@ -245,6 +245,12 @@ struct FusedLayout {
 #define TCNN_LDS_LEVELS 1
 #endif
 
+// All of a slice's in-range corner loads in flight before the first combine (k_fused_train_grid, 2D
+// inputs); 0 for A/B builds
+#ifndef TCNN_FUSED_EAGER
+#define TCNN_FUSED_EAGER 1
+#endif
+
 #ifndef TCNN_FUSED_WAVES
 #define TCNN_FUSED_WAVES 4
 #endif
@@ -819,6 +825,39 @@ __global__ __launch_bounds__(64 * FUSED_WAVES, 8 / FUSED_WAVES) void k_fused_tra
 					xB[tau][d] = par ? xs[tau][d] : o;
 				}
 #endif
+#if TCNN_PAIR_GATHER
+			// EAGER (r06, 2D inputs): all of the lane's corner loads -- 4 levels x 2 tiles -- in flight before
+			// the first combine (encode_level_f2_pair_gather / _combine), not one level's at a time;
+			// bit-identical. Fused kernel 46.2 -> 44.6 us at 2^18 points, 2^15 -0.4 us
+			// (profiles/r06_fused_eager_ab.txt). 3D inputs keep the per-level schedule (their 8 corners per
+			// level would spill).
+			constexpr bool EAGER = TCNN_FUSED_EAGER && D == 2;
+			if constexpr (EAGER) {
+				PairGather<(1u << D) / 2> g[KI][4][2];
+#pragma unroll
+				for (int s = 0; s < KI; ++s)
+#pragma unroll
+					for (int pp = 0; pp < 4; ++pp) {
+						const int level = 16 * s + 8 * (pp >> 1) + 2 * q + (pp & 1);
+						const LevelConsts<D> lc = level_consts<D>(sLvl[level], hash_grid);
+#pragma unroll
+						for (int tau = 0; tau < 2; ++tau) g[s][pp][tau] = encode_level_f2_pair_gather<D, H>(a.table, lc, xA[tau], xB[tau], par);
+					}
+#pragma unroll
+				for (int s = 0; s < KI; ++s)
+#pragma unroll
+					for (int pp = 0; pp < 4; ++pp) {
+						const float sc = sLvl[16 * s + 8 * (pp >> 1) + 2 * q + (pp & 1)].scale;
+#pragma unroll
+						for (int tau = 0; tau < 2; ++tau) {
+							const h2 e = encode_level_f2_pair_combine<D>(g[s][pp][tau], sc, xA[tau], xB[tau], par);
+							xt[tau][2 * s + (pp >> 1)][2 * (pp & 1) + 0] = e[0];
+							xt[tau][2 * s + (pp >> 1)][2 * (pp & 1) + 1] = e[1];
+						}
+					}
+			} else
+#endif
+			{
 			// level constants once per level, shared by the lane's two samples
 #pragma unroll
 			for (int s = 0; s < KI; ++s)
@@ -837,6 +876,7 @@ __global__ __launch_bounds__(64 * FUSED_WAVES, 8 / FUSED_WAVES) void k_fused_tra
 						xt[tau][2 * s + (pp >> 1)][2 * (pp & 1) + 1] = e[1];
 					}
 				}
+			}
 		} else {
 #pragma unroll
 			for (int tau = 0; tau < 2; ++tau)

@@ -61,7 +61,8 @@ def test_hot_kernels_do_not_spill(kernels):
     hot = {}
     # every fused-kernel instantiation except the loss-driven one reading a kept encoding (ENC_MEM
     # with the loss: only the TCNN_SPLIT_ENCODE experiment launches it) and the phase-timestamp
-    # diagnostic (PROF, tcnn_debug_fused_phase_cycles: its timestamps take registers)
+    # diagnostic (PROF, tcnn_debug_fused_phase_cycles: its timestamps take registers); template
+    # arguments end <..., EXT_DOUT, ENC_MEM, PROF>
     hot.update({k: v for k, v in _pick(kernels, "k_fused_train_grid").items()
                 if not k.endswith(("ELb0ELb1ELb0EEEvNS_14FusedTrainArgsE", "ELb1EEEvNS_14FusedTrainArgsE"))})
     hot.update(_pick(kernels, "k_grid_bwd_ldsILj2ELj2E"))  # D = 2, F = 2 (config_hash), every hash / option variant
